@@ -1,0 +1,606 @@
+/* oracle/lbfgs_oracle.c — TEST INFRASTRUCTURE ONLY (never linked into the product).
+ *
+ * A plain-C restatement of the reference algorithm, used as the checker for the HIP path.
+ * Each function cites the reference lines it restates. Compiled with -ffp-contract=off so that
+ * every a*b+c below is two roundings, exactly like the reference binary (x86-64, no FMA).
+ * The only FMA is the explicit fma() of the canonical dot (ORC_CANON), which mirrors the
+ * device kernels' v_fma_f64 accumulation.
+ */
+#include "lbfgs_oracle.h"
+
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------------------------------
+ * x0: std::mt19937 + std::uniform_real_distribution<double> (libstdc++ 11)
+ * ---------------------------------------------------------------------------------------- */
+typedef struct {
+    uint32_t mt[624];
+    int idx;
+} mt19937;
+
+static void mt_seed(mt19937* s, uint32_t seed) {
+    s->mt[0] = seed;
+    for (int i = 1; i < 624; ++i)
+        s->mt[i] = 1812433253u * (s->mt[i - 1] ^ (s->mt[i - 1] >> 30)) + (uint32_t)i;
+    s->idx = 624;
+}
+
+static uint32_t mt_next(mt19937* s) {
+    if (s->idx >= 624) {
+        for (int i = 0; i < 624; ++i) {
+            uint32_t y = (s->mt[i] & 0x80000000u) | (s->mt[(i + 1) % 624] & 0x7fffffffu);
+            s->mt[i] = s->mt[(i + 397) % 624] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+        }
+        s->idx = 0;
+    }
+    uint32_t y = s->mt[s->idx++];
+    y ^= y >> 11;
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= y >> 18;
+    return y;
+}
+
+void orc_x0_uniform(double* x, int64_t n, uint32_t seed, double lo, double hi) {
+    mt19937* s = (mt19937*)malloc(sizeof(mt19937));
+    mt_seed(s, seed);
+    for (int64_t i = 0; i < n; ++i) {
+        /* generate_canonical<double,53>: sum = g1 + g2 * 2^32 (rounded), / 2^64 */
+        double sum = 0.0, tmp = 1.0;
+        for (int k = 0; k < 2; ++k) {
+            sum += (double)mt_next(s) * tmp;
+            tmp *= 4294967296.0;
+        }
+        double u = sum / tmp;
+        if (u >= 1.0) u = nextafter(1.0, 0.0);
+        x[i] = u * (hi - lo) + lo; /* uniform_real_distribution::operator() */
+    }
+    free(s);
+}
+
+void orc_checksum(const double* x, int64_t n, uint64_t* c1, uint64_t* c2) {
+    uint64_t a = 0, b = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        uint64_t u;
+        memcpy(&u, &x[i], 8);
+        a += u;
+        b += (uint64_t)(i + 1) * u;
+    }
+    *c1 = a;
+    *c2 = b;
+}
+
+/* ------------------------------------------------------------------------------------------
+ * Reductions.
+ * ORC_SEQ  : vector_utils.cpp:32-41 (dotProduct), :78-86 (vectorNorm) — left to right.
+ * ORC_CANON: the device order:
+ *   seg_len L = roundup(ceil(n/8192), 512); segment s = [sL, min((s+1)L, n));
+ *   thread t = 64w + lane (256 per segment); thread t visits, for u = 0.., row r = 4u + w,
+ *   elements sL + 128r + 2 lane + v (v = 0,1) that are < segment end and < limit;
+ *   dot: acc = fma(a, b, acc); sum: acc = acc + t.
+ *   segment partial = balanced pairwise tree over the 256 thread accumulators;
+ *   group g partial  = balanced pairwise tree over segment partials 1024g..1024g+1023
+ *                      (0.0 for segments >= nseg);
+ *   total = ((((((Q0+Q1)+Q2)+Q3)+Q4)+Q5)+Q6)+Q7.
+ * ---------------------------------------------------------------------------------------- */
+#define CANON_SEGS 8192
+#define CANON_GROUPS 8
+#define CANON_SEG_PER_GROUP 1024
+
+void orc_canon_geometry(int64_t n, int64_t* seg_len, int64_t* nseg) {
+    int64_t per = (n + CANON_SEGS - 1) / CANON_SEGS;
+    int64_t L = ((per + 511) / 512) * 512;
+    if (L < 512) L = 512;
+    *seg_len = L;
+    *nseg = (n + L - 1) / L;
+}
+
+static double tree_sum(double* a, int count) { /* balanced, natural order, in place */
+    for (int w = count; w > 1; w >>= 1)
+        for (int j = 0; j < w / 2; ++j) a[j] = a[2 * j] + a[2 * j + 1];
+    return a[0];
+}
+
+/* kind 0: dot of (a,b) with fma; kind 1: sum of a[] */
+static void canon_groups(const double* a, const double* b, int64_t n, int64_t limit, int kind,
+                         double* q8) {
+    int64_t L, nseg;
+    orc_canon_geometry(n, &L, &nseg);
+    double* segp = (double*)calloc(CANON_SEGS, sizeof(double));
+    double acc[256];
+    for (int64_t s = 0; s < nseg; ++s) {
+        int64_t sbeg = s * L;
+        int64_t send = sbeg + L < n ? sbeg + L : n;
+        if (send > limit) send = limit > sbeg ? limit : sbeg;
+        for (int t = 0; t < 256; ++t) {
+            int w = t >> 6, lane = t & 63;
+            double v = 0.0;
+            for (int64_t u = 0; u < L / 512; ++u) {
+                int64_t base = sbeg + 128 * (4 * u + w) + 2 * lane;
+                for (int k = 0; k < 2; ++k) {
+                    int64_t e = base + k;
+                    if (e < send) v = kind == 0 ? fma(a[e], b[e], v) : v + a[e];
+                }
+            }
+            acc[t] = v;
+        }
+        segp[s] = tree_sum(acc, 256);
+    }
+    for (int g = 0; g < CANON_GROUPS; ++g) q8[g] = tree_sum(segp + g * CANON_SEG_PER_GROUP, CANON_SEG_PER_GROUP);
+    free(segp);
+}
+
+static double canon_total(const double* q8) {
+    double t = q8[0];
+    for (int g = 1; g < CANON_GROUPS; ++g) t = t + q8[g];
+    return t;
+}
+
+void orc_canon_dot_groups(const double* a, const double* b, int64_t n, double* q8) {
+    canon_groups(a, b, n, n, 0, q8);
+}
+
+double orc_dot(const double* a, const double* b, int64_t n, int mode) {
+    if (mode == ORC_CANON) {
+        double q8[CANON_GROUPS];
+        canon_groups(a, b, n, n, 0, q8);
+        return canon_total(q8);
+    }
+    double sum = 0.; /* vector_utils.cpp:36-38 */
+    for (int64_t i = 0; i < n; ++i) sum += a[i] * b[i];
+    return sum;
+}
+
+double orc_sum(const double* t, int64_t n, int64_t limit, int mode) {
+    if (mode == ORC_CANON) {
+        double q8[CANON_GROUPS];
+        canon_groups(t, NULL, n, limit, 1, q8);
+        return canon_total(q8);
+    }
+    double sum = 0.0;
+    for (int64_t i = 0; i < limit; ++i) sum += t[i];
+    return sum;
+}
+
+static double orc_norm(const double* v, int64_t n, int mode) {
+    if (mode == ORC_CANON) return sqrt(orc_dot(v, v, n, mode));
+    double r = 0.; /* vector_utils.cpp:80-85 */
+    for (int64_t i = 0; i < n; ++i) r += v[i] * v[i];
+    return sqrt(r);
+}
+
+/* ------------------------------------------------------------------------------------------
+ * Objectives.
+ * ---------------------------------------------------------------------------------------- */
+static double* g_terms = NULL; /* scratch for canonical f */
+static int64_t g_terms_n = 0;
+
+static double* terms_buf(int64_t n) {
+    if (g_terms_n < n) {
+        free(g_terms);
+        g_terms = (double*)malloc(sizeof(double) * (size_t)(n > 0 ? n : 1));
+        g_terms_n = n;
+    }
+    return g_terms;
+}
+
+double orc_f(int obj, const double* x, int64_t n, int mode) {
+    if (mode == ORC_SEQ) {
+        double sum = 0.0;
+        if (obj == ORC_OBJ_ROSENBROCK) { /* benchmark.cpp:58-68 */
+            for (int64_t i = 0; i + 1 < n; i++) {
+                double term1 = x[i + 1] - x[i] * x[i];
+                double term2 = 1 - x[i];
+                sum += 100.0 * term1 * term1 + term2 * term2;
+            }
+        } else if (obj == ORC_OBJ_QUAD_TRIDIAG) { /* benchmark.cpp:17-33 */
+            for (int64_t i = 0; i < n; i++) sum += 1000.0 * x[i] * x[i];
+            for (int64_t i = 0; i < n - 1; i++) sum += (1000.0 / 10.0) * x[i] * x[i + 1];
+        } else { /* main.cpp:7-13 */
+            for (int64_t i = 0; i < n; i++) sum += (x[i] - 1) * (x[i] - 1);
+        }
+        return sum;
+    }
+    /* canonical: the same per-element terms, summed in the device order */
+    double* t = terms_buf(n);
+    int64_t limit = n;
+    if (obj == ORC_OBJ_ROSENBROCK) {
+        for (int64_t i = 0; i + 1 < n; i++) {
+            double term1 = x[i + 1] - x[i] * x[i];
+            double term2 = 1 - x[i];
+            t[i] = 100.0 * term1 * term1 + term2 * term2;
+        }
+        limit = n - 1;
+    } else if (obj == ORC_OBJ_QUAD_TRIDIAG) {
+        for (int64_t i = 0; i < n; i++) {
+            double dterm = 1000.0 * x[i] * x[i];
+            t[i] = (i + 1 < n) ? dterm + 100.0 * x[i] * x[i + 1] : dterm;
+        }
+    } else {
+        for (int64_t i = 0; i < n; i++) t[i] = (x[i] - 1) * (x[i] - 1);
+    }
+    return orc_sum(t, n, limit, ORC_CANON);
+}
+
+void orc_grad(int obj, const double* x, int64_t n, double* g) {
+    if (obj == ORC_OBJ_ROSENBROCK) { /* benchmark.cpp:70-81 */
+        for (int64_t i = 0; i < n; ++i) g[i] = 0.0;
+        for (int64_t i = 0; i + 1 < n; i++) {
+            double term1 = 2.0 * (x[i] - 1);
+            double term2 = x[i + 1] - x[i] * x[i];
+            g[i] += term1 - 400.0 * x[i] * term2;
+            g[i + 1] += 200.0 * term2;
+        }
+    } else if (obj == ORC_OBJ_QUAD_TRIDIAG) { /* benchmark.cpp:37-56 */
+        for (int64_t i = 0; i < n; i++) g[i] = 2.0 * 1000.0 * x[i];
+        for (int64_t i = 0; i < n - 1; i++) {
+            g[i] += (1000.0 / 10.0) * x[i + 1];
+            g[i + 1] += (1000.0 / 10.0) * x[i];
+        }
+    } else { /* main.cpp:15-21 */
+        for (int64_t i = 0; i < n; i++) g[i] = 2.0 * (x[i] - 1);
+    }
+}
+
+/* ------------------------------------------------------------------------------------------
+ * Driver state, call logging.
+ * ---------------------------------------------------------------------------------------- */
+typedef struct {
+    const orc_opts* o;
+    int64_t n;
+    double* flog;
+    int64_t flog_cap, flog_n;
+    uint64_t* glog;
+    int64_t glog_cap, glog_n;
+    int64_t nf, ng;
+    char* msg;
+    int msg_cap, msg_len;
+    double* tmp; /* trial point scratch */
+} ctx_t;
+
+static void say(ctx_t* c, const char* fmt, ...) {
+    char buf[256];
+    va_list ap;
+    va_start(ap, fmt);
+    int k = vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    if (c->o->verbose) fputs(buf, stdout);
+    if (c->msg && k > 0 && c->msg_len + k < c->msg_cap) {
+        memcpy(c->msg + c->msg_len, buf, (size_t)k);
+        c->msg_len += k;
+        c->msg[c->msg_len] = 0;
+    }
+}
+
+static double F(ctx_t* c, const double* x) {
+    double v = orc_f(c->o->obj, x, c->n, c->o->mode);
+    if (c->flog && c->flog_n < c->flog_cap) c->flog[c->flog_n++] = v;
+    c->nf++;
+    return v;
+}
+
+static void G(ctx_t* c, const double* x, double* g) {
+    orc_grad(c->o->obj, x, c->n, g);
+    if (c->glog && c->glog_n + 3 <= c->glog_cap) {
+        uint64_t c1, c2, gb;
+        double gn = orc_norm(g, c->n, ORC_SEQ); /* the trace driver logs the sequential norm */
+        orc_checksum(x, c->n, &c1, &c2);
+        memcpy(&gb, &gn, 8);
+        c->glog[c->glog_n++] = c1;
+        c->glog[c->glog_n++] = c2;
+        c->glog[c->glog_n++] = gb;
+    }
+    c->ng++;
+}
+
+static void trial_point(const double* x, const double* d, double alpha, int64_t n, double* out) {
+    for (int64_t i = 0; i < n; ++i) out[i] = x[i] + alpha * d[i]; /* add(x, scalarProduct(alpha, d)) */
+}
+
+/* ------------------------------------------------------------------------------------------
+ * Line searches — line_search.cpp:8-189.
+ * ---------------------------------------------------------------------------------------- */
+static double cubic_interp(double a0, double a1, double p0, double dp0, double p1, double dp1) {
+    double d1 = dp0 + dp1 - 3 * (p1 - p0) / (a1 - a0); /* line_search.cpp:9-11 */
+    double d2 = copysign(sqrt(d1 * d1 - dp0 * dp1), a1 - a0);
+    return a0 + (a1 - a0) * (dp0 + d2 - d1) / (dp0 - dp1 + 2 * d2);
+}
+
+static double quad_interp(double a0, double a1, double p0, double dp0, double p1) {
+    (void)a1; /* line_search.cpp:14-16 */
+    return a0 - 0.5 * dp0 * a0 * a0 / (p1 - p0 - dp0 * a0);
+}
+
+static double ls_backtracking(ctx_t* c, const double* x, const double* d, const double* g) {
+    const orc_opts* o = c->o; /* line_search.cpp:19-30 */
+    double alpha = o->initial_step;
+    for (;;) {
+        double fx = F(c, x);
+        trial_point(x, d, alpha, c->n, c->tmp);
+        double ft = F(c, c->tmp);
+        double gd = orc_dot(g, d, c->n, o->mode);
+        if (!(fx - ft < o->c1 * alpha * gd)) break;
+        alpha *= o->backtracking_alpha;
+        if (alpha < o->backtracking_tol) break;
+    }
+    return alpha;
+}
+
+static double ls_backtracking_wolfe(ctx_t* c, const double* x, const double* d, const double* g,
+                                    double* gnew) {
+    const orc_opts* o = c->o; /* line_search.cpp:33-55 */
+    double alpha = o->initial_step;
+    for (;;) {
+        trial_point(x, d, alpha, c->n, c->tmp);
+        G(c, c->tmp, gnew);
+        double fn = F(c, c->tmp);
+        double fx = F(c, x);
+        double gd = orc_dot(g, d, c->n, o->mode);
+        if (fn > fx + o->c1 * alpha * gd) {
+            alpha *= o->backtracking_alpha;
+        } else if (orc_dot(gnew, d, c->n, o->mode) < o->c2 * gd) {
+            alpha *= 1.1;
+        } else {
+            break;
+        }
+        if (alpha < o->backtracking_tol) break;
+    }
+    return alpha;
+}
+
+static double ls_interpolation(ctx_t* c, const double* x, const double* d, const double* g) {
+    const orc_opts* o = c->o; /* line_search.cpp:57-121 */
+    const double f_x = F(c, x);
+    const double gd = orc_dot(g, d, c->n, o->mode);
+    double alpha = o->initial_step, alpha_prev = 0.0, f_prev = f_x;
+    int it = 0;
+    while (it++ < 20) {
+        trial_point(x, d, alpha, c->n, c->tmp);
+        double f_new = F(c, c->tmp);
+        if (f_new <= f_x + o->c1 * alpha * gd) return alpha;
+        if (alpha < o->wolfe_interp_min) return o->wolfe_interp_min;
+        if (alpha_prev > 0) {
+            double delta = alpha - alpha_prev;
+            if (fabs(delta) < 1e-10) {
+                alpha *= 0.5;
+            } else {
+                double ga = (f_new - f_x - gd * alpha) / (alpha * alpha);
+                alpha = cubic_interp(alpha_prev, alpha, f_prev, gd, f_new, ga);
+                if (alpha < 0.1 * alpha_prev || alpha > 0.9 * alpha_prev) alpha = alpha_prev * 0.5;
+            }
+        } else {
+            alpha = quad_interp(alpha, 0.0, f_new, gd, f_x);
+            if (alpha < 0.1 * o->initial_step || alpha > 0.9 * o->initial_step)
+                alpha = o->initial_step * 0.5;
+        }
+        alpha_prev = alpha;
+        f_prev = f_new;
+    }
+    return alpha;
+}
+
+static double ls_wolfe(ctx_t* c, const double* x, const double* d, const double* g, double* gnew) {
+    const orc_opts* o = c->o; /* line_search.cpp:125-189 */
+    const double f_x = F(c, x);
+    const double gd = orc_dot(g, d, c->n, o->mode);
+    double alpha = o->initial_step;
+    double alpha_lo = 0.0, alpha_hi = INFINITY, f_lo = f_x, dphi_lo = gd;
+    for (int iter = 0; iter < 20; ++iter) {
+        trial_point(x, d, alpha, c->n, c->tmp);
+        double f_new = F(c, c->tmp);
+        if (f_new > f_x + o->c1 * alpha * gd || (f_new >= f_lo && iter > 0)) {
+            alpha_hi = alpha;
+            alpha = cubic_interp(alpha_lo, alpha_hi, f_lo, dphi_lo, f_new,
+                                 (f_new - f_x - gd * alpha) / (alpha * alpha));
+            continue;
+        }
+        G(c, c->tmp, gnew);
+        double dphi_new = orc_dot(gnew, d, c->n, o->mode);
+        if (fabs(dphi_new) <= -o->c2 * gd) return alpha;
+        if (dphi_new >= 0) {
+            alpha_hi = alpha;
+            alpha = cubic_interp(alpha_lo, alpha_hi, f_lo, dphi_lo, f_new, dphi_new);
+        } else {
+            alpha_lo = alpha;
+            f_lo = f_new;
+            dphi_lo = dphi_new;
+            if (alpha_hi == INFINITY)
+                alpha *= 2;
+            else
+                alpha = cubic_interp(alpha_lo, alpha_hi, f_lo, dphi_lo, f_new, dphi_new);
+        }
+        if (alpha < o->wolfe_interp_min) return o->wolfe_interp_min;
+    }
+    return alpha;
+}
+
+/* ------------------------------------------------------------------------------------------
+ * LBFGS — lbfgs.cpp:17-203.
+ * ---------------------------------------------------------------------------------------- */
+int orc_lbfgs(const orc_opts* o, const double* x0, double* x_out,
+              double* tr_f, double* tr_gnorm, double* tr_alpha, uint64_t* tr_c1, uint64_t* tr_c2,
+              int64_t* tr_nf, int trace_cap,
+              double* flog, int64_t flog_cap, int64_t* flog_n,
+              uint64_t* glog, int64_t glog_cap, int64_t* glog_n,
+              char* msg, int msg_cap, orc_result* res) {
+    const int64_t n = o->n;
+    const int m = o->m;
+    if (n < 1 || m < 1 || o->ls < 0 || o->ls > 3) return -1;
+    ctx_t C;
+    memset(&C, 0, sizeof C);
+    C.o = o;
+    C.n = n;
+    C.flog = flog;
+    C.flog_cap = flog_cap;
+    C.glog = glog;
+    C.glog_cap = glog_cap;
+    C.msg = msg;
+    C.msg_cap = msg_cap;
+    if (msg && msg_cap > 0) msg[0] = 0;
+
+    size_t vb = sizeof(double) * (size_t)n;
+    double* x = (double*)malloc(vb);
+    double* g = (double*)malloc(vb);
+    double* d = (double*)malloc(vb);
+    double* q = (double*)malloc(vb);
+    double* r = (double*)malloc(vb);
+    double* xn = (double*)malloc(vb);
+    double* gn = (double*)malloc(vb);
+    C.tmp = (double*)malloc(vb);
+    double* alpha_i = (double*)malloc(sizeof(double) * (size_t)m);
+    /* history deque: hs[0] oldest .. hs[h-1] newest; storage pool of m+1 pairs */
+    double** hs = (double**)malloc(sizeof(double*) * (size_t)(m + 1));
+    double** hy = (double**)malloc(sizeof(double*) * (size_t)(m + 1));
+    for (int i = 0; i <= m; ++i) {
+        hs[i] = (double*)malloc(vb);
+        hy[i] = (double*)malloc(vb);
+    }
+    int h = 0;
+
+    memcpy(x, x0, vb);
+    double f_current = F(&C, x0); /* :29 */
+    G(&C, x, g);                  /* :30 */
+    int status = ORC_MAX_ITER, ntr = 0, k;
+    const int mode = o->mode;
+
+    for (k = 0; k < o->maxit; ++k) {
+        double gnorm = orc_norm(g, n, mode);
+        if (ntr < trace_cap) {
+            tr_f[ntr] = f_current;
+            tr_gnorm[ntr] = gnorm;
+            tr_alpha[ntr] = NAN;
+            orc_checksum(x, n, &tr_c1[ntr], &tr_c2[ntr]);
+            tr_nf[ntr] = C.nf;
+        }
+        if (o->verbose) printf("Iteration %d, f = %g, |grad| = %g\n", k, f_current, gnorm); /* :76-78 */
+        if (gnorm < o->tol) {                                                               /* :80 */
+            say(&C, "Converged!\n");
+            status = ORC_CONVERGED;
+            ntr++;
+            goto done;
+        }
+        if (k == 0 || h == 0) { /* :87-91 */
+            for (int64_t i = 0; i < n; ++i) d[i] = -g[i];
+        } else { /* two-loop :94-143 */
+            memcpy(q, g, vb);
+            for (int i = h - 1; i >= 0; --i) {
+                double rho = 1.0 / orc_dot(hy[i], hs[i], n, mode);
+                if (!isfinite(rho)) {
+                    say(&C, "Warning: Invalid rho at iteration %d\n", k);
+                    for (int64_t j = 0; j < n; ++j) d[j] = -g[j];
+                    goto perform_line_search;
+                }
+                alpha_i[i] = rho * orc_dot(hs[i], q, n, mode);
+                for (int64_t j = 0; j < n; ++j) q[j] -= alpha_i[i] * hy[i][j];
+            }
+            {
+                double gamma = orc_dot(hs[h - 1], hy[h - 1], n, mode) / orc_dot(hy[h - 1], hy[h - 1], n, mode);
+                if (gamma <= 0 || !isfinite(gamma)) {
+                    say(&C, "Warning: Invalid gamma at iteration %d\n", k);
+                    for (int64_t j = 0; j < n; ++j) d[j] = -g[j];
+                    goto perform_line_search;
+                }
+                for (int64_t i = 0; i < n; ++i) r[i] = q[i] * gamma;
+            }
+            for (int i = 0; i < h; ++i) {
+                double rho = 1.0 / orc_dot(hy[i], hs[i], n, mode);
+                double beta = rho * orc_dot(hy[i], r, n, mode);
+                for (int64_t j = 0; j < n; ++j) r[j] += hs[i][j] * (alpha_i[i] - beta);
+            }
+            for (int64_t j = 0; j < n; ++j) d[j] = -r[j];
+        }
+    perform_line_search:; /* :146-156 */
+        double gd = orc_dot(g, d, n, mode);
+        if (gd >= 0) {
+            say(&C, "Warning: Not a descent direction, using gradient\n");
+            for (int64_t j = 0; j < n; ++j) d[j] = -g[j];
+            gd = orc_dot(g, d, n, mode);
+        }
+        (void)gd;
+        double alpha;
+        switch (o->ls) {
+            case ORC_LS_BACKTRACKING: alpha = ls_backtracking(&C, x, d, g); break;
+            case ORC_LS_INTERPOLATION: alpha = ls_interpolation(&C, x, d, g); break;
+            case ORC_LS_WOLFE: alpha = ls_wolfe(&C, x, d, g, gn); break;
+            default: alpha = ls_backtracking_wolfe(&C, x, d, g, gn); break;
+        }
+        if (ntr < trace_cap) tr_alpha[ntr] = alpha;
+        ntr++;
+        trial_point(x, d, alpha, n, xn); /* :159 */
+        f_current = F(&C, xn);           /* :160-161 */
+        if (alpha < 1e-10) {             /* :164-168 */
+            say(&C, "Warning: Line search failed at iteration %d\n", k);
+            status = ORC_LS_FAILED;
+            goto done;
+        }
+        G(&C, xn, gn); /* :171 */
+        {
+            /* :174-195 — the new pair is written to the spare pool slot hs[h] (h <= m) */
+            double* sk = hs[h];
+            double* yk = hy[h];
+            for (int64_t i = 0; i < n; ++i) {
+                sk[i] = xn[i] - x[i];
+                yk[i] = gn[i] - g[i];
+            }
+            double sy = orc_dot(sk, yk, n, mode);
+            if (sy > 0) {
+                if (h >= m) { /* pop_front: rotate the oldest into the spare slot */
+                    double* s0 = hs[0];
+                    double* y0 = hy[0];
+                    for (int i = 0; i < m; ++i) {
+                        hs[i] = hs[i + 1];
+                        hy[i] = hy[i + 1];
+                    }
+                    hs[m] = s0;
+                    hy[m] = y0;
+                } else {
+                    h++;
+                }
+            } else {
+                say(&C, "Warning: Skipping update, sy = %g\n", sy);
+            }
+        }
+        { /* :197-198 */
+            double* t = x;
+            x = xn;
+            xn = t;
+            t = g;
+            g = gn;
+            gn = t;
+        }
+    }
+    /* maximum iterations: final state entry */
+    if (ntr < trace_cap) {
+        tr_f[ntr] = f_current;
+        tr_gnorm[ntr] = orc_norm(g, n, mode);
+        tr_alpha[ntr] = NAN;
+        orc_checksum(x, n, &tr_c1[ntr], &tr_c2[ntr]);
+        tr_nf[ntr] = C.nf;
+    }
+    ntr++;
+    say(&C, "Maximum iterations reached\n");
+
+done:
+    if (x_out) memcpy(x_out, x, vb);
+    if (res) {
+        res->iters = k;
+        res->status = status;
+        res->ntrace = ntr;
+        res->nf = C.nf;
+        res->ng = C.ng;
+    }
+    if (flog_n) *flog_n = C.flog_n;
+    if (glog_n) *glog_n = C.glog_n;
+    free(x); free(g); free(d); free(q); free(r); free(xn); free(gn); free(C.tmp); free(alpha_i);
+    for (int i = 0; i <= m; ++i) {
+        free(hs[i]);
+        free(hy[i]);
+    }
+    free(hs);
+    free(hy);
+    return 0;
+}

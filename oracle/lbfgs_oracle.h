@@ -1,0 +1,72 @@
+/* oracle/lbfgs_oracle.h — TEST INFRASTRUCTURE ONLY.
+ *
+ * Plain-C restatement of the reference sequential L-BFGS
+ * (/root/reference/sequential-implementation/lbfgs.cpp:17-203, line_search.cpp:8-189,
+ *  vector_utils.cpp:32-86, benchmark.cpp:16-81, main.cpp:7-21) used as the CHECKER for the
+ * HIP product. Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load
+ * it. Parity of this restatement is pinned against traces of the reference itself
+ * (oracle/_ref, tests/golden/), see tests/test_oracle_golden.py.
+ *
+ * Two reduction orders:
+ *   ORC_SEQ   : strictly left-to-right sums, exactly as the reference (bit-exact vs reference)
+ *   ORC_CANON : the product's canonical device tree order, so that the HIP
+ *               path can be checked bit-exactly over a whole run.
+ */
+#ifndef LBFGS_ORACLE_H
+#define LBFGS_ORACLE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { ORC_OBJ_ROSENBROCK = 0, ORC_OBJ_QUAD_TRIDIAG = 1, ORC_OBJ_QUAD_SEPARABLE = 2 };
+enum { ORC_LS_BACKTRACKING = 0, ORC_LS_INTERPOLATION = 1, ORC_LS_WOLFE = 2, ORC_LS_BACKTRACKING_WOLFE = 3 };
+enum { ORC_SEQ = 0, ORC_CANON = 1 };
+enum { ORC_CONVERGED = 0, ORC_MAX_ITER = 1, ORC_LS_FAILED = 2 };
+
+typedef struct {
+    int obj, ls, mode, verbose;
+    int64_t n;
+    int m, maxit;
+    double tol;
+    /* config.h:5-17 */
+    double c1, c2, initial_step, backtracking_alpha, backtracking_tol, wolfe_interp_min;
+} orc_opts;
+
+typedef struct {
+    int iters, status, ntrace;
+    int64_t nf, ng;
+} orc_result;
+
+/* x0 exactly as std::mt19937(seed) + std::uniform_real_distribution<double>(lo, hi)
+ * (libstdc++ generate_canonical<double,53>, two 32-bit draws per value; main.cpp:36-43). */
+void orc_x0_uniform(double* x, int64_t n, uint32_t seed, double lo, double hi);
+
+/* Reductions. */
+double orc_dot(const double* a, const double* b, int64_t n, int mode);
+double orc_sum(const double* t, int64_t n, int64_t limit, int mode); /* terms t[e], e < limit */
+void orc_canon_geometry(int64_t n, int64_t* seg_len, int64_t* nseg);
+/* group partials Q_0..Q_7 of the canonical order (total = sequential sum of the 8). */
+void orc_canon_dot_groups(const double* a, const double* b, int64_t n, double* q8);
+
+/* Objectives (benchmark.cpp:16-81, main.cpp:7-21). */
+double orc_f(int obj, const double* x, int64_t n, int mode);
+void orc_grad(int obj, const double* x, int64_t n, double* g);
+
+/* Full L-BFGS run. Trace entry k = state at the top of iteration k (plus the final state);
+ * tr_alpha[k] = step taken in iteration k (NaN for the last entry). flog/glog record every
+ * objective call in the reference's call order (reference-faithful evaluation). */
+int orc_lbfgs(const orc_opts* o, const double* x0, double* x_out,
+              double* tr_f, double* tr_gnorm, double* tr_alpha, uint64_t* tr_c1, uint64_t* tr_c2,
+              int64_t* tr_nf, int trace_cap,
+              double* flog, int64_t flog_cap, int64_t* flog_n,
+              uint64_t* glog, int64_t glog_cap, int64_t* glog_n,
+              char* msg, int msg_cap, orc_result* res);
+
+void orc_checksum(const double* x, int64_t n, uint64_t* c1, uint64_t* c2);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,162 @@
+"""ctypes binding of oracle/_build/liboracle.so — TEST INFRASTRUCTURE ONLY.
+
+The oracle is the checker (a plain-C restatement of the reference, pinned against the
+reference's own traces in tests/golden/). Product code must never import this module.
+"""
+import ctypes as C
+import json
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+ORACLE_SO = os.path.join(ORACLE_DIR, "_build", "liboracle.so")
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+OBJ = {"rosenbrock": 0, "quad_tridiag": 1, "quad_sep": 2}
+LS = {"backtracking": 0, "interpolation": 1, "wolfe": 2, "backtracking_wolfe": 3}
+SEQ, CANON = 0, 1
+STATUS = {0: "converged", 1: "max_iter", 2: "ls_failed"}
+
+# sequential-implementation/config.h:5-17
+CONFIG_H = dict(c1=1e-4, c2=0.9, initial_step=1.0, backtracking_alpha=0.5,
+                backtracking_tol=1e-8, wolfe_interp_min=1e-10)
+
+
+class Opts(C.Structure):
+    _fields_ = [("obj", C.c_int), ("ls", C.c_int), ("mode", C.c_int), ("verbose", C.c_int),
+                ("n", C.c_int64), ("m", C.c_int), ("maxit", C.c_int), ("tol", C.c_double),
+                ("c1", C.c_double), ("c2", C.c_double), ("initial_step", C.c_double),
+                ("backtracking_alpha", C.c_double), ("backtracking_tol", C.c_double),
+                ("wolfe_interp_min", C.c_double)]
+
+
+class Result(C.Structure):
+    _fields_ = [("iters", C.c_int), ("status", C.c_int), ("ntrace", C.c_int),
+                ("nf", C.c_int64), ("ng", C.c_int64)]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(ORACLE_SO):
+            subprocess.run(["make", "-C", ORACLE_DIR, "oracle"], check=True,
+                           capture_output=True)
+        L = C.CDLL(ORACLE_SO)
+        dp = np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")
+        up = np.ctypeslib.ndpointer(dtype=np.uint64, flags="C_CONTIGUOUS")
+        ip = np.ctypeslib.ndpointer(dtype=np.int64, flags="C_CONTIGUOUS")
+        L.orc_x0_uniform.argtypes = [dp, C.c_int64, C.c_uint32, C.c_double, C.c_double]
+        L.orc_dot.argtypes = [dp, dp, C.c_int64, C.c_int]
+        L.orc_dot.restype = C.c_double
+        L.orc_sum.argtypes = [dp, C.c_int64, C.c_int64, C.c_int]
+        L.orc_sum.restype = C.c_double
+        L.orc_canon_dot_groups.argtypes = [dp, dp, C.c_int64, dp]
+        L.orc_canon_geometry.argtypes = [C.c_int64, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
+        L.orc_f.argtypes = [C.c_int, dp, C.c_int64, C.c_int]
+        L.orc_f.restype = C.c_double
+        L.orc_grad.argtypes = [C.c_int, dp, C.c_int64, dp]
+        L.orc_checksum.argtypes = [dp, C.c_int64, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+        L.orc_lbfgs.argtypes = [C.POINTER(Opts), dp, dp, dp, dp, dp, up, up, ip, C.c_int,
+                                dp, C.c_int64, C.POINTER(C.c_int64),
+                                up, C.c_int64, C.POINTER(C.c_int64),
+                                C.c_char_p, C.c_int, C.POINTER(Result)]
+        L.orc_lbfgs.restype = C.c_int
+        _lib = L
+    return _lib
+
+
+def x0_uniform(n, seed, lo, hi):
+    x = np.empty(n, dtype=np.float64)
+    lib().orc_x0_uniform(x, n, seed, lo, hi)
+    return x
+
+
+def dot(a, b, mode=CANON):
+    return lib().orc_dot(np.ascontiguousarray(a, np.float64), np.ascontiguousarray(b, np.float64),
+                         len(a), mode)
+
+
+def canon_groups(a, b):
+    q = np.zeros(8)
+    lib().orc_canon_dot_groups(np.ascontiguousarray(a, np.float64),
+                               np.ascontiguousarray(b, np.float64), len(a), q)
+    return q
+
+
+def geometry(n):
+    L, ns = C.c_int64(), C.c_int64()
+    lib().orc_canon_geometry(n, C.byref(L), C.byref(ns))
+    return L.value, ns.value
+
+
+def f(obj, x, mode=CANON):
+    return lib().orc_f(OBJ[obj], np.ascontiguousarray(x, np.float64), len(x), mode)
+
+
+def grad(obj, x):
+    g = np.empty(len(x))
+    lib().orc_grad(OBJ[obj], np.ascontiguousarray(x, np.float64), len(x), g)
+    return g
+
+
+def checksum(x):
+    a, b = C.c_uint64(), C.c_uint64()
+    lib().orc_checksum(np.ascontiguousarray(x, np.float64), len(x), C.byref(a), C.byref(b))
+    return a.value, b.value
+
+
+def np_checksum(x):
+    u = np.ascontiguousarray(x, np.float64).view(np.uint64)
+    idx = np.arange(1, len(u) + 1, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        return int(u.sum(dtype=np.uint64)), int((u * idx).sum(dtype=np.uint64))
+
+
+def lbfgs(obj, x0, ls, m, maxit, tol, mode=CANON, consts=None, log_calls=False, verbose=False):
+    """Run the oracle; returns a dict with x, trace arrays, call logs and messages."""
+    x0 = np.ascontiguousarray(x0, np.float64)
+    n = len(x0)
+    k = dict(CONFIG_H)
+    if consts:
+        k.update(consts)
+    o = Opts(obj=OBJ[obj], ls=LS[ls], mode=mode, verbose=int(verbose), n=n, m=m, maxit=maxit,
+             tol=tol, **k)
+    cap = maxit + 2
+    x = np.empty(n)
+    trf, trg, tra = np.empty(cap), np.empty(cap), np.empty(cap)
+    tc1, tc2 = np.empty(cap, np.uint64), np.empty(cap, np.uint64)
+    tnf = np.empty(cap, np.int64)
+    fcap = (60 * maxit + 100) if log_calls else 0
+    flog = np.empty(max(fcap, 1))
+    gcap = 3 * (30 * maxit + 10) if log_calls else 0
+    glog = np.empty(max(gcap, 1), np.uint64)
+    fn, gn = C.c_int64(0), C.c_int64(0)
+    msg = C.create_string_buffer(1 << 20)
+    res = Result()
+    rc = lib().orc_lbfgs(C.byref(o), x0, x, trf, trg, tra, tc1, tc2, tnf, cap, flog, fcap,
+                         C.byref(fn), glog, gcap, C.byref(gn), msg, len(msg), C.byref(res))
+    assert rc == 0
+    nt = res.ntrace
+    return dict(x=x, f=trf[:nt].copy(), gnorm=trg[:nt].copy(), alpha=tra[:nt].copy(),
+                c1=tc1[:nt].copy(), c2=tc2[:nt].copy(), nf=tnf[:nt].copy(),
+                iters=res.iters, status=STATUS[res.status], nf_total=res.nf, ng_total=res.ng,
+                flog=flog[:fn.value].copy(), glog=glog[:gn.value].reshape(-1, 3).copy(),
+                messages=msg.value.decode())
+
+
+def load_golden(name):
+    with open(os.path.join(GOLDEN, name + ".json")) as fp:
+        meta = json.load(fp)
+    arr = np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
+    return meta, {k: arr[k] for k in arr.files}
+
+
+def golden_cases():
+    return sorted(f[:-5] for f in os.listdir(GOLDEN)
+                  if f.endswith(".json") and not f.startswith("kat_"))
