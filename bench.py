@@ -1,0 +1,223 @@
+#!/usr/bin/env python3
+"""Headline benchmark: L-BFGS iterations/s and achieved HBM GB/s on n = 1e8 Rosenbrock, m = 10,
+backtracking line search, fp64 (BASELINE.json metric; configs[2] on one GPU, the 1->8 GPU
+series sharding the same n across ranks).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+A step is one L-BFGS iteration of the whole n-vector problem (two-loop recursion, line search,
+commit). Warm-up iterations fill the m-pair history, so every timed step uses h = m pairs.
+All vectors are resident in HBM before timing starts. One process per GPU; the solver's data
+path exchanges group partials with RCCL all-gathers inside liblbfgs_hip.so; torch.distributed
+(gloo) is only used for the rendezvous (unique id), barriers and the max-over-ranks time.
+
+Prints ONE JSON line (rank 0).
+"""
+import argparse
+import json
+import os
+import platform
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "cuda-lbfgs_amd"))
+import lbfgs_amd as L  # noqa: E402  (load the HIP library before anything else touches HIP)
+
+import numpy as np  # noqa: E402
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=100)
+    p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--n", type=float, default=1e8)
+    p.add_argument("--m", type=int, default=10)
+    p.add_argument("--objective", default="rosenbrock")
+    p.add_argument("--line-search", default="backtracking")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-n", type=float, default=1e7, help="CPU baseline sample size")
+    p.add_argument("--no-prof", action="store_true", help="no per-kernel HIP events")
+    return p.parse_args()
+
+
+class Dist:
+    def __init__(self, world):
+        self.world = world
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        self.dist = None
+        if world > 1:
+            import torch.distributed as dist
+
+            dist.init_process_group("gloo", rank=self.rank, world_size=world)
+            self.dist = dist
+
+    def broadcast_bytes(self, b):
+        if not self.dist:
+            return b
+        obj = [b]
+        self.dist.broadcast_object_list(obj, src=0)
+        return obj[0]
+
+    def barrier(self):
+        if self.dist:
+            self.dist.barrier()
+
+    def allreduce(self, v, op="max"):
+        if not self.dist:
+            return v
+        import torch
+
+        t = torch.tensor([v], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX if op == "max" else self.dist.ReduceOp.SUM)
+        return float(t.item())
+
+    def close(self):
+        if self.dist:
+            self.dist.destroy_process_group()
+
+
+def cpu_baseline(n_sample, m, steps_for_h):
+    """The reference itself (oracle/_ref/ref_lbfgs: the reference's sequential sources compiled
+    unmodified, -O2 -ffp-contract=off), single core, Rosenbrock n_sample, m, backtracking.
+    Per-iteration times come from the trace driver's grad() timestamps; the steady state uses
+    the iterations with h = m pairs, scaled linearly in n to the benchmark's n."""
+    ref = os.path.join(ROOT, "oracle", "_ref", "ref_lbfgs")
+    n_sample = int(n_sample)
+    iters = m + 2
+    if not os.path.exists(ref):
+        return None
+    with tempfile.TemporaryDirectory() as tmp:
+        pre = os.path.join(tmp, "cpu")
+        cmd = [ref, "rosenbrock", str(n_sample), str(m), "backtracking", str(iters), "1e-5", "42",
+               "-2", "2", pre, "0"]
+        try:
+            cmd = ["taskset", "-c", "0"] + cmd
+            subprocess.run(cmd, check=True, capture_output=True, timeout=600)
+        except (FileNotFoundError, subprocess.CalledProcessError):
+            subprocess.run(cmd[3:], check=True, capture_output=True, timeout=600)
+        g = np.fromfile(pre + ".g.bin", dtype=np.uint64).reshape(-1, 5)
+        t = g[:, 3].copy().view(np.float64)
+    dt = np.diff(t)  # dt[k] = time of iteration k (grad call k -> k+1)
+    steady = dt[m:]  # iterations with h = m
+    return dict(per_iter_s=float(np.mean(steady)), iters_timed=len(steady), total_s=float(t[-1]))
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def main():
+    a = parse()
+    n = int(a.n)
+    D = Dist(a.gpus)
+    world, rank = a.gpus, D.rank
+    uid = D.broadcast_bytes(L.unique_id() if (world > 1 and rank == 0) else None) if world > 1 else None
+
+    x0 = L.x0_uniform(n, 42, -2.0, 2.0)
+    ctx = L.Context(n, a.m, device=D.local_rank, rank=rank, world=world, uid=uid)
+    ctx.init(a.objective, x0, a.line_search, tolerance=1e-5)
+    del x0
+    ctx.step(a.warmup)
+    ctx.sync()
+
+    if not a.no_prof:
+        ctx.prof_reset()
+        ctx.prof_enable(True)
+    D.barrier()
+    ctx.sync()
+    t0 = time.perf_counter()
+    res = ctx.step(a.steps)
+    ctx.sync()
+    t_local = time.perf_counter() - t0
+    D.barrier()
+    ctx.prof_enable(False)
+    T = D.allreduce(t_local, "max")
+    bytes_all = D.allreduce(res["bytes"], "sum")
+
+    prof = {}
+    if not a.no_prof:
+        for kname in L.KERNELS:
+            p = ctx.prof_get(kname)
+            if p["launches"]:
+                prof[kname] = p
+    done_steps = a.steps
+    if res["status"] != "running":
+        done_steps = max(res["iterations"] - a.warmup, 1)
+
+    out = None
+    if rank == 0:
+        value = done_steps / T
+        roof = None
+        if prof:
+            dom = max(prof, key=lambda k: prof[k]["ms"])
+            p = prof[dom]
+            avg_s = p["ms"] / p["launches"] / 1e3
+            per_launch = p["bytes"] / p["launches"]  # this rank's algorithmic bytes per launch
+            achieved = per_launch / avg_s / 1e9
+            roof = dict(bound="hbm", kernel=dom, achieved=round(achieved, 1), peak=HBM_PEAK_GBPS,
+                        unit="GB/s", frac=round(achieved / HBM_PEAK_GBPS, 4), traffic=None,
+                        bytes_per_launch=per_launch, avg_launch_us=round(avg_s * 1e6, 2),
+                        launches=p["launches"],
+                        kernel_share={k: round(v["ms"] / sum(q["ms"] for q in prof.values()), 4)
+                                      for k, v in prof.items()})
+        cpu = None
+        if world == 1 and not a.no_cpu_baseline:
+            cb = cpu_baseline(a.cpu_n, a.m, a.m)
+            if cb:
+                scale = n / int(a.cpu_n)
+                cpu = dict(value=round(1.0 / (cb["per_iter_s"] * scale), 6), unit="iters/s", cores=1,
+                           kind="reference",
+                           sample=(f"reference sequential LBFGS (oracle/_ref, sources compiled -O2 "
+                                   f"-ffp-contract=off), Rosenbrock n={int(a.cpu_n):.0e} m={a.m} "
+                                   f"backtracking, mean of {cb['iters_timed']} steady iterations "
+                                   f"(h=m) = {cb['per_iter_s']:.3f} s/iter, scaled x{scale:g} "
+                                   f"linearly in n to n={n:.0e}; 1 of {os.cpu_count()} cores "
+                                   f"({cpu_model()})"),
+                           per_iter_s_sample=cb["per_iter_s"], total_s=round(cb["total_s"], 2))
+        out = {
+            "metric": "L-BFGS iters/sec (n=1e8 Rosenbrock, m=10, fp64)",
+            "value": round(value, 4),
+            "unit": "iters/s",
+            "n_gpus": world,
+            "steps": done_steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(T / done_steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic: x0 ~ U(-2,2) from std::mt19937(42), as the reference's main.cpp",
+            "config": {"workload": (f"{a.objective} n={n:.0e} m={a.m} {a.line_search}, "
+                                    f"{'sharded over ' + str(world) + ' GPUs' if world > 1 else 'one GPU'}"
+                                    " (BASELINE configs[2])"),
+                       "n": n, "m": a.m, "line_search": a.line_search,
+                       "parallelism": f"shard{world}" if world > 1 else "single"},
+            "achieved_hbm_gbps": round(bytes_all / T / 1e9, 1),
+            "bytes_per_step": bytes_all / max(done_steps, 1),
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "solver": {"status": res["status"], "f": res["f"], "gnorm": res["gnorm"],
+                       "trials_f": res["trials_f"], "commits": res["commits"],
+                       "passes": res["passes"]},
+        }
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    D.close()
+
+
+if __name__ == "__main__":
+    main()

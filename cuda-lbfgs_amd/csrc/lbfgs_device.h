@@ -1,0 +1,121 @@
+/* lbfgs_device.h — internal C interface between the C host driver (lbfgs_driver.c) and the
+ * HIP device layer (lbfgs_kernels.hip). Not installed; the public ABI is include/lbfgs_hip.h.
+ *
+ * Every vector is an fp64 array of the rank's n_loc elements, addressed from its element 0,
+ * with ghost cells at [-1] and [n_loc] and zeroed padding behind it (see lbk_vec_alloc).
+ * Every reduction is written as 8 group partials into a result slot:
+ *   slot s, component k  ->  slots[s*LBK_SLOT + g*LBK_KMAX + k], g = 0..7
+ * and its value is the fixed-order sum Q0+Q1+...+Q7 (lbk_total).
+ */
+#ifndef LBFGS_DEVICE_H
+#define LBFGS_DEVICE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LBK_KMAX 8
+#define LBK_GROUPS 8
+#define LBK_SLOT (LBK_GROUPS * LBK_KMAX) /* doubles per slot */
+#define LBK_NSLOTS 256
+#define LBK_SEGS 8192
+#define LBK_SEG_PER_GROUP 1024
+
+/* objective ids (match include/lbfgs_hip.h) */
+#define LBK_OBJ_ROSENBROCK 0
+#define LBK_OBJ_QUAD_TRIDIAG 1
+#define LBK_OBJ_QUAD_SEPARABLE 2
+#define LBK_OBJ_NONE 3 /* gradient supplied in a buffer, f computed elsewhere (host callback) */
+
+/* direction modes of the commit kernel */
+#define LBK_D_BUF 0     /* d read from a buffer */
+#define LBK_D_NEG_G 1   /* d = -g                           (lbfgs.cpp:90, :151) */
+#define LBK_D_TWOLOOP 2 /* d = -(r + s (alpha_i - beta_i)) (last second-loop pass, :137-143) */
+
+/* commit reduction components */
+#define LBK_C_GD 0   /* g . d            */
+#define LBK_C_F 1    /* f(x + a d)       */
+#define LBK_C_SY 2   /* s . y            */
+#define LBK_C_YY 3   /* y . y            */
+#define LBK_C_GG 4   /* g_new . g_new    */
+#define LBK_C_SG 5   /* s . g_new  (alpha of the next first pass) */
+#define LBK_C_DPHI 6 /* g_new . d        */
+
+/* kernel kinds, for profiling / byte accounting */
+enum {
+    LBK_K_DOT = 0, LBK_K_AXPY_DOT, LBK_K_MID, LBK_K_AXPY2_DOT, LBK_K_LAST, LBK_K_NEGDOT,
+    LBK_K_EVAL, LBK_K_TRIAL_F, LBK_K_TRIAL_FG, LBK_K_COMMIT, LBK_K_POINT, LBK_K_CHECKSUM,
+    LBK_K_COUNT
+};
+
+typedef struct {
+    int64_t n;       /* global length */
+    int64_t L;       /* canonical segment length */
+    int64_t nseg;    /* global number of non-empty segments */
+    int64_t seg_lo;  /* first global segment of this rank */
+    int64_t seg_hi;  /* one past the last */
+    int64_t elem_lo; /* global index of local element 0 */
+    int64_t n_loc;   /* local elements */
+    int g_lo, g_hi;  /* groups owned by this rank */
+    int rank, world;
+} lbk_geo;
+
+typedef struct lbk_ctx lbk_ctx;
+
+/* lifecycle */
+int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const void* nccl_id);
+void lbk_destroy(lbk_ctx* c);
+const lbk_geo* lbk_geometry(const lbk_ctx* c);
+const char* lbk_last_error(const lbk_ctx* c);
+int lbk_unique_id(void* out128);
+
+/* memory */
+double* lbk_vec_alloc(lbk_ctx* c);
+void lbk_vec_free(lbk_ctx* c, double* v);
+int lbk_upload(lbk_ctx* c, double* dst, const double* host_global);     /* incl. ghosts */
+int lbk_download(lbk_ctx* c, double* host_global, const double* src);   /* local part */
+int lbk_copy(lbk_ctx* c, double* dst, const double* src);               /* incl. ghosts */
+int lbk_download_local(lbk_ctx* c, double* host_local, const double* src);
+int lbk_upload_local(lbk_ctx* c, double* dst, const double* host_local);
+
+/* kernels (async on the context stream). 'slot' = result slot index; slot references
+ * (prev, beta, alpha) are (slot index, component) pairs packed as slot*LBK_KMAX + comp. */
+int lbk_dot(lbk_ctx* c, const double* a, const double* b, int slot);
+int lbk_axpy_dot(lbk_ctx* c, double* qout, const double* qin, const double* y, const double* s,
+                 double rho, int ref_alpha, int slot);
+int lbk_mid(lbk_ctx* c, double* rout, const double* qin, const double* y0, double rho0,
+            double gamma, int ref_alpha, int slot);
+int lbk_axpy2_dot(lbk_ctx* c, double* r, const double* s, const double* ynext, double rho,
+                  int ref_beta, int ref_alpha, int slot);
+int lbk_last(lbk_ctx* c, double* dout, const double* r, const double* s, const double* g,
+             double rho, int ref_beta, int ref_alpha, int slot);
+int lbk_negdot(lbk_ctx* c, double* dout, const double* g, int slot);
+int lbk_eval(lbk_ctx* c, int obj, const double* x, double* gout, int slot);  /* f, g.g */
+int lbk_trial(lbk_ctx* c, int obj, const double* x, const double* d, double alpha,
+              double* gout, int slot);                                           /* f, gt.d */
+/* commit at x + alpha*d (d per dmode); writes xn, s_out, y_out and (obj != NONE) gn.
+ * For obj == NONE the new gradient is read from gn (host-supplied). */
+int lbk_commit(lbk_ctx* c, int obj, int dmode, const double* x, const double* dsrc,
+               const double* s_last, const double* g, double rho, int ref_beta, int ref_alpha,
+               double alpha, double* xn, double* gn, double* s_out, double* y_out, int slot);
+/* z = x + alpha * d (host-callback objectives) */
+int lbk_point(lbk_ctx* c, double* z, const double* x, const double* d, double alpha);
+int lbk_checksum(lbk_ctx* c, const double* x, uint64_t* c1, uint64_t* c2); /* sync */
+
+/* results */
+int lbk_fetch(lbk_ctx* c, int slot, int ncomp, double* totals);   /* sync, fixed-order totals */
+int lbk_fetch_groups(lbk_ctx* c, int slot, double* groups64);     /* sync, raw 8 x KMAX */
+double lbk_total(const double* groups64, int comp);
+int lbk_sync(lbk_ctx* c);
+
+/* profiling: per-kind event timing (enable before the timed region) */
+void lbk_prof_enable(lbk_ctx* c, int on);
+int lbk_prof_get(lbk_ctx* c, int kind, double* ms, int64_t* launches, double* bytes);
+void lbk_prof_reset(lbk_ctx* c);
+double lbk_bytes_moved(const lbk_ctx* c); /* algorithmic bytes of all launches so far */
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,892 @@
+/* lbfgs_driver.c — C host driver of the MI355X L-BFGS solver (public ABI: include/lbfgs_hip.h).
+ *
+ * The control flow is the reference's LBFGS() (sequential-implementation/lbfgs.cpp:17-203) and
+ * its line searches (line_search.cpp:8-189), restated over scalars only: every n-vector lives
+ * on the GPU and every vector operation is a fused device pass (lbfgs_kernels.hip). The host
+ * sees, per iteration, one 512-byte read-back of the commit's reductions (g.d, f, s.y, y.y,
+ * |g|^2, s.g, g.d_phi), plus one per extra line-search trial.
+ *
+ * Per-iteration device schedule (h stored pairs, reference line numbers):
+ *   [P0]  s_{h-1}.g         fused into the previous commit (SG), or lbk_dot if that pair
+ *                           was not pushed                                     (:133)
+ *   h-1 x k_axpy_dot        q -= alpha_{i+1} y_{i+1};  s_i.q                    (:124-138)
+ *   k_mid                   r = (q - alpha_0 y_0) gamma;  y_0.r                 (:141-154,:160)
+ *   h-1 x k_axpy2_dot       r += s_i (alpha_i - beta_i);  y_{i+1}.r             (:157-165)
+ *   k_commit (TWOLOOP)      d = -(r + s(alpha-beta)), g.d, x+a0 d, f, grad, s, y, dots
+ *                           — the last second-loop pass, the first line-search trial at
+ *                           a0 = INITIAL_STEP_SIZE and the commit, in one pass  (:163-198)
+ * If the line search accepts a0 (the common case) the iteration is complete; otherwise d is
+ * materialised (k_last), the remaining trials run as k_trial passes and the commit is redone
+ * at the accepted step. Results are bit-identical to running the reference's steps
+ * separately in the canonical reduction order (oracle/lbfgs_oracle.c, ORC_CANON).
+ */
+#define _POSIX_C_SOURCE 199309L
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include "lbfgs_device.h"
+#include "lbfgs_hip.h"
+
+#define MMAX 64
+
+/* result slots */
+#define SLOT_INIT 0
+#define SLOT_COMMIT0 1 /* commits alternate 1 / 2 so SG survives into the next iteration */
+#define SLOT_P0 3
+#define SLOT_A0 4 /* + i  : s_i . q          */
+#define SLOT_B0(m) (4 + (m)) /* + i : y_i . r   */
+#define SLOT_LAST(m) (4 + 2 * (m))
+#define SLOT_TRIAL(m) (5 + 2 * (m))
+#define SLOT_MISC(m) (6 + 2 * (m))
+#define REF(slot, comp) ((slot) * LBK_KMAX + (comp))
+
+struct lbfgs_ctx {
+    lbk_ctx* dev;
+    const lbk_geo* geo;
+    int64_t n;
+    int m;
+    /* device vectors */
+    double *x, *g, *xn, *gn, *d, *q, *r, *gt;
+    double* S[MMAX + 1];
+    double* Y[MMAX + 1];
+    /* history: ring[0] oldest .. ring[h-1] newest, indices into the m+1 pair pool */
+    int h, ring[MMAX + 1], free_pair;
+    double sy[MMAX + 1], yy[MMAX + 1];
+    /* solver state */
+    int inited, obj, ls, k, status, finished;
+    lbfgs_constants K;
+    double tol;
+    unsigned flags;
+    double f_cur, gg;
+    int sg_valid, sg_ref;
+    lbfgs_host_fn cb;
+    double *hx, *hg; /* host buffers (callbacks) */
+    /* per-iteration working state */
+    int dmode, d_ready;
+    double rho_last, a0;
+    int ref_b_last, ref_a_last, s_last_pair;
+    int spec_valid;
+    double spec_f, spec_dphi, spec_tot[LBK_KMAX];
+    int gt_valid;
+    double gt_alpha;
+    /* counters */
+    int64_t trials_f, trials_fg, commits, passes;
+    /* messages / trace */
+    char* msg;
+    int msg_len, msg_cap;
+    double *tr_f, *tr_gn, *tr_a;
+    uint64_t *tr_c1, *tr_c2;
+    int tr_len, tr_cap;
+    char err[256];
+};
+
+/* ------------------------------------------------------------------------------------------ */
+static double now_s(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
+static void say(lbfgs_ctx* c, const char* fmt, ...) {
+    char buf[256];
+    va_list ap;
+    va_start(ap, fmt);
+    int k = vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    if (k < 0) return;
+    if (!(c->flags & LBFGS_FLAG_QUIET)) {
+        fputs(buf, stdout);
+        fflush(stdout);
+    }
+    if (c->msg_len + k + 1 > c->msg_cap) {
+        int cap = c->msg_cap ? c->msg_cap * 2 : 4096;
+        while (cap < c->msg_len + k + 1) cap *= 2;
+        char* p = (char*)realloc(c->msg, (size_t)cap);
+        if (!p) return;
+        c->msg = p;
+        c->msg_cap = cap;
+    }
+    memcpy(c->msg + c->msg_len, buf, (size_t)k);
+    c->msg_len += k;
+    c->msg[c->msg_len] = 0;
+}
+
+static int dev_err(lbfgs_ctx* c, int rc) {
+    if (rc < 0) snprintf(c->err, sizeof c->err, "%s", lbk_last_error(c->dev));
+    return rc < -6 ? LBFGS_ERR_HIP : rc;
+}
+#define DEV(call)                                 \
+    do {                                          \
+        int rc_ = (call);                         \
+        if (rc_ != 0) return dev_err(c, rc_);     \
+        c->passes++;                              \
+    } while (0)
+#define DEVNC(call)                               \
+    do {                                          \
+        int rc_ = (call);                         \
+        if (rc_ != 0) return dev_err(c, rc_);     \
+    } while (0)
+
+static int trace_push(lbfgs_ctx* c, double f, double gn, int with_ck) {
+    if (!(c->flags & LBFGS_FLAG_TRACE)) return 0;
+    if (c->tr_len == c->tr_cap) {
+        int cap = c->tr_cap ? 2 * c->tr_cap : 1024;
+        double* a = (double*)realloc(c->tr_f, sizeof(double) * cap);
+        if (a) c->tr_f = a;
+        a = (double*)realloc(c->tr_gn, sizeof(double) * cap);
+        if (a) c->tr_gn = a;
+        a = (double*)realloc(c->tr_a, sizeof(double) * cap);
+        if (a) c->tr_a = a;
+        uint64_t* u = (uint64_t*)realloc(c->tr_c1, sizeof(uint64_t) * cap);
+        if (u) c->tr_c1 = u;
+        u = (uint64_t*)realloc(c->tr_c2, sizeof(uint64_t) * cap);
+        if (u) c->tr_c2 = u;
+        if (!c->tr_f || !c->tr_gn || !c->tr_a || !c->tr_c1 || !c->tr_c2) return LBFGS_ERR_NOMEM;
+        c->tr_cap = cap;
+    }
+    int i = c->tr_len++;
+    c->tr_f[i] = f;
+    c->tr_gn[i] = gn;
+    c->tr_a[i] = NAN;
+    c->tr_c1[i] = c->tr_c2[i] = 0;
+    if (with_ck) DEVNC(lbk_checksum(c->dev, c->x, &c->tr_c1[i], &c->tr_c2[i]));
+    return 0;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+void lbfgs_constants_default(lbfgs_constants* k) { /* sequential-implementation/config.h:5-17 */
+    k->c1 = 1e-4;
+    k->c2 = 0.9;
+    k->initial_step = 1.0;
+    k->backtracking_alpha = 0.5;
+    k->backtracking_tol = 1e-8;
+    k->wolfe_interp_min = 1e-10;
+    k->wolfe_interp_max = 10.0;
+}
+
+void lbfgs_constants_cuda(lbfgs_constants* k) { /* parallel-implementation/constants.h:5-17 */
+    lbfgs_constants_default(k);
+    k->c2 = 0.7;
+}
+
+int lbfgs_unique_id(void* out128) { return lbk_unique_id(out128) == 0 ? 0 : LBFGS_ERR_RCCL; }
+
+static void free_vectors(lbfgs_ctx* c) {
+    double** v[] = {&c->x, &c->g, &c->xn, &c->gn, &c->d, &c->q, &c->r, &c->gt};
+    for (size_t i = 0; i < sizeof v / sizeof v[0]; ++i) {
+        lbk_vec_free(c->dev, *v[i]);
+        *v[i] = NULL;
+    }
+    for (int i = 0; i <= MMAX; ++i) {
+        lbk_vec_free(c->dev, c->S[i]);
+        lbk_vec_free(c->dev, c->Y[i]);
+        c->S[i] = c->Y[i] = NULL;
+    }
+}
+
+int lbfgs_ctx_create_sharded(lbfgs_ctx** out, int64_t n, int m, int device, int rank, int world,
+                             const void* unique_id) {
+    if (!out) return LBFGS_ERR_BAD_ARG;
+    *out = NULL;
+    if (n < 1 || m < 1 || m > MMAX || world < 1 || (8 % world) != 0 || rank < 0 || rank >= world)
+        return LBFGS_ERR_BAD_ARG;
+    if (world > 1 && !unique_id) return LBFGS_ERR_BAD_ARG;
+    lbfgs_ctx* c = (lbfgs_ctx*)calloc(1, sizeof(lbfgs_ctx));
+    if (!c) return LBFGS_ERR_NOMEM;
+    c->n = n;
+    c->m = m;
+    int rc = lbk_create(&c->dev, device, n, rank, world, unique_id);
+    if (rc != 0) {
+        if (c->dev) {
+            snprintf(c->err, sizeof c->err, "%s", lbk_last_error(c->dev));
+            fprintf(stderr, "lbfgs_ctx_create: %s\n", c->err);
+            lbk_destroy(c->dev);
+        }
+        free(c);
+        return rc == -3 ? LBFGS_ERR_RCCL : rc == -1 ? LBFGS_ERR_BAD_ARG : LBFGS_ERR_HIP;
+    }
+    c->geo = lbk_geometry(c->dev);
+    double** v[] = {&c->x, &c->g, &c->xn, &c->gn, &c->d, &c->q, &c->r, &c->gt};
+    int ok = 1;
+    for (size_t i = 0; i < sizeof v / sizeof v[0]; ++i) ok &= (*v[i] = lbk_vec_alloc(c->dev)) != NULL;
+    for (int i = 0; i <= m; ++i) {
+        ok &= (c->S[i] = lbk_vec_alloc(c->dev)) != NULL;
+        ok &= (c->Y[i] = lbk_vec_alloc(c->dev)) != NULL;
+    }
+    if (!ok) {
+        fprintf(stderr, "lbfgs_ctx_create: %s\n", lbk_last_error(c->dev));
+        free_vectors(c);
+        lbk_destroy(c->dev);
+        free(c);
+        return LBFGS_ERR_NOMEM;
+    }
+    lbk_sync(c->dev);
+    *out = c;
+    return 0;
+}
+
+int lbfgs_ctx_create(lbfgs_ctx** out, int64_t n, int m, int device) {
+    return lbfgs_ctx_create_sharded(out, n, m, device, 0, 1, NULL);
+}
+
+void lbfgs_ctx_destroy(lbfgs_ctx* c) {
+    if (!c) return;
+    free_vectors(c);
+    lbk_destroy(c->dev);
+    free(c->hx);
+    free(c->hg);
+    free(c->msg);
+    free(c->tr_f);
+    free(c->tr_gn);
+    free(c->tr_a);
+    free(c->tr_c1);
+    free(c->tr_c2);
+    free(c);
+}
+
+const char* lbfgs_last_error(const lbfgs_ctx* c) { return c ? c->err : "null context"; }
+
+int lbfgs_local_range(const lbfgs_ctx* c, int64_t* elem_lo, int64_t* n_loc) {
+    if (!c) return LBFGS_ERR_BAD_ARG;
+    if (elem_lo) *elem_lo = c->geo->elem_lo;
+    if (n_loc) *n_loc = c->geo->n_loc;
+    return 0;
+}
+
+int lbfgs_sync(lbfgs_ctx* c) { return lbk_sync(c->dev) == 0 ? 0 : LBFGS_ERR_HIP; }
+
+/* ------------------------------------------------------------------------------------------
+ * Host-callback objective helpers (LBFGS_OBJ_HOST; single rank)
+ * ---------------------------------------------------------------------------------------- */
+static int host_bufs(lbfgs_ctx* c) {
+    if (!c->hx) c->hx = (double*)malloc(sizeof(double) * (size_t)c->n);
+    if (!c->hg) c->hg = (double*)malloc(sizeof(double) * (size_t)c->n);
+    return (c->hx && c->hg) ? 0 : LBFGS_ERR_NOMEM;
+}
+
+/* f (and optionally grad -> device vector gdst) at z = x + alpha d on the host */
+static int host_eval_at(lbfgs_ctx* c, double alpha, double* f, double* gdst) {
+    DEV(lbk_point(c->dev, c->xn, c->x, c->d, alpha));
+    DEVNC(lbk_download_local(c->dev, c->hx, c->xn));
+    *f = c->cb.f(c->hx, c->n, c->cb.user);
+    if (gdst) {
+        c->cb.grad(c->hx, c->n, c->hg, c->cb.user);
+        DEVNC(lbk_upload_local(c->dev, gdst, c->hg));
+    }
+    return 0;
+}
+
+/* ------------------------------------------------------------------------------------------
+ * Line-search trial evaluation. The fused speculative commit already evaluated f and
+ * g_new.d at a0; every other step runs one k_trial pass over materialised x, d.
+ * ---------------------------------------------------------------------------------------- */
+static int materialize_d(lbfgs_ctx* c) {
+    if (c->d_ready) return 0;
+    const int m = c->m;
+    if (c->dmode == LBK_D_TWOLOOP) {
+        DEV(lbk_last(c->dev, c->d, c->r, c->S[c->s_last_pair], c->g, c->rho_last, c->ref_b_last,
+                     c->ref_a_last, SLOT_LAST(m)));
+    } else if (c->dmode == LBK_D_NEG_G) {
+        DEV(lbk_negdot(c->dev, c->d, c->g, SLOT_LAST(m)));
+    }
+    c->dmode = LBK_D_BUF;
+    c->d_ready = 1;
+    return 0;
+}
+
+static int trial(lbfgs_ctx* c, double alpha, int need_g, double* f, double* dphi) {
+    if (c->spec_valid && alpha == c->a0) {
+        *f = c->spec_f;
+        if (dphi) *dphi = c->spec_dphi;
+        return 0;
+    }
+    int rc = materialize_d(c);
+    if (rc) return rc;
+    if (c->obj == LBFGS_OBJ_HOST) {
+        rc = host_eval_at(c, alpha, f, need_g ? c->gt : NULL);
+        if (rc) return rc;
+        if (need_g) {
+            double t;
+            DEV(lbk_dot(c->dev, c->gt, c->d, SLOT_TRIAL(c->m)));
+            DEVNC(lbk_fetch(c->dev, SLOT_TRIAL(c->m), 1, &t));
+            *dphi = t;
+            c->gt_valid = 1;
+            c->gt_alpha = alpha;
+        }
+    } else {
+        double t[2];
+        DEV(lbk_trial(c->dev, c->obj, c->x, c->d, alpha, need_g ? c->gt : NULL, SLOT_TRIAL(c->m)));
+        DEVNC(lbk_fetch(c->dev, SLOT_TRIAL(c->m), 2, t));
+        *f = t[0];
+        if (need_g && dphi) *dphi = t[1];
+    }
+    if (need_g)
+        c->trials_fg++;
+    else
+        c->trials_f++;
+    return 0;
+}
+
+static double cubic_interp(double a0, double a1, double p0, double dp0, double p1, double dp1) {
+    double d1 = dp0 + dp1 - 3 * (p1 - p0) / (a1 - a0); /* line_search.cpp:8-12 */
+    double d2 = copysign(sqrt(d1 * d1 - dp0 * dp1), a1 - a0);
+    return a0 + (a1 - a0) * (dp0 + d2 - d1) / (dp0 - dp1 + 2 * d2);
+}
+
+static double quad_interp(double a0, double p0, double dp0, double p1) { /* :14-16 */
+    return a0 - 0.5 * dp0 * a0 * a0 / (p1 - p0 - dp0 * a0);
+}
+
+/* line_search.cpp:19-30 (f(x) == f_current, g.d == gd: identical values, evaluated once) */
+static int ls_backtracking(lbfgs_ctx* c, double gd, double* out) {
+    const lbfgs_constants* K = &c->K;
+    double alpha = K->initial_step;
+    for (;;) {
+        double ft;
+        int rc = trial(c, alpha, 0, &ft, NULL);
+        if (rc) return rc;
+        if (!(c->f_cur - ft < K->c1 * alpha * gd)) break;
+        alpha *= K->backtracking_alpha;
+        if (alpha < K->backtracking_tol) break;
+    }
+    *out = alpha;
+    return 0;
+}
+
+/* line_search.cpp:33-55 */
+static int ls_backtracking_wolfe(lbfgs_ctx* c, double gd, double* out) {
+    const lbfgs_constants* K = &c->K;
+    double alpha = K->initial_step;
+    for (;;) {
+        double fn, dphi;
+        int rc = trial(c, alpha, 1, &fn, &dphi);
+        if (rc) return rc;
+        if (fn > c->f_cur + K->c1 * alpha * gd) {
+            alpha *= K->backtracking_alpha;
+        } else if (dphi < K->c2 * gd) {
+            alpha *= 1.1;
+        } else {
+            break;
+        }
+        if (alpha < K->backtracking_tol) break;
+    }
+    *out = alpha;
+    return 0;
+}
+
+/* line_search.cpp:57-121 */
+static int ls_interpolation(lbfgs_ctx* c, double gd, double* out) {
+    const lbfgs_constants* K = &c->K;
+    const double f_x = c->f_cur;
+    double alpha = K->initial_step, alpha_prev = 0.0, f_prev = f_x;
+    int it = 0;
+    while (it++ < 20) {
+        double f_new;
+        int rc = trial(c, alpha, 0, &f_new, NULL);
+        if (rc) return rc;
+        if (f_new <= f_x + K->c1 * alpha * gd) {
+            *out = alpha;
+            return 0;
+        }
+        if (alpha < K->wolfe_interp_min) {
+            *out = K->wolfe_interp_min;
+            return 0;
+        }
+        if (alpha_prev > 0) {
+            double delta = alpha - alpha_prev;
+            if (fabs(delta) < 1e-10) {
+                alpha *= 0.5;
+            } else {
+                double ga = (f_new - f_x - gd * alpha) / (alpha * alpha);
+                alpha = cubic_interp(alpha_prev, alpha, f_prev, gd, f_new, ga);
+                if (alpha < 0.1 * alpha_prev || alpha > 0.9 * alpha_prev) alpha = alpha_prev * 0.5;
+            }
+        } else {
+            alpha = quad_interp(alpha, f_new, gd, f_x);
+            if (alpha < 0.1 * K->initial_step || alpha > 0.9 * K->initial_step)
+                alpha = K->initial_step * 0.5;
+        }
+        alpha_prev = alpha;
+        f_prev = f_new;
+    }
+    *out = alpha;
+    return 0;
+}
+
+/* line_search.cpp:125-189 */
+static int ls_wolfe(lbfgs_ctx* c, double gd, double* out) {
+    const lbfgs_constants* K = &c->K;
+    const double f_x = c->f_cur;
+    double alpha = K->initial_step;
+    double alpha_lo = 0.0, alpha_hi = INFINITY, f_lo = f_x, dphi_lo = gd;
+    for (int iter = 0; iter < 20; ++iter) {
+        double f_new, dphi_new;
+        /* f first; the gradient only if the sufficient-decrease tests pass (:144-153) */
+        int rc = trial(c, alpha, 0, &f_new, NULL);
+        if (rc) return rc;
+        if (f_new > f_x + K->c1 * alpha * gd || (f_new >= f_lo && iter > 0)) {
+            alpha_hi = alpha;
+            alpha = cubic_interp(alpha_lo, alpha_hi, f_lo, dphi_lo, f_new,
+                                 (f_new - f_x - gd * alpha) / (alpha * alpha));
+            continue;
+        }
+        rc = trial(c, alpha, 1, &f_new, &dphi_new);
+        if (rc) return rc;
+        if (fabs(dphi_new) <= -K->c2 * gd) {
+            *out = alpha;
+            return 0;
+        }
+        if (dphi_new >= 0) {
+            alpha_hi = alpha;
+            alpha = cubic_interp(alpha_lo, alpha_hi, f_lo, dphi_lo, f_new, dphi_new);
+        } else {
+            alpha_lo = alpha;
+            f_lo = f_new;
+            dphi_lo = dphi_new;
+            if (alpha_hi == INFINITY)
+                alpha *= 2;
+            else
+                alpha = cubic_interp(alpha_lo, alpha_hi, f_lo, dphi_lo, f_new, dphi_new);
+        }
+        if (alpha < K->wolfe_interp_min) {
+            *out = K->wolfe_interp_min;
+            return 0;
+        }
+    }
+    *out = alpha;
+    return 0;
+}
+
+/* ------------------------------------------------------------------------------------------
+ * Commit at step alpha: x_new, g_new, s, y and their reductions into tot[].
+ * ---------------------------------------------------------------------------------------- */
+static int commit(lbfgs_ctx* c, int dmode, double alpha, int cslot, double* tot) {
+    const int pair = c->free_pair;
+    const double* dsrc = dmode == LBK_D_BUF ? c->d : c->r;
+    const double* s_last = dmode == LBK_D_TWOLOOP ? c->S[c->s_last_pair] : NULL;
+    int obj = c->obj;
+    if (c->obj == LBFGS_OBJ_HOST) {
+        /* host objective: g_new on the device first (reuse the trial gradient if it is the
+         * gradient at exactly this step), f on the host */
+        double f;
+        if (c->gt_valid && c->gt_alpha == alpha) {
+            int rc = host_eval_at(c, alpha, &f, NULL);
+            if (rc) return rc;
+            DEVNC(lbk_copy(c->dev, c->gn, c->gt));
+        } else {
+            int rc = host_eval_at(c, alpha, &f, c->gn);
+            if (rc) return rc;
+        }
+        obj = LBK_OBJ_NONE;
+        DEV(lbk_commit(c->dev, obj, dmode, c->x, dsrc, s_last, c->g, c->rho_last, c->ref_b_last,
+                       c->ref_a_last, alpha, c->xn, c->gn, c->S[pair], c->Y[pair], cslot));
+        DEVNC(lbk_fetch(c->dev, cslot, 7, tot));
+        tot[LBK_C_F] = f;
+    } else {
+        DEV(lbk_commit(c->dev, obj, dmode, c->x, dsrc, s_last, c->g, c->rho_last, c->ref_b_last,
+                       c->ref_a_last, alpha, c->xn, c->gn, c->S[pair], c->Y[pair], cslot));
+        DEVNC(lbk_fetch(c->dev, cslot, 7, tot));
+    }
+    c->commits++;
+    return 0;
+}
+
+/* ------------------------------------------------------------------------------------------
+ * One iteration of lbfgs.cpp:72-199. Returns 0 to continue, 1 when finished, < 0 on error.
+ * ---------------------------------------------------------------------------------------- */
+static int iterate(lbfgs_ctx* c) {
+    const int k = c->k, m = c->m, h = c->h;
+    const double gnorm = sqrt(c->gg);
+    int rc = trace_push(c, c->f_cur, gnorm, 1);
+    if (rc) return rc;
+    if (c->flags & LBFGS_FLAG_VERBOSE) { /* :76-78 */
+        printf("Iteration %d, f = %g, |grad| = %g\n", k, c->f_cur, gnorm);
+        fflush(stdout);
+    }
+    if (gnorm < c->tol) { /* :80-84 */
+        say(c, "Converged!\n");
+        c->status = LBFGS_STATUS_CONVERGED;
+        return 1;
+    }
+
+    /* ---- search direction (:87-143) ---- */
+    int dmode = LBK_D_NEG_G;
+    c->d_ready = 0;
+    c->spec_valid = 0;
+    c->gt_valid = 0;
+    if (!(k == 0 || h == 0)) {
+        int bad_rho = 0;
+        for (int i = h - 1; i >= 0; --i)
+            if (!isfinite(1.0 / c->sy[c->ring[i]])) bad_rho = 1; /* :102-108 */
+        double gamma = 0.0;
+        if (bad_rho) {
+            say(c, "Warning: Invalid rho at iteration %d\n", k);
+        } else {
+            const int top = c->ring[h - 1];
+            gamma = c->sy[top] / c->yy[top]; /* :117-118 */
+            if (gamma <= 0 || !isfinite(gamma)) {
+                say(c, "Warning: Invalid gamma at iteration %d\n", k);
+            } else {
+                dmode = LBK_D_TWOLOOP;
+            }
+        }
+        if (dmode == LBK_D_TWOLOOP) {
+            int refA[MMAX], refB[MMAX];
+            double rho[MMAX];
+            for (int i = 0; i < h; ++i) rho[i] = 1.0 / c->sy[c->ring[i]];
+            const int top = c->ring[h - 1];
+            if (c->sg_valid) {
+                refA[h - 1] = c->sg_ref; /* s_{h-1}.g from the previous commit */
+            } else {
+                DEV(lbk_dot(c->dev, c->S[top], c->g, SLOT_P0));
+                refA[h - 1] = REF(SLOT_P0, 0);
+            }
+            const double* qsrc = c->g;
+            for (int i = h - 2; i >= 0; --i) {
+                DEV(lbk_axpy_dot(c->dev, c->q, qsrc, c->Y[c->ring[i + 1]], c->S[c->ring[i]], rho[i + 1],
+                                 refA[i + 1], SLOT_A0 + i));
+                refA[i] = REF(SLOT_A0 + i, 0);
+                qsrc = c->q;
+            }
+            DEV(lbk_mid(c->dev, c->r, qsrc, c->Y[c->ring[0]], rho[0], gamma, refA[0], SLOT_B0(m)));
+            refB[0] = REF(SLOT_B0(m), 0);
+            for (int i = 0; i + 1 < h; ++i) {
+                DEV(lbk_axpy2_dot(c->dev, c->r, c->S[c->ring[i]], c->Y[c->ring[i + 1]], rho[i], refB[i],
+                                  refA[i], SLOT_B0(m) + i + 1));
+                refB[i + 1] = REF(SLOT_B0(m) + i + 1, 0);
+            }
+            c->rho_last = rho[h - 1];
+            c->ref_b_last = refB[h - 1];
+            c->ref_a_last = refA[h - 1];
+            c->s_last_pair = top;
+        }
+    }
+    c->dmode = dmode;
+
+    /* ---- descent check (:146-153) and the line search (:156) ---- */
+    const int cslot = SLOT_COMMIT0 + (k & 1);
+    double tot[LBK_KMAX];
+    double gd;
+    c->a0 = c->K.initial_step;
+    if (c->obj != LBFGS_OBJ_HOST) {
+        /* fused: last two-loop pass + first trial at a0 + commit */
+        rc = commit(c, dmode, c->a0, cslot, tot);
+        if (rc) return rc;
+        gd = tot[LBK_C_GD];
+        if (gd >= 0) {
+            say(c, "Warning: Not a descent direction, using gradient\n");
+            c->dmode = dmode = LBK_D_NEG_G;
+            c->d_ready = 0;
+            rc = commit(c, dmode, c->a0, cslot, tot);
+            if (rc) return rc;
+            gd = tot[LBK_C_GD];
+        }
+        c->spec_valid = 1;
+        c->spec_f = tot[LBK_C_F];
+        c->spec_dphi = tot[LBK_C_DPHI];
+        memcpy(c->spec_tot, tot, sizeof tot);
+    } else {
+        rc = materialize_d(c);
+        if (rc) return rc;
+        DEVNC(lbk_fetch(c->dev, SLOT_LAST(m), 1, &gd));
+        if (gd >= 0) {
+            say(c, "Warning: Not a descent direction, using gradient\n");
+            c->dmode = LBK_D_NEG_G;
+            c->d_ready = 0;
+            rc = materialize_d(c);
+            if (rc) return rc;
+            DEVNC(lbk_fetch(c->dev, SLOT_LAST(m), 1, &gd));
+        }
+    }
+
+    double alpha;
+    switch (c->ls) {
+        case LBFGS_LS_BACKTRACKING: rc = ls_backtracking(c, gd, &alpha); break;
+        case LBFGS_LS_INTERPOLATION: rc = ls_interpolation(c, gd, &alpha); break;
+        case LBFGS_LS_WOLFE: rc = ls_wolfe(c, gd, &alpha); break;
+        default: rc = ls_backtracking_wolfe(c, gd, &alpha); break;
+    }
+    if (rc) return rc;
+    if (c->flags & LBFGS_FLAG_TRACE) c->tr_a[c->tr_len - 1] = alpha;
+
+    /* ---- commit (:159-198) ---- */
+    if (!(c->spec_valid && alpha == c->a0)) {
+        rc = materialize_d(c);
+        if (rc) return rc;
+        rc = commit(c, LBK_D_BUF, alpha, cslot, tot);
+        if (rc) return rc;
+    }
+    c->f_cur = tot[LBK_C_F];
+    if (alpha < 1e-10) { /* :164-168 */
+        say(c, "Warning: Line search failed at iteration %d\n", k);
+        c->status = LBFGS_STATUS_LS_FAILED;
+        return 1;
+    }
+    const double sy = tot[LBK_C_SY];
+    if (sy > 0) { /* :182-191 */
+        const int pair = c->free_pair;
+        if (c->h >= m) {
+            const int oldest = c->ring[0];
+            for (int i = 0; i + 1 < m; ++i) c->ring[i] = c->ring[i + 1];
+            c->ring[m - 1] = pair;
+            c->free_pair = oldest;
+        } else {
+            c->ring[c->h++] = pair;
+            c->free_pair = c->h; /* pool slots 0..h-1 used, h is free */
+        }
+        c->sy[pair] = sy;
+        c->yy[pair] = tot[LBK_C_YY];
+        c->sg_valid = 1;
+        c->sg_ref = REF(cslot, LBK_C_SG);
+    } else {
+        say(c, "Warning: Skipping update, sy = %g\n", sy); /* :192-195 */
+        c->sg_valid = 0;
+    }
+    /* x = x_new, g = g_new (:197-198) */
+    double* t = c->x;
+    c->x = c->xn;
+    c->xn = t;
+    t = c->g;
+    c->g = c->gn;
+    c->gn = t;
+    c->gg = tot[LBK_C_GG];
+    c->k++;
+    return 0;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+int lbfgs_solver_init(lbfgs_ctx* c, int objective, const lbfgs_host_fn* cb, int line_search,
+                      const lbfgs_constants* k, const double* x0_host, double tolerance,
+                      unsigned flags) {
+    if (!c || !x0_host) return LBFGS_ERR_BAD_ARG;
+    if (objective < 0 || objective > LBFGS_OBJ_HOST) return LBFGS_ERR_BAD_ARG;
+    if (line_search < 0 || line_search > LBFGS_LS_BACKTRACKING_WOLFE) return LBFGS_ERR_BAD_ARG;
+    if (objective == LBFGS_OBJ_HOST) {
+        if (!cb || !cb->f || !cb->grad || c->geo->world != 1) return LBFGS_ERR_BAD_ARG;
+        c->cb = *cb;
+        if (host_bufs(c)) return LBFGS_ERR_NOMEM;
+    }
+    c->obj = objective;
+    c->ls = line_search;
+    if (k)
+        c->K = *k;
+    else
+        lbfgs_constants_default(&c->K);
+    c->tol = tolerance;
+    c->flags = flags;
+    c->k = 0;
+    c->h = 0;
+    c->free_pair = 0;
+    c->sg_valid = 0;
+    c->status = LBFGS_STATUS_RUNNING;
+    c->finished = 0;
+    c->msg_len = 0;
+    if (c->msg) c->msg[0] = 0;
+    c->tr_len = 0;
+    c->trials_f = c->trials_fg = c->commits = c->passes = 0;
+
+    DEVNC(lbk_upload(c->dev, c->x, x0_host)); /* x = x0 */
+    if (objective == LBFGS_OBJ_HOST) {         /* :29-30 */
+        c->f_cur = c->cb.f(x0_host, c->n, c->cb.user);
+        c->cb.grad(x0_host, c->n, c->hg, c->cb.user);
+        DEVNC(lbk_upload_local(c->dev, c->g, c->hg));
+        DEV(lbk_dot(c->dev, c->g, c->g, SLOT_INIT));
+        DEVNC(lbk_fetch(c->dev, SLOT_INIT, 1, &c->gg));
+    } else {
+        double t[2];
+        DEV(lbk_eval(c->dev, objective, c->x, c->g, SLOT_INIT));
+        DEVNC(lbk_fetch(c->dev, SLOT_INIT, 2, t));
+        c->f_cur = t[0];
+        c->gg = t[1];
+    }
+    c->inited = 1;
+    return 0;
+}
+
+static void fill_result(lbfgs_ctx* c, lbfgs_result* out, double t0, double b0) {
+    if (!out) return;
+    out->iterations = c->k;
+    out->status = c->status;
+    out->f = c->f_cur;
+    out->gnorm = sqrt(c->gg);
+    out->trials_f = c->trials_f;
+    out->trials_fg = c->trials_fg;
+    out->commits = c->commits;
+    out->passes = c->passes;
+    out->bytes = lbk_bytes_moved(c->dev) - b0;
+    out->seconds = now_s() - t0;
+}
+
+int lbfgs_solver_step(lbfgs_ctx* c, int max_steps, lbfgs_result* out) {
+    if (!c || !c->inited) return LBFGS_ERR_STATE;
+    const double t0 = now_s(), b0 = lbk_bytes_moved(c->dev);
+    if (!c->finished) {
+        for (int s = 0; s < max_steps; ++s) {
+            int rc = iterate(c);
+            if (rc < 0) return rc;
+            if (rc == 1) {
+                c->finished = 1;
+                break;
+            }
+        }
+    }
+    fill_result(c, out, t0, b0);
+    return c->finished ? c->status : LBFGS_STATUS_RUNNING;
+}
+
+int lbfgs_get_x(lbfgs_ctx* c, double* x_out_host) {
+    if (!c || !x_out_host) return LBFGS_ERR_BAD_ARG;
+    DEVNC(lbk_download(c->dev, x_out_host, c->x));
+    return 0;
+}
+
+int lbfgs_minimize(lbfgs_ctx* c, int objective, const lbfgs_host_fn* cb, int line_search,
+                   const lbfgs_constants* k, const double* x0_host, double* x_out_host,
+                   int max_iterations, double tolerance, unsigned flags, lbfgs_result* out) {
+    const double t0 = now_s();
+    if (!c) return LBFGS_ERR_BAD_ARG;
+    const double b0 = lbk_bytes_moved(c->dev);
+    int rc = lbfgs_solver_init(c, objective, cb, line_search, k, x0_host, tolerance, flags);
+    if (rc) return rc;
+    rc = lbfgs_solver_step(c, max_iterations, NULL);
+    if (rc < 0) return rc;
+    if (!c->finished) { /* :201-202 */
+        rc = trace_push(c, c->f_cur, sqrt(c->gg), 1);
+        if (rc) return rc;
+        say(c, "Maximum iterations reached\n");
+        c->status = LBFGS_STATUS_MAX_ITER;
+        c->finished = 1;
+    }
+    if (x_out_host) {
+        rc = lbfgs_get_x(c, x_out_host);
+        if (rc) return rc;
+    }
+    fill_result(c, out, t0, b0);
+    return c->status;
+}
+
+int lbfgs_messages(const lbfgs_ctx* c, char* buf, int cap) {
+    if (!c || !buf || cap <= 0) return LBFGS_ERR_BAD_ARG;
+    int k = c->msg_len < cap - 1 ? c->msg_len : cap - 1;
+    if (k > 0) memcpy(buf, c->msg, (size_t)k);
+    buf[k] = 0;
+    return c->msg_len;
+}
+
+int lbfgs_trace_len(const lbfgs_ctx* c) { return c ? c->tr_len : 0; }
+
+int lbfgs_trace_get(const lbfgs_ctx* c, double* f, double* gnorm, double* alpha, uint64_t* c1,
+                    uint64_t* c2, int cap) {
+    if (!c) return LBFGS_ERR_BAD_ARG;
+    int k = c->tr_len < cap ? c->tr_len : cap;
+    for (int i = 0; i < k; ++i) {
+        if (f) f[i] = c->tr_f[i];
+        if (gnorm) gnorm[i] = c->tr_gn[i];
+        if (alpha) alpha[i] = c->tr_a[i];
+        if (c1) c1[i] = c->tr_c1[i];
+        if (c2) c2[i] = c->tr_c2[i];
+    }
+    return k;
+}
+
+/* ------------------------------------------------------------------------------------------
+ * Device primitives over host buffers (tests, drop-in vector_utils). They use the context's
+ * work vectors and therefore end any solve in progress.
+ * ---------------------------------------------------------------------------------------- */
+int lbfgs_dev_dot(lbfgs_ctx* c, const double* a, const double* b, double* out) {
+    if (!c || !a || !b || !out) return LBFGS_ERR_BAD_ARG;
+    c->inited = 0;
+    DEVNC(lbk_upload(c->dev, c->q, a));
+    DEVNC(lbk_upload(c->dev, c->r, b));
+    DEV(lbk_dot(c->dev, c->q, c->r, SLOT_MISC(c->m)));
+    DEVNC(lbk_fetch(c->dev, SLOT_MISC(c->m), 1, out));
+    return 0;
+}
+
+int lbfgs_dev_norm(lbfgs_ctx* c, const double* v, double* out) {
+    if (!c || !v || !out) return LBFGS_ERR_BAD_ARG;
+    double t;
+    int rc = lbfgs_dev_dot(c, v, v, &t);
+    if (rc) return rc;
+    *out = sqrt(t);
+    return 0;
+}
+
+int lbfgs_dev_objective(lbfgs_ctx* c, int obj, const double* x, double* f_out, double* g_out) {
+    if (!c || !x || obj < 0 || obj >= LBFGS_OBJ_HOST) return LBFGS_ERR_BAD_ARG;
+    c->inited = 0;
+    double t[2];
+    DEVNC(lbk_upload(c->dev, c->q, x));
+    DEV(lbk_eval(c->dev, obj, c->q, c->gt, SLOT_MISC(c->m)));
+    DEVNC(lbk_fetch(c->dev, SLOT_MISC(c->m), 2, t));
+    if (f_out) *f_out = t[0];
+    if (g_out) DEVNC(lbk_download(c->dev, g_out, c->gt));
+    return 0;
+}
+
+int lbfgs_dev_trial(lbfgs_ctx* c, int obj, const double* x, const double* d, double alpha,
+                    double* f_out, double* g_out, double* dphi_out) {
+    if (!c || !x || !d || obj < 0 || obj >= LBFGS_OBJ_HOST) return LBFGS_ERR_BAD_ARG;
+    c->inited = 0;
+    double t[2];
+    DEVNC(lbk_upload(c->dev, c->q, x));
+    DEVNC(lbk_upload(c->dev, c->d, d));
+    DEV(lbk_trial(c->dev, obj, c->q, c->d, alpha, g_out ? c->gt : NULL, SLOT_MISC(c->m)));
+    DEVNC(lbk_fetch(c->dev, SLOT_MISC(c->m), 2, t));
+    if (f_out) *f_out = t[0];
+    if (dphi_out) *dphi_out = t[1];
+    if (g_out) DEVNC(lbk_download(c->dev, g_out, c->gt));
+    return 0;
+}
+
+int lbfgs_dev_twoloop(lbfgs_ctx* c, const double* g, const double* const* S, const double* const* Y,
+                      int h, double* d_out, double* gd_out) {
+    if (!c || !g || h < 1 || h > c->m || !S || !Y) return LBFGS_ERR_BAD_ARG;
+    c->inited = 0;
+    const int m = c->m;
+    DEVNC(lbk_upload(c->dev, c->g, g));
+    for (int i = 0; i < h; ++i) {
+        DEVNC(lbk_upload(c->dev, c->S[i], S[i]));
+        DEVNC(lbk_upload(c->dev, c->Y[i], Y[i]));
+        c->ring[i] = i;
+        DEV(lbk_dot(c->dev, c->S[i], c->Y[i], SLOT_MISC(m)));
+        DEVNC(lbk_fetch(c->dev, SLOT_MISC(m), 1, &c->sy[i]));
+        DEV(lbk_dot(c->dev, c->Y[i], c->Y[i], SLOT_MISC(m)));
+        DEVNC(lbk_fetch(c->dev, SLOT_MISC(m), 1, &c->yy[i]));
+    }
+    int refA[MMAX], refB[MMAX];
+    double rho[MMAX];
+    for (int i = 0; i < h; ++i) rho[i] = 1.0 / c->sy[i];
+    const double gamma = c->sy[h - 1] / c->yy[h - 1];
+    DEV(lbk_dot(c->dev, c->S[h - 1], c->g, SLOT_P0));
+    refA[h - 1] = REF(SLOT_P0, 0);
+    const double* qsrc = c->g;
+    for (int i = h - 2; i >= 0; --i) {
+        DEV(lbk_axpy_dot(c->dev, c->q, qsrc, c->Y[i + 1], c->S[i], rho[i + 1], refA[i + 1], SLOT_A0 + i));
+        refA[i] = REF(SLOT_A0 + i, 0);
+        qsrc = c->q;
+    }
+    DEV(lbk_mid(c->dev, c->r, qsrc, c->Y[0], rho[0], gamma, refA[0], SLOT_B0(m)));
+    refB[0] = REF(SLOT_B0(m), 0);
+    for (int i = 0; i + 1 < h; ++i) {
+        DEV(lbk_axpy2_dot(c->dev, c->r, c->S[i], c->Y[i + 1], rho[i], refB[i], refA[i], SLOT_B0(m) + i + 1));
+        refB[i + 1] = REF(SLOT_B0(m) + i + 1, 0);
+    }
+    DEV(lbk_last(c->dev, c->d, c->r, c->S[h - 1], c->g, rho[h - 1], refB[h - 1], refA[h - 1], SLOT_LAST(m)));
+    double gd;
+    DEVNC(lbk_fetch(c->dev, SLOT_LAST(m), 1, &gd));
+    if (gd_out) *gd_out = gd;
+    if (d_out) DEVNC(lbk_download(c->dev, d_out, c->d));
+    return 0;
+}
+
+/* ---- profiling ---- */
+void lbfgs_prof_enable(lbfgs_ctx* c, int on) { lbk_prof_enable(c->dev, on); }
+void lbfgs_prof_reset(lbfgs_ctx* c) { lbk_prof_reset(c->dev); }
+int lbfgs_prof_get(lbfgs_ctx* c, int kind, double* ms, int64_t* launches, double* bytes) {
+    return lbk_prof_get(c->dev, kind, ms, launches, bytes) == 0 ? 0 : LBFGS_ERR_BAD_ARG;
+}

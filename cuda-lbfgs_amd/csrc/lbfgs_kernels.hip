@@ -1,0 +1,1132 @@
+// lbfgs_kernels.hip — MI355X (gfx950, CDNA4) device layer of the L-BFGS solver.
+//
+// Every kernel is one streaming pass over fp64 n-vectors that fuses the elementwise work of
+// one step of the reference algorithm with the dot products that depend on it:
+//
+//   k_axpy_dot   q = q_in - alpha_{i+1} y_{i+1};  s_i . q        (lbfgs.cpp:124-138, one i)
+//   k_mid        r = (q - alpha_0 y_0) * gamma;   y_0 . r        (:134-137, :141-154, :160)
+//   k_axpy2_dot  r += s_i (alpha_i - beta_i);      y_{i+1} . r    (:157-165)
+//   k_last       d = -(r + s (alpha - beta));      g . d          (:163-171)
+//   k_commit     d (any mode), x_new = x + a d, f(x_new), g_new, s, y and the five dots
+//                g.d, s.y, y.y, g_new.g_new, s.g_new, g_new.d in ONE pass  (:171-205)
+//   k_trial      f(x + a d) [, g_t and g_t . d]  without materialising x + a d
+//                (line_search.cpp:19-30, :125-189)
+//
+// The scalar that a pass needs from the previous pass (alpha_i = rho_i (s_i . q), beta_i) is
+// never sent to the host: the producing kernel leaves 8 group partials in a device result
+// slot and the consuming kernel forms the fixed-order total in its prologue.
+//
+// Canonical reduction order (restated in oracle/lbfgs_oracle.c for checking):
+//   segment s = [s L, min((s+1) L, n)), L = roundup(ceil(n/8192), 512), one 256-thread
+//   workgroup per segment; thread (w, lane) visits rows 4u + w (128 elements each), two
+//   elements per lane (one 16-B load), accumulating with v_fma_f64 (dots) / v_add_f64 (sums);
+//   wave butterfly (shfl_xor 1..32) -> ((w0 + w1) + (w2 + w3)) = segment partial;
+//   group g = segments 1024g..1024g+1023, reduced by the workgroup that arrives last at the
+//   group's ticket (write-through sc1 partials, agent-scope atomic ticket) into a balanced
+//   tree; total = Q0 + Q1 + ... + Q7 in order. The order depends on n only, so results are
+//   identical for any grid, any launch timing and any number of GPUs that divides 8.
+//
+// Elementwise arithmetic is compiled with -ffp-contract=off so every expression below rounds
+// exactly like the reference's C++ (x86-64, no FMA); the only FMAs are the explicit fma() of
+// the dot accumulations.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "lbfgs_device.h"
+
+#define LB_BLOCK 256
+
+namespace {
+
+struct Geo {
+    int64_t n, L, nseg, seg_lo, elem_lo, n_loc;
+    int g_lo;
+};
+
+struct Red {
+    double* partials;  // [LBK_KMAX][LBK_SEGS], local segment index
+    unsigned* cnt;     // [LBK_GROUPS] tickets
+    double* slot;      // this launch's result slot [LBK_GROUPS][LBK_KMAX]
+};
+
+__device__ __forceinline__ double2 ld2(const double* p) {
+    return *reinterpret_cast<const double2*>(p);
+}
+__device__ __forceinline__ void st2m(double* p, double2 v, bool v0, bool v1) {
+    if (v1) {
+        *reinterpret_cast<double2*>(p) = v;
+    } else if (v0) {
+        p[0] = v.x;
+    }
+}
+
+// fixed-order total of the 8 group partials of one slot component
+__device__ __forceinline__ double slot_total(const double* p) {
+    double t = p[0];
+#pragma unroll
+    for (int g = 1; g < LBK_GROUPS; ++g) t = t + p[g * LBK_KMAX];
+    return t;
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) v = v + __shfl_xor(v, m, 64);
+    return v;
+}
+
+__device__ __forceinline__ unsigned long long dbits(double v) {
+    return (unsigned long long)__double_as_longlong(v);
+}
+__device__ __forceinline__ double bitsd(unsigned long long u) {
+    return __longlong_as_double((long long)u);
+}
+
+// Per-workgroup view of its segment.
+struct Seg {
+    int64_t sbeg;   // global index of segment start
+    int64_t lb;     // local index of segment start
+    int64_t len;    // valid elements in this segment
+    int nrows;      // rows (of 128) this wave visits
+    int lane, w;
+};
+
+__device__ __forceinline__ Seg seg_setup(const Geo& geo) {
+    Seg s;
+    const int64_t sg = geo.seg_lo + blockIdx.x;
+    s.sbeg = sg * geo.L;
+    const int64_t send = min(s.sbeg + geo.L, geo.n);
+    s.len = send - s.sbeg;
+    s.lb = s.sbeg - geo.elem_lo;
+    s.lane = threadIdx.x & 63;
+    s.w = threadIdx.x >> 6;
+    const int nrow_tot = (int)((s.len + 127) / 128);
+    s.nrows = nrow_tot > s.w ? (nrow_tot - s.w + 3) / 4 : 0;
+    return s;
+}
+
+// Offset (within the segment) of this lane's first element in row u of its wave.
+__device__ __forceinline__ int64_t row_off(const Seg& s, int u) {
+    return (int64_t)(4 * u + s.w) * 128 + 2 * s.lane;
+}
+
+// Segment partials -> tickets -> group partial by the last-arriving workgroup.
+template <int K>
+__device__ __forceinline__ void reduce_publish(double (&acc)[K], const Geo& geo, const Red& red) {
+    __shared__ double lds[4][K];
+    __shared__ int last_flag;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+#pragma unroll
+    for (int k = 0; k < K; ++k) acc[k] = wave_sum(acc[k]);
+    if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) lds[w][k] = acc[k];
+    }
+    __syncthreads();
+    const int64_t b = blockIdx.x;
+    const int64_t sg = geo.seg_lo + b;
+    const int g = (int)(sg / LBK_SEG_PER_GROUP);
+    if (t == 0) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const double p = (lds[0][k] + lds[1][k]) + (lds[2][k] + lds[3][k]);
+            // write-through (sc1) store: visible to the last arriver's sc1 loads
+            __hip_atomic_store(reinterpret_cast<unsigned long long*>(red.partials + (int64_t)k * LBK_SEGS + b),
+                               dbits(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int64_t hi = min(geo.nseg, (int64_t)(g + 1) * LBK_SEG_PER_GROUP);
+        const unsigned expect = (unsigned)(hi - (int64_t)g * LBK_SEG_PER_GROUP);
+        const unsigned old = __hip_atomic_fetch_add(red.cnt + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last_flag = (old + 1u == expect);
+    }
+    __syncthreads();
+    if (!last_flag) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // stage 2: balanced tree over the group's 1024 segment partials (0.0 beyond nseg)
+    const int64_t gseg0 = (int64_t)g * LBK_SEG_PER_GROUP;
+    const int64_t lbase = gseg0 - geo.seg_lo;
+    double q[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        double p[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int64_t j = 4 * t + i;
+            p[i] = (gseg0 + j < geo.nseg)
+                       ? bitsd(__hip_atomic_load(reinterpret_cast<unsigned long long*>(
+                                                     red.partials + (int64_t)k * LBK_SEGS + lbase + j),
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                       : 0.0;
+        }
+        q[k] = wave_sum((p[0] + p[1]) + (p[2] + p[3]));
+    }
+    __syncthreads();  // lds reuse
+    if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) lds[w][k] = q[k];
+    }
+    __syncthreads();
+    if (t == 0) {
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            red.slot[g * LBK_KMAX + k] = (lds[0][k] + lds[1][k]) + (lds[2][k] + lds[3][k]);
+        __hip_atomic_store(red.cnt + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// Objectives (benchmark.cpp:58-81, :16-56; main.cpp:7-21), per element e with neighbours.
+// ---------------------------------------------------------------------------------------
+template <int OBJ>
+__device__ __forceinline__ double obj_term(double zc, double zp, bool has_p) {
+    if (OBJ == LBK_OBJ_ROSENBROCK) {
+        const double term1 = zp - zc * zc;
+        const double term2 = 1.0 - zc;
+        return 100.0 * term1 * term1 + term2 * term2;  // valid only when has_p
+    } else if (OBJ == LBK_OBJ_QUAD_TRIDIAG) {
+        const double dterm = 1000.0 * zc * zc;
+        return has_p ? dterm + 100.0 * zc * zp : dterm;
+    } else {
+        return (zc - 1.0) * (zc - 1.0);
+    }
+}
+// does element e contribute an f term?
+template <int OBJ>
+__device__ __forceinline__ bool obj_has_term(bool has_p) {
+    return OBJ == LBK_OBJ_ROSENBROCK ? has_p : true;
+}
+
+template <int OBJ>
+__device__ __forceinline__ double obj_grad(double zm, double zc, double zp, bool has_m, bool has_p) {
+    if (OBJ == LBK_OBJ_ROSENBROCK) {
+        double g = 0.0;
+        if (has_m) g = g + 200.0 * (zc - zm * zm);  // grad[i+1] += 200 term2 (first)
+        if (has_p) {
+            const double term1 = 2.0 * (zc - 1.0);
+            const double term2 = zp - zc * zc;
+            g = g + (term1 - 400.0 * zc * term2);    // grad[i] += term1 - 400 x term2
+        }
+        return g;
+    } else if (OBJ == LBK_OBJ_QUAD_TRIDIAG) {
+        double g = 2000.0 * zc;
+        if (has_m) g = g + 100.0 * zm;
+        if (has_p) g = g + 100.0 * zp;
+        return g;
+    } else {
+        return 2.0 * (zc - 1.0);
+    }
+}
+
+// Neighbour exchange inside a row: lane l holds z[2l], z[2l+1]; the halo value zh is
+// z[-1] on lane 0 and z[128] on lane 63.
+__device__ __forceinline__ void neighbours(double z0, double z1, double zh, int lane, double& zl, double& zr) {
+    zl = __shfl_up(z1, 1, 64);
+    zr = __shfl_down(z0, 1, 64);
+    if (lane == 0) zl = zh;
+    if (lane == 63) zr = zh;
+}
+
+// ---------------------------------------------------------------------------------------
+// Two-loop recursion passes
+// ---------------------------------------------------------------------------------------
+constexpr int U2 = 4;  // rows in flight per wave for the BLAS-1 passes
+
+__global__ __launch_bounds__(LB_BLOCK) void k_dot(const double* __restrict__ a, const double* __restrict__ b,
+                                                  Geo geo, Red red) {
+    const Seg s = seg_setup(geo);
+    double acc[1] = {0.0};
+    for (int u0 = 0; u0 < s.nrows; u0 += U2) {
+        double2 av[U2], bv[U2];
+#pragma unroll
+        for (int j = 0; j < U2; ++j) {
+            if (u0 + j < s.nrows) {
+                const int64_t i = s.lb + row_off(s, u0 + j);
+                av[j] = ld2(a + i);
+                bv[j] = ld2(b + i);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < U2; ++j) {
+            if (u0 + j < s.nrows) {
+                const int64_t o = row_off(s, u0 + j);
+                if (o < s.len) acc[0] = fma(av[j].x, bv[j].x, acc[0]);
+                if (o + 1 < s.len) acc[0] = fma(av[j].y, bv[j].y, acc[0]);
+            }
+        }
+    }
+    reduce_publish<1>(acc, geo, red);
+}
+
+// q = qin - alpha y;  acc += s . q     with alpha = rho * total(prev)
+__global__ __launch_bounds__(LB_BLOCK) void k_axpy_dot(double* qout, const double* qin, const double* __restrict__ y,
+                                                       const double* __restrict__ sv, double rho,
+                                                       const double* __restrict__ prev, Geo geo, Red red) {
+    const double alpha = rho * slot_total(prev);
+    const Seg s = seg_setup(geo);
+    double acc[1] = {0.0};
+    for (int u0 = 0; u0 < s.nrows; u0 += U2) {
+        double2 qv[U2], yv[U2], ss[U2];
+#pragma unroll
+        for (int j = 0; j < U2; ++j) {
+            if (u0 + j < s.nrows) {
+                const int64_t i = s.lb + row_off(s, u0 + j);
+                qv[j] = ld2(qin + i);
+                yv[j] = ld2(y + i);
+                ss[j] = ld2(sv + i);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < U2; ++j) {
+            if (u0 + j < s.nrows) {
+                const int64_t o = row_off(s, u0 + j);
+                const bool v0 = o < s.len, v1 = o + 1 < s.len;
+                double2 qn;
+                qn.x = qv[j].x - alpha * yv[j].x;
+                qn.y = qv[j].y - alpha * yv[j].y;
+                st2m(qout + s.lb + o, qn, v0, v1);
+                if (v0) acc[0] = fma(ss[j].x, qn.x, acc[0]);
+                if (v1) acc[0] = fma(ss[j].y, qn.y, acc[0]);
+            }
+        }
+    }
+    reduce_publish<1>(acc, geo, red);
+}
+
+// r = (qin - alpha0 y0) * gamma;  acc += y0 . r
+__global__ __launch_bounds__(LB_BLOCK) void k_mid(double* __restrict__ rout, const double* __restrict__ qin,
+                                                  const double* __restrict__ y0, double rho0, double gamma,
+                                                  const double* __restrict__ prev, Geo geo, Red red) {
+    const double alpha = rho0 * slot_total(prev);
+    const Seg s = seg_setup(geo);
+    double acc[1] = {0.0};
+    for (int u0 = 0; u0 < s.nrows; u0 += U2) {
+        double2 qv[U2], yv[U2];
+#pragma unroll
+        for (int j = 0; j < U2; ++j) {
+            if (u0 + j < s.nrows) {
+                const int64_t i = s.lb + row_off(s, u0 + j);
+                qv[j] = ld2(qin + i);
+                yv[j] = ld2(y0 + i);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < U2; ++j) {
+            if (u0 + j < s.nrows) {
+                const int64_t o = row_off(s, u0 + j);
+                const bool v0 = o < s.len, v1 = o + 1 < s.len;
+                double2 r;
+                r.x = (qv[j].x - alpha * yv[j].x) * gamma;
+                r.y = (qv[j].y - alpha * yv[j].y) * gamma;
+                st2m(rout + s.lb + o, r, v0, v1);
+                if (v0) acc[0] = fma(yv[j].x, r.x, acc[0]);
+                if (v1) acc[0] = fma(yv[j].y, r.y, acc[0]);
+            }
+        }
+    }
+    reduce_publish<1>(acc, geo, red);
+}
+
+// r += s (alpha - beta);  acc += ynext . r    beta = rho*total(pb), alpha = rho*total(pa)
+__global__ __launch_bounds__(LB_BLOCK) void k_axpy2_dot(double* r, const double* __restrict__ sv,
+                                                        const double* __restrict__ yn, double rho,
+                                                        const double* __restrict__ pb, const double* __restrict__ pa,
+                                                        Geo geo, Red red) {
+    const double beta = rho * slot_total(pb);
+    const double alpha = rho * slot_total(pa);
+    const double coef = alpha - beta;
+    const Seg s = seg_setup(geo);
+    double acc[1] = {0.0};
+    for (int u0 = 0; u0 < s.nrows; u0 += U2) {
+        double2 rv[U2], ss[U2], yv[U2];
+#pragma unroll
+        for (int j = 0; j < U2; ++j) {
+            if (u0 + j < s.nrows) {
+                const int64_t i = s.lb + row_off(s, u0 + j);
+                rv[j] = ld2(r + i);
+                ss[j] = ld2(sv + i);
+                yv[j] = ld2(yn + i);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < U2; ++j) {
+            if (u0 + j < s.nrows) {
+                const int64_t o = row_off(s, u0 + j);
+                const bool v0 = o < s.len, v1 = o + 1 < s.len;
+                double2 rn;
+                rn.x = rv[j].x + ss[j].x * coef;
+                rn.y = rv[j].y + ss[j].y * coef;
+                st2m(r + s.lb + o, rn, v0, v1);
+                if (v0) acc[0] = fma(yv[j].x, rn.x, acc[0]);
+                if (v1) acc[0] = fma(yv[j].y, rn.y, acc[0]);
+            }
+        }
+    }
+    reduce_publish<1>(acc, geo, red);
+}
+
+// d = -(r + s (alpha - beta));  acc += g . d
+__global__ __launch_bounds__(LB_BLOCK) void k_last(double* __restrict__ dout, const double* __restrict__ r,
+                                                   const double* __restrict__ sv, const double* __restrict__ g,
+                                                   double rho, const double* __restrict__ pb,
+                                                   const double* __restrict__ pa, Geo geo, Red red) {
+    const double beta = rho * slot_total(pb);
+    const double alpha = rho * slot_total(pa);
+    const double coef = alpha - beta;
+    const Seg s = seg_setup(geo);
+    double acc[1] = {0.0};
+    for (int u0 = 0; u0 < s.nrows; u0 += U2) {
+        double2 rv[U2], ss[U2], gv[U2];
+#pragma unroll
+        for (int j = 0; j < U2; ++j) {
+            if (u0 + j < s.nrows) {
+                const int64_t i = s.lb + row_off(s, u0 + j);
+                rv[j] = ld2(r + i);
+                ss[j] = ld2(sv + i);
+                gv[j] = ld2(g + i);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < U2; ++j) {
+            if (u0 + j < s.nrows) {
+                const int64_t o = row_off(s, u0 + j);
+                const bool v0 = o < s.len, v1 = o + 1 < s.len;
+                double2 d;
+                d.x = -(rv[j].x + ss[j].x * coef);
+                d.y = -(rv[j].y + ss[j].y * coef);
+                st2m(dout + s.lb + o, d, v0, v1);
+                if (v0) acc[0] = fma(gv[j].x, d.x, acc[0]);
+                if (v1) acc[0] = fma(gv[j].y, d.y, acc[0]);
+            }
+        }
+    }
+    reduce_publish<1>(acc, geo, red);
+}
+
+// d = -g;  acc += g . d
+__global__ __launch_bounds__(LB_BLOCK) void k_negdot(double* __restrict__ dout, const double* __restrict__ g,
+                                                     Geo geo, Red red) {
+    const Seg s = seg_setup(geo);
+    double acc[1] = {0.0};
+    for (int u0 = 0; u0 < s.nrows; u0 += U2) {
+        double2 gv[U2];
+#pragma unroll
+        for (int j = 0; j < U2; ++j)
+            if (u0 + j < s.nrows) gv[j] = ld2(g + s.lb + row_off(s, u0 + j));
+#pragma unroll
+        for (int j = 0; j < U2; ++j) {
+            if (u0 + j < s.nrows) {
+                const int64_t o = row_off(s, u0 + j);
+                const bool v0 = o < s.len, v1 = o + 1 < s.len;
+                double2 d;
+                d.x = -gv[j].x;
+                d.y = -gv[j].y;
+                st2m(dout + s.lb + o, d, v0, v1);
+                if (v0) acc[0] = fma(gv[j].x, d.x, acc[0]);
+                if (v1) acc[0] = fma(gv[j].y, d.y, acc[0]);
+            }
+        }
+    }
+    reduce_publish<1>(acc, geo, red);
+}
+
+// ---------------------------------------------------------------------------------------
+// Objective passes: evaluation point z = x + alpha d with d given by DMODE.
+// ---------------------------------------------------------------------------------------
+struct DirArgs {
+    const double* dsrc;  // D_BUF: d;  D_TWOLOOP: r
+    const double* s;     // D_TWOLOOP: s_{h-1}
+    const double* g;     // D_NEG_G / commit: g
+    double coef;         // D_TWOLOOP: alpha - beta (formed on the device, see k_commit)
+    const double* pa;    // D_TWOLOOP: slot of s_{h-1} . q   (alpha = rho * total)
+    const double* pb;    // D_TWOLOOP: slot of y_{h-1} . r   (beta  = rho * total)
+    double rho;
+};
+
+template <int DMODE>
+__device__ __forceinline__ double2 load_dir(const DirArgs& da, int64_t i, double2 gv) {
+    double2 d;
+    if (DMODE == LBK_D_BUF) {
+        d = ld2(da.dsrc + i);
+    } else if (DMODE == LBK_D_NEG_G) {
+        d.x = -gv.x;
+        d.y = -gv.y;
+    } else {
+        const double2 rv = ld2(da.dsrc + i);
+        const double2 sv = ld2(da.s + i);
+        d.x = -(rv.x + sv.x * da.coef);
+        d.y = -(rv.y + sv.y * da.coef);
+    }
+    return d;
+}
+template <int DMODE>
+__device__ __forceinline__ double load_dir1(const DirArgs& da, int64_t i) {
+    if (DMODE == LBK_D_BUF) return da.dsrc[i];
+    if (DMODE == LBK_D_NEG_G) return -da.g[i];
+    return -(da.dsrc[i] + da.s[i] * da.coef);
+}
+
+constexpr int UO = 2;  // rows in flight per wave for the objective passes
+
+// Evaluate f (and optionally g) at z = x + alpha*d.
+//   EVAL mode (NO_DIR): z = x; reductions: f, g.g     (lbfgs.cpp:29-30)
+//   TRIAL mode: reductions f, g_t . d                  (line_search.cpp)
+template <int OBJ, bool NO_DIR, bool WITH_G>
+__global__ __launch_bounds__(LB_BLOCK) void k_objective(const double* __restrict__ x, DirArgs da, double alpha,
+                                                        double* __restrict__ gout, Geo geo, Red red) {
+    const Seg s = seg_setup(geo);
+    double acc[2] = {0.0, 0.0};
+    const int64_t n = geo.n;
+    for (int u0 = 0; u0 < s.nrows; u0 += UO) {
+        double2 z[UO], dd[UO];
+        double zh[UO];
+#pragma unroll
+        for (int j = 0; j < UO; ++j) {
+            if (u0 + j < s.nrows) {
+                const int64_t i = s.lb + row_off(s, u0 + j);
+                const double2 xv = ld2(x + i);
+                if (NO_DIR) {
+                    z[j] = xv;
+                } else {
+                    dd[j] = load_dir<LBK_D_BUF>(da, i, xv);
+                    z[j].x = xv.x + alpha * dd[j].x;
+                    z[j].y = xv.y + alpha * dd[j].y;
+                }
+                zh[j] = 0.0;
+                if (OBJ != LBK_OBJ_QUAD_SEPARABLE && (s.lane == 0 || s.lane == 63)) {
+                    const int64_t hi = (s.lane == 0) ? i - 1 : i + 2;
+                    if (hi >= -1 && hi <= geo.n_loc) {
+                        zh[j] = NO_DIR ? x[hi] : x[hi] + alpha * load_dir1<LBK_D_BUF>(da, hi);
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < UO; ++j) {
+            if (u0 + j < s.nrows) {
+                const int64_t o = row_off(s, u0 + j);
+                const int64_t e0 = s.sbeg + o;
+                const bool v0 = o < s.len, v1 = o + 1 < s.len;
+                double zl, zr;
+                neighbours(z[j].x, z[j].y, zh[j], s.lane, zl, zr);
+                // element e0: (zl, z.x, z.y); element e0+1: (z.x, z.y, zr)
+                const bool p0 = e0 + 1 < n, p1 = e0 + 2 < n;
+                const bool m0 = e0 > 0;
+                if (v0 && obj_has_term<OBJ>(p0)) acc[0] = acc[0] + obj_term<OBJ>(z[j].x, z[j].y, p0);
+                if (v1 && obj_has_term<OBJ>(p1)) acc[0] = acc[0] + obj_term<OBJ>(z[j].y, zr, p1);
+                if (WITH_G) {
+                    double2 gv;
+                    gv.x = obj_grad<OBJ>(zl, z[j].x, z[j].y, m0, p0);
+                    gv.y = obj_grad<OBJ>(z[j].x, z[j].y, zr, true, p1);
+                    if (gout) st2m(gout + s.lb + o, gv, v0, v1);
+                    if (NO_DIR) {
+                        if (v0) acc[1] = fma(gv.x, gv.x, acc[1]);
+                        if (v1) acc[1] = fma(gv.y, gv.y, acc[1]);
+                    } else {
+                        if (v0) acc[1] = fma(gv.x, dd[j].x, acc[1]);
+                        if (v1) acc[1] = fma(gv.y, dd[j].y, acc[1]);
+                    }
+                }
+            }
+        }
+    }
+    reduce_publish<2>(acc, geo, red);
+}
+
+// The commit: d per DMODE, x_new = x + alpha d, f(x_new), g_new = grad f(x_new) (or read
+// from gn for OBJ == NONE), s = x_new - x, y = g_new - g, and the dots
+//   [GD] g.d  [F] f  [SY] s.y  [YY] y.y  [GG] g_new.g_new  [SG] s.g_new  [DPHI] g_new.d
+template <int OBJ, int DMODE>
+__global__ __launch_bounds__(LB_BLOCK) void k_commit(const double* __restrict__ x, DirArgs da, double alpha,
+                                                     double* __restrict__ xn, double* __restrict__ gn,
+                                                     double* __restrict__ so, double* __restrict__ yo,
+                                                     Geo geo, Red red) {
+    if (DMODE == LBK_D_TWOLOOP) {
+        const double beta = da.rho * slot_total(da.pb);
+        const double alph = da.rho * slot_total(da.pa);
+        da.coef = alph - beta;  // r[j] += s[j] * (alpha[i] - beta)  (lbfgs.cpp:137)
+    }
+    const Seg s = seg_setup(geo);
+    double acc[7] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    const int64_t n = geo.n;
+    const double* __restrict__ g = da.g;
+    for (int u0 = 0; u0 < s.nrows; u0 += UO) {
+        double2 xv[UO], gv[UO], dd[UO], z[UO], gx[UO];
+        double zh[UO];
+#pragma unroll
+        for (int j = 0; j < UO; ++j) {
+            if (u0 + j < s.nrows) {
+                const int64_t i = s.lb + row_off(s, u0 + j);
+                xv[j] = ld2(x + i);
+                gv[j] = ld2(g + i);
+                dd[j] = load_dir<DMODE>(da, i, gv[j]);
+                if (OBJ == LBK_OBJ_NONE) gx[j] = ld2(gn + i);
+                z[j].x = xv[j].x + alpha * dd[j].x;
+                z[j].y = xv[j].y + alpha * dd[j].y;
+                zh[j] = 0.0;
+                if (OBJ != LBK_OBJ_NONE && OBJ != LBK_OBJ_QUAD_SEPARABLE && (s.lane == 0 || s.lane == 63)) {
+                    const int64_t hi = (s.lane == 0) ? i - 1 : i + 2;
+                    if (hi >= -1 && hi <= geo.n_loc) zh[j] = x[hi] + alpha * load_dir1<DMODE>(da, hi);
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < UO; ++j) {
+            if (u0 + j < s.nrows) {
+                const int64_t o = row_off(s, u0 + j);
+                const int64_t e0 = s.sbeg + o;
+                const int64_t i = s.lb + o;
+                const bool v0 = o < s.len, v1 = o + 1 < s.len;
+                double2 g2;
+                if (OBJ == LBK_OBJ_NONE) {
+                    g2 = gx[j];
+                } else {
+                    double zl, zr;
+                    neighbours(z[j].x, z[j].y, zh[j], s.lane, zl, zr);
+                    const bool p0 = e0 + 1 < n, p1 = e0 + 2 < n;
+                    if (v0 && obj_has_term<OBJ>(p0)) acc[LBK_C_F] = acc[LBK_C_F] + obj_term<OBJ>(z[j].x, z[j].y, p0);
+                    if (v1 && obj_has_term<OBJ>(p1)) acc[LBK_C_F] = acc[LBK_C_F] + obj_term<OBJ>(z[j].y, zr, p1);
+                    g2.x = obj_grad<OBJ>(zl, z[j].x, z[j].y, e0 > 0, p0);
+                    g2.y = obj_grad<OBJ>(z[j].x, z[j].y, zr, true, p1);
+                    st2m(gn + i, g2, v0, v1);
+                }
+                st2m(xn + i, z[j], v0, v1);
+                double2 sv, yv;
+                sv.x = z[j].x - xv[j].x;
+                sv.y = z[j].y - xv[j].y;
+                yv.x = g2.x - gv[j].x;
+                yv.y = g2.y - gv[j].y;
+                st2m(so + i, sv, v0, v1);
+                st2m(yo + i, yv, v0, v1);
+                if (v0) {
+                    acc[LBK_C_GD] = fma(gv[j].x, dd[j].x, acc[LBK_C_GD]);
+                    acc[LBK_C_SY] = fma(sv.x, yv.x, acc[LBK_C_SY]);
+                    acc[LBK_C_YY] = fma(yv.x, yv.x, acc[LBK_C_YY]);
+                    acc[LBK_C_GG] = fma(g2.x, g2.x, acc[LBK_C_GG]);
+                    acc[LBK_C_SG] = fma(sv.x, g2.x, acc[LBK_C_SG]);
+                    acc[LBK_C_DPHI] = fma(g2.x, dd[j].x, acc[LBK_C_DPHI]);
+                }
+                if (v1) {
+                    acc[LBK_C_GD] = fma(gv[j].y, dd[j].y, acc[LBK_C_GD]);
+                    acc[LBK_C_SY] = fma(sv.y, yv.y, acc[LBK_C_SY]);
+                    acc[LBK_C_YY] = fma(yv.y, yv.y, acc[LBK_C_YY]);
+                    acc[LBK_C_GG] = fma(g2.y, g2.y, acc[LBK_C_GG]);
+                    acc[LBK_C_SG] = fma(sv.y, g2.y, acc[LBK_C_SG]);
+                    acc[LBK_C_DPHI] = fma(g2.y, dd[j].y, acc[LBK_C_DPHI]);
+                }
+            }
+        }
+    }
+    reduce_publish<7>(acc, geo, red);
+}
+
+// z = x + alpha d over the whole local range incl. ghosts (host-callback objectives)
+__global__ void k_point(double* __restrict__ z, const double* __restrict__ x, const double* __restrict__ d,
+                        double alpha, int64_t lo, int64_t hi) {
+    const int64_t i = lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < hi) z[i] = x[i] + alpha * d[i];
+}
+
+// integer checksums of the bit patterns (exact in any order)
+__global__ void k_checksum(const double* __restrict__ x, int64_t n_loc, int64_t elem_lo,
+                           unsigned long long* out) {
+    unsigned long long a = 0, b = 0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_loc;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const unsigned long long u = dbits(x[i]);
+        a += u;
+        b += (unsigned long long)(elem_lo + i + 1) * u;
+    }
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) {
+        a += __shfl_xor(a, m, 64);
+        b += __shfl_xor(b, m, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(out, a);
+        atomicAdd(out + 1, b);
+    }
+}
+
+}  // namespace
+
+// =========================================================================================
+// Host side of the device layer
+// =========================================================================================
+struct lbk_ctx {
+    lbk_geo geo;
+    int device;
+    hipStream_t stream;
+    double* partials;   // LBK_KMAX * LBK_SEGS
+    unsigned* cnt;      // LBK_GROUPS
+    double* slots;      // LBK_NSLOTS * LBK_SLOT
+    double* h_slots;    // pinned mirror
+    unsigned long long* d_ck;
+    unsigned long long* h_ck;
+    int64_t vec_doubles;  // allocation per vector
+    ncclComm_t comm;
+    char err[256];
+    // profiling
+    int prof_on;
+    std::vector<hipEvent_t> ev_free;
+    struct Pending {
+        int kind;
+        hipEvent_t a, b;
+        double bytes;
+    };
+    std::vector<Pending> pending;
+    double prof_ms[LBK_K_COUNT];
+    int64_t prof_n[LBK_K_COUNT];
+    double prof_bytes[LBK_K_COUNT];
+    double bytes_total;
+};
+
+namespace {
+
+#define HIPCHK(c, expr)                                                                      \
+    do {                                                                                     \
+        hipError_t e_ = (expr);                                                              \
+        if (e_ != hipSuccess) {                                                              \
+            snprintf((c)->err, sizeof((c)->err), "%s:%d %s: %s", __FILE__, __LINE__, #expr, \
+                     hipGetErrorString(e_));                                                 \
+            return -2;                                                                       \
+        }                                                                                    \
+    } while (0)
+
+Geo kgeo(const lbk_ctx* c) {
+    Geo g;
+    g.n = c->geo.n;
+    g.L = c->geo.L;
+    g.nseg = c->geo.nseg;
+    g.seg_lo = c->geo.seg_lo;
+    g.elem_lo = c->geo.elem_lo;
+    g.n_loc = c->geo.n_loc;
+    g.g_lo = c->geo.g_lo;
+    return g;
+}
+
+Red kred(const lbk_ctx* c, int slot) {
+    Red r;
+    r.partials = c->partials;
+    r.cnt = c->cnt;
+    r.slot = c->slots + (int64_t)slot * LBK_SLOT;
+    return r;
+}
+
+const double* sref(const lbk_ctx* c, int ref) {
+    return c->slots + (int64_t)(ref / LBK_KMAX) * LBK_SLOT + (ref % LBK_KMAX);
+}
+
+int nblocks(const lbk_ctx* c) { return (int)(c->geo.seg_hi - c->geo.seg_lo); }
+
+hipEvent_t ev_get(lbk_ctx* c) {
+    if (!c->ev_free.empty()) {
+        hipEvent_t e = c->ev_free.back();
+        c->ev_free.pop_back();
+        return e;
+    }
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+
+int prof_flush(lbk_ctx* c) {
+    for (auto& p : c->pending) {
+        float ms = 0.f;
+        HIPCHK(c, hipEventSynchronize(p.b));
+        HIPCHK(c, hipEventElapsedTime(&ms, p.a, p.b));
+        c->prof_ms[p.kind] += ms;
+        c->prof_n[p.kind] += 1;
+        c->prof_bytes[p.kind] += p.bytes;
+        c->ev_free.push_back(p.a);
+        c->ev_free.push_back(p.b);
+    }
+    c->pending.clear();
+    return 0;
+}
+
+// launch wrapper: byte accounting, optional event timing, all-gather of group partials
+template <class F>
+int launch(lbk_ctx* c, int kind, double vec_passes, int slot, F&& fn) {
+    const double bytes = vec_passes * 8.0 * (double)c->geo.n_loc;
+    c->bytes_total += bytes;
+    hipEvent_t a = nullptr, b = nullptr;
+    if (c->prof_on) {
+        if (c->pending.size() > 4096 && prof_flush(c) != 0) return -2;
+        a = ev_get(c);
+        b = ev_get(c);
+        if (a) HIPCHK(c, hipEventRecord(a, c->stream));
+    }
+    if (nblocks(c) > 0) {
+        fn();
+        HIPCHK(c, hipGetLastError());
+    }
+    if (c->prof_on && a && b) {
+        HIPCHK(c, hipEventRecord(b, c->stream));
+        c->pending.push_back({kind, a, b, bytes});
+    }
+    if (c->geo.world > 1 && slot >= 0) {
+        // each rank owns groups [g_lo, g_hi): gather them so every rank holds all 8
+        const int per = (c->geo.g_hi - c->geo.g_lo) * LBK_KMAX;
+        double* base = c->slots + (int64_t)slot * LBK_SLOT;
+        ncclResult_t r = ncclAllGather(base + c->geo.g_lo * LBK_KMAX, base, (size_t)per, ncclDouble, c->comm, c->stream);
+        if (r != ncclSuccess) {
+            snprintf(c->err, sizeof c->err, "ncclAllGather: %s", ncclGetErrorString(r));
+            return -3;
+        }
+    }
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int lbk_unique_id(void* out128) {
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return -3;
+    memcpy(out128, &id, sizeof id);
+    return 0;
+}
+
+int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const void* nccl_id) {
+    *out = nullptr;
+    if (n < 1 || world < 1 || (LBK_GROUPS % world) != 0 || rank < 0 || rank >= world) return -1;
+    lbk_ctx* c = new (std::nothrow) lbk_ctx();
+    if (!c) return -4;
+    c->device = device;
+    lbk_geo& G = c->geo;
+    G.n = n;
+    const int64_t per = (n + LBK_SEGS - 1) / LBK_SEGS;
+    G.L = ((per + 511) / 512) * 512;
+    if (G.L < 512) G.L = 512;
+    G.nseg = (n + G.L - 1) / G.L;
+    G.rank = rank;
+    G.world = world;
+    G.g_lo = rank * (LBK_GROUPS / world);
+    G.g_hi = (rank + 1) * (LBK_GROUPS / world);
+    G.seg_lo = std::min<int64_t>((int64_t)G.g_lo * LBK_SEG_PER_GROUP, G.nseg);
+    G.seg_hi = std::min<int64_t>((int64_t)G.g_hi * LBK_SEG_PER_GROUP, G.nseg);
+    G.elem_lo = std::min<int64_t>(G.seg_lo * G.L, n);
+    const int64_t elem_hi = std::min<int64_t>(G.seg_hi * G.L, n);
+    G.n_loc = elem_hi - G.elem_lo;
+    // front pad 2 (ghost at -1, 16-B alignment of element 0), back: whole rows + halo
+    c->vec_doubles = 2 + ((G.n_loc + 511) / 512) * 512 + 512;
+    *out = c;
+#define CK(expr)                                                                             \
+    do {                                                                                     \
+        hipError_t e_ = (expr);                                                              \
+        if (e_ != hipSuccess) {                                                              \
+            snprintf(c->err, sizeof c->err, "%s: %s", #expr, hipGetErrorString(e_));        \
+            return -2;                                                                       \
+        }                                                                                    \
+    } while (0)
+    CK(hipSetDevice(device));
+    CK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    CK(hipMalloc(&c->partials, sizeof(double) * LBK_KMAX * LBK_SEGS));
+    CK(hipMalloc(&c->cnt, sizeof(unsigned) * 16));
+    CK(hipMalloc(&c->slots, sizeof(double) * LBK_NSLOTS * LBK_SLOT));
+    CK(hipHostMalloc(&c->h_slots, sizeof(double) * LBK_NSLOTS * LBK_SLOT, hipHostMallocDefault));
+    CK(hipMalloc(&c->d_ck, 2 * sizeof(unsigned long long)));
+    CK(hipHostMalloc(&c->h_ck, 2 * sizeof(unsigned long long), hipHostMallocDefault));
+    CK(hipMemset(c->partials, 0, sizeof(double) * LBK_KMAX * LBK_SEGS));
+    CK(hipMemset(c->cnt, 0, sizeof(unsigned) * 16));
+    CK(hipMemset(c->slots, 0, sizeof(double) * LBK_NSLOTS * LBK_SLOT));
+    CK(hipDeviceSynchronize());
+#undef CK
+    if (world > 1) {
+        ncclUniqueId id;
+        memcpy(&id, nccl_id, sizeof id);
+        ncclResult_t r = ncclCommInitRank(&c->comm, world, id, rank);
+        if (r != ncclSuccess) {
+            snprintf(c->err, sizeof c->err, "ncclCommInitRank: %s", ncclGetErrorString(r));
+            return -3;
+        }
+    }
+    return 0;
+}
+
+void lbk_destroy(lbk_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    prof_flush(c);
+    for (auto e : c->ev_free) (void)hipEventDestroy(e);
+    if (c->comm) ncclCommDestroy(c->comm);
+    (void)hipFree(c->partials);
+    (void)hipFree(c->cnt);
+    (void)hipFree(c->slots);
+    (void)hipHostFree(c->h_slots);
+    (void)hipFree(c->d_ck);
+    (void)hipHostFree(c->h_ck);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+const lbk_geo* lbk_geometry(const lbk_ctx* c) { return &c->geo; }
+const char* lbk_last_error(const lbk_ctx* c) { return c ? c->err : "no context"; }
+
+double* lbk_vec_alloc(lbk_ctx* c) {
+    double* p = nullptr;
+    if (hipMalloc(&p, sizeof(double) * c->vec_doubles) != hipSuccess) {
+        snprintf(c->err, sizeof c->err, "hipMalloc of %lld doubles failed", (long long)c->vec_doubles);
+        return nullptr;
+    }
+    if (hipMemsetAsync(p, 0, sizeof(double) * c->vec_doubles, c->stream) != hipSuccess) {
+        (void)hipFree(p);
+        return nullptr;
+    }
+    return p + 2;
+}
+
+void lbk_vec_free(lbk_ctx* c, double* v) {
+    (void)c;
+    if (v) (void)hipFree(v - 2);
+}
+
+int lbk_upload(lbk_ctx* c, double* dst, const double* host_global) {
+    // local range plus the ghosts that exist globally
+    const int64_t lo = c->geo.elem_lo > 0 ? c->geo.elem_lo - 1 : 0;
+    const int64_t hi = std::min<int64_t>(c->geo.elem_lo + c->geo.n_loc + 1, c->geo.n);
+    if (hi <= lo) return 0;
+    HIPCHK(c, hipMemcpyAsync(dst + (lo - c->geo.elem_lo), host_global + lo, sizeof(double) * (hi - lo),
+                             hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+int lbk_upload_local(lbk_ctx* c, double* dst, const double* host_local) {
+    if (c->geo.n_loc == 0) return 0;
+    HIPCHK(c, hipMemcpyAsync(dst, host_local, sizeof(double) * c->geo.n_loc, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+int lbk_download(lbk_ctx* c, double* host_global, const double* src) {
+    return lbk_download_local(c, host_global + c->geo.elem_lo, src);
+}
+
+int lbk_download_local(lbk_ctx* c, double* host_local, const double* src) {
+    if (c->geo.n_loc == 0) return 0;
+    HIPCHK(c, hipMemcpyAsync(host_local, src, sizeof(double) * c->geo.n_loc, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+int lbk_copy(lbk_ctx* c, double* dst, const double* src) {
+    HIPCHK(c, hipMemcpyAsync(dst - 1, src - 1, sizeof(double) * (c->geo.n_loc + 2), hipMemcpyDeviceToDevice,
+                             c->stream));
+    return 0;
+}
+
+int lbk_dot(lbk_ctx* c, const double* a, const double* b, int slot) {
+    Geo g = kgeo(c);
+    Red r = kred(c, slot);
+    return launch(c, LBK_K_DOT, 2, slot, [&] {
+        hipLaunchKernelGGL(k_dot, dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, a, b, g, r);
+    });
+}
+
+int lbk_axpy_dot(lbk_ctx* c, double* qout, const double* qin, const double* y, const double* s, double rho,
+                 int ref_alpha, int slot) {
+    Geo g = kgeo(c);
+    Red r = kred(c, slot);
+    const double* pa = sref(c, ref_alpha);
+    return launch(c, LBK_K_AXPY_DOT, 4, slot, [&] {
+        hipLaunchKernelGGL(k_axpy_dot, dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, qout, qin, y, s, rho, pa, g, r);
+    });
+}
+
+int lbk_mid(lbk_ctx* c, double* rout, const double* qin, const double* y0, double rho0, double gamma,
+            int ref_alpha, int slot) {
+    Geo g = kgeo(c);
+    Red r = kred(c, slot);
+    const double* pa = sref(c, ref_alpha);
+    return launch(c, LBK_K_MID, 3, slot, [&] {
+        hipLaunchKernelGGL(k_mid, dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, rout, qin, y0, rho0, gamma, pa, g, r);
+    });
+}
+
+int lbk_axpy2_dot(lbk_ctx* c, double* rr, const double* s, const double* ynext, double rho, int ref_beta,
+                  int ref_alpha, int slot) {
+    Geo g = kgeo(c);
+    Red r = kred(c, slot);
+    const double* pb = sref(c, ref_beta);
+    const double* pa = sref(c, ref_alpha);
+    return launch(c, LBK_K_AXPY2_DOT, 4, slot, [&] {
+        hipLaunchKernelGGL(k_axpy2_dot, dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, rr, s, ynext, rho, pb, pa, g, r);
+    });
+}
+
+int lbk_last(lbk_ctx* c, double* dout, const double* rr, const double* s, const double* gg, double rho,
+             int ref_beta, int ref_alpha, int slot) {
+    Geo g = kgeo(c);
+    Red r = kred(c, slot);
+    const double* pb = sref(c, ref_beta);
+    const double* pa = sref(c, ref_alpha);
+    return launch(c, LBK_K_LAST, 4, slot, [&] {
+        hipLaunchKernelGGL(k_last, dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, dout, rr, s, gg, rho, pb, pa, g, r);
+    });
+}
+
+int lbk_negdot(lbk_ctx* c, double* dout, const double* gg, int slot) {
+    Geo g = kgeo(c);
+    Red r = kred(c, slot);
+    return launch(c, LBK_K_NEGDOT, 2, slot, [&] {
+        hipLaunchKernelGGL(k_negdot, dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, dout, gg, g, r);
+    });
+}
+
+#define OBJ_DISPATCH(obj, TEMPLATE_CALL)                                      \
+    switch (obj) {                                                            \
+        case LBK_OBJ_ROSENBROCK: { constexpr int O_ = LBK_OBJ_ROSENBROCK; TEMPLATE_CALL; } break;         \
+        case LBK_OBJ_QUAD_TRIDIAG: { constexpr int O_ = LBK_OBJ_QUAD_TRIDIAG; TEMPLATE_CALL; } break;     \
+        case LBK_OBJ_QUAD_SEPARABLE: { constexpr int O_ = LBK_OBJ_QUAD_SEPARABLE; TEMPLATE_CALL; } break; \
+        default: return -1;                                                   \
+    }
+
+int lbk_eval(lbk_ctx* c, int obj, const double* x, double* gout, int slot) {
+    Geo g = kgeo(c);
+    Red r = kred(c, slot);
+    DirArgs da = {nullptr, nullptr, nullptr, 0.0, nullptr, nullptr, 0.0};
+    return launch(c, LBK_K_EVAL, gout ? 2 : 1, slot, [&] {
+        OBJ_DISPATCH(obj, hipLaunchKernelGGL((k_objective<O_, true, true>), dim3(nblocks(c)), dim3(LB_BLOCK), 0,
+                                             c->stream, x, da, 0.0, gout, g, r));
+        return 0;
+    });
+}
+
+int lbk_trial(lbk_ctx* c, int obj, const double* x, const double* d, double alpha, double* gout, int slot) {
+    Geo g = kgeo(c);
+    Red r = kred(c, slot);
+    DirArgs da = {d, nullptr, nullptr, 0.0, nullptr, nullptr, 0.0};
+    const int kind = gout ? LBK_K_TRIAL_FG : LBK_K_TRIAL_F;
+    return launch(c, kind, gout ? 3 : 2, slot, [&] {
+        if (gout) {
+            OBJ_DISPATCH(obj, hipLaunchKernelGGL((k_objective<O_, false, true>), dim3(nblocks(c)), dim3(LB_BLOCK),
+                                                 0, c->stream, x, da, alpha, gout, g, r));
+        } else {
+            OBJ_DISPATCH(obj, hipLaunchKernelGGL((k_objective<O_, false, false>), dim3(nblocks(c)), dim3(LB_BLOCK),
+                                                 0, c->stream, x, da, alpha, gout, g, r));
+        }
+        return 0;
+    });
+}
+
+int lbk_commit(lbk_ctx* c, int obj, int dmode, const double* x, const double* dsrc, const double* s_last,
+               const double* gg, double rho, int ref_beta, int ref_alpha, double alpha, double* xn, double* gn,
+               double* s_out, double* y_out, int slot) {
+    Geo g = kgeo(c);
+    Red r = kred(c, slot);
+    DirArgs da = {dsrc, s_last, gg, 0.0, nullptr, nullptr, rho};
+    if (dmode == LBK_D_TWOLOOP) {
+        da.pa = sref(c, ref_alpha);
+        da.pb = sref(c, ref_beta);
+    }
+    double passes = 4.0 + (dmode == LBK_D_BUF ? 3.0 : dmode == LBK_D_NEG_G ? 2.0 : 4.0);
+    return launch(c, LBK_K_COMMIT, passes, slot, [&] {
+        if (obj == LBK_OBJ_NONE) {
+            switch (dmode) {
+                case LBK_D_BUF: hipLaunchKernelGGL((k_commit<LBK_OBJ_NONE, LBK_D_BUF>), dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, x, da, alpha, xn, gn, s_out, y_out, g, r); break;
+                case LBK_D_NEG_G: hipLaunchKernelGGL((k_commit<LBK_OBJ_NONE, LBK_D_NEG_G>), dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, x, da, alpha, xn, gn, s_out, y_out, g, r); break;
+                default: hipLaunchKernelGGL((k_commit<LBK_OBJ_NONE, LBK_D_TWOLOOP>), dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, x, da, alpha, xn, gn, s_out, y_out, g, r); break;
+            }
+            return 0;
+        }
+        switch (dmode) {
+            case LBK_D_BUF:
+                OBJ_DISPATCH(obj, hipLaunchKernelGGL((k_commit<O_, LBK_D_BUF>), dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, x, da, alpha, xn, gn, s_out, y_out, g, r));
+                break;
+            case LBK_D_NEG_G:
+                OBJ_DISPATCH(obj, hipLaunchKernelGGL((k_commit<O_, LBK_D_NEG_G>), dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, x, da, alpha, xn, gn, s_out, y_out, g, r));
+                break;
+            default:
+                OBJ_DISPATCH(obj, hipLaunchKernelGGL((k_commit<O_, LBK_D_TWOLOOP>), dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, x, da, alpha, xn, gn, s_out, y_out, g, r));
+                break;
+        }
+        return 0;
+    });
+}
+
+int lbk_point(lbk_ctx* c, double* z, const double* x, const double* d, double alpha) {
+    const int64_t lo = -1, hi = c->geo.n_loc + 1;
+    const int64_t cnt = hi - lo;
+    const int nb = (int)((cnt + 255) / 256);
+    return launch(c, LBK_K_POINT, 3, -1, [&] {
+        hipLaunchKernelGGL(k_point, dim3(nb), dim3(256), 0, c->stream, z, x, d, alpha, lo, hi);
+    });
+}
+
+int lbk_checksum(lbk_ctx* c, const double* x, uint64_t* c1, uint64_t* c2) {
+    HIPCHK(c, hipMemsetAsync(c->d_ck, 0, 2 * sizeof(unsigned long long), c->stream));
+    if (c->geo.n_loc > 0) {
+        int nb = (int)std::min<int64_t>((c->geo.n_loc + 255) / 256, 2048);
+        hipLaunchKernelGGL(k_checksum, dim3(nb), dim3(256), 0, c->stream, x, c->geo.n_loc, c->geo.elem_lo, c->d_ck);
+        HIPCHK(c, hipGetLastError());
+    }
+    if (c->geo.world > 1) {
+        ncclResult_t r = ncclAllReduce(c->d_ck, c->d_ck, 2, ncclUint64, ncclSum, c->comm, c->stream);
+        if (r != ncclSuccess) return -3;
+    }
+    HIPCHK(c, hipMemcpyAsync(c->h_ck, c->d_ck, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    *c1 = c->h_ck[0];
+    *c2 = c->h_ck[1];
+    return 0;
+}
+
+double lbk_total(const double* groups64, int comp) {
+    double t = groups64[comp];
+    for (int g = 1; g < LBK_GROUPS; ++g) t = t + groups64[g * LBK_KMAX + comp];
+    return t;
+}
+
+int lbk_fetch_groups(lbk_ctx* c, int slot, double* groups64) {
+    double* h = c->h_slots + (int64_t)slot * LBK_SLOT;
+    HIPCHK(c, hipMemcpyAsync(h, c->slots + (int64_t)slot * LBK_SLOT, sizeof(double) * LBK_SLOT,
+                             hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    memcpy(groups64, h, sizeof(double) * LBK_SLOT);
+    return 0;
+}
+
+int lbk_fetch(lbk_ctx* c, int slot, int ncomp, double* totals) {
+    double g64[LBK_SLOT];
+    int rc = lbk_fetch_groups(c, slot, g64);
+    if (rc) return rc;
+    for (int k = 0; k < ncomp; ++k) totals[k] = lbk_total(g64, k);
+    return 0;
+}
+
+int lbk_sync(lbk_ctx* c) {
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+void lbk_prof_enable(lbk_ctx* c, int on) { c->prof_on = on; }
+
+int lbk_prof_get(lbk_ctx* c, int kind, double* ms, int64_t* launches, double* bytes) {
+    if (prof_flush(c) != 0) return -2;
+    if (kind < 0 || kind >= LBK_K_COUNT) return -1;
+    *ms = c->prof_ms[kind];
+    *launches = c->prof_n[kind];
+    *bytes = c->prof_bytes[kind];
+    return 0;
+}
+
+void lbk_prof_reset(lbk_ctx* c) {
+    prof_flush(c);
+    for (int k = 0; k < LBK_K_COUNT; ++k) {
+        c->prof_ms[k] = 0;
+        c->prof_n[k] = 0;
+        c->prof_bytes[k] = 0;
+    }
+}
+
+double lbk_bytes_moved(const lbk_ctx* c) { return c->bytes_total; }
+
+}  // extern "C"

@@ -1,0 +1,325 @@
+"""Python binding of liblbfgs_hip.so (include/lbfgs_hip.h) — the MI355X L-BFGS solver.
+
+The shared library is the product: HIP kernels for gfx950 plus the C host driver. This module
+is a thin ctypes layer for tests and benchmarks; it never computes anything itself and raises
+if the library is missing (there is no CPU fallback).
+
+    import lbfgs_amd as L
+    with L.Context(n=10**8, m=10) as ctx:
+        res = ctx.minimize("rosenbrock", x0, "backtracking", max_iterations=100)
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liblbfgs_hip.so")
+
+OBJECTIVES = {"rosenbrock": 0, "quad_tridiag": 1, "quad_sep": 2, "host": 3}
+LINE_SEARCHES = {"backtracking": 0, "interpolation": 1, "wolfe": 2, "backtracking_wolfe": 3}
+STATUS = {0: "converged", 1: "max_iter", 2: "ls_failed", 3: "running"}
+FLAG_VERBOSE, FLAG_QUIET, FLAG_TRACE = 1, 2, 4
+KERNELS = ["dot", "axpy_dot", "mid", "axpy2_dot", "last", "negdot", "eval", "trial_f",
+           "trial_fg", "commit", "point", "checksum"]
+
+
+class LbfgsError(RuntimeError):
+    pass
+
+
+class Constants(C.Structure):
+    _fields_ = [("c1", C.c_double), ("c2", C.c_double), ("initial_step", C.c_double),
+                ("backtracking_alpha", C.c_double), ("backtracking_tol", C.c_double),
+                ("wolfe_interp_min", C.c_double), ("wolfe_interp_max", C.c_double)]
+
+
+class Result(C.Structure):
+    _fields_ = [("iterations", C.c_int), ("status", C.c_int), ("f", C.c_double),
+                ("gnorm", C.c_double), ("trials_f", C.c_int64), ("trials_fg", C.c_int64),
+                ("commits", C.c_int64), ("passes", C.c_int64), ("bytes", C.c_double),
+                ("seconds", C.c_double)]
+
+    def as_dict(self):
+        d = {k: getattr(self, k) for k, _ in self._fields_}
+        d["status"] = STATUS.get(self.status, self.status)
+        return d
+
+
+HOST_F = C.CFUNCTYPE(C.c_double, C.POINTER(C.c_double), C.c_int64, C.c_void_p)
+HOST_G = C.CFUNCTYPE(None, C.POINTER(C.c_double), C.c_int64, C.POINTER(C.c_double), C.c_void_p)
+
+
+class HostFn(C.Structure):
+    _fields_ = [("f", HOST_F), ("grad", HOST_G), ("user", C.c_void_p)]
+
+
+_lib = None
+
+
+def lib():
+    """Load liblbfgs_hip.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise LbfgsError(f"{LIB_PATH} not built: run `make -C cuda-lbfgs_amd` "
+                         "(or __graft_entry__.build())")
+    L = C.CDLL(LIB_PATH)
+    dp = np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")
+    vp = C.c_void_p
+    L.lbfgs_ctx_create.argtypes = [C.POINTER(vp), C.c_int64, C.c_int, C.c_int]
+    L.lbfgs_ctx_create_sharded.argtypes = [C.POINTER(vp), C.c_int64, C.c_int, C.c_int, C.c_int,
+                                           C.c_int, C.c_char_p]
+    L.lbfgs_unique_id.argtypes = [C.c_char_p]
+    L.lbfgs_ctx_destroy.argtypes = [vp]
+    L.lbfgs_ctx_destroy.restype = None
+    L.lbfgs_last_error.argtypes = [vp]
+    L.lbfgs_last_error.restype = C.c_char_p
+    L.lbfgs_local_range.argtypes = [vp, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
+    L.lbfgs_constants_default.argtypes = [C.POINTER(Constants)]
+    L.lbfgs_constants_default.restype = None
+    L.lbfgs_constants_cuda.argtypes = [C.POINTER(Constants)]
+    L.lbfgs_constants_cuda.restype = None
+    L.lbfgs_minimize.argtypes = [vp, C.c_int, C.POINTER(HostFn), C.c_int, C.POINTER(Constants),
+                                 dp, dp, C.c_int, C.c_double, C.c_uint, C.POINTER(Result)]
+    L.lbfgs_solver_init.argtypes = [vp, C.c_int, C.POINTER(HostFn), C.c_int,
+                                    C.POINTER(Constants), dp, C.c_double, C.c_uint]
+    L.lbfgs_solver_step.argtypes = [vp, C.c_int, C.POINTER(Result)]
+    L.lbfgs_get_x.argtypes = [vp, dp]
+    L.lbfgs_sync.argtypes = [vp]
+    L.lbfgs_messages.argtypes = [vp, C.c_char_p, C.c_int]
+    L.lbfgs_trace_len.argtypes = [vp]
+    L.lbfgs_trace_get.argtypes = [vp, dp, dp, dp, np.ctypeslib.ndpointer(dtype=np.uint64),
+                                  np.ctypeslib.ndpointer(dtype=np.uint64), C.c_int]
+    L.lbfgs_dev_dot.argtypes = [vp, dp, dp, C.POINTER(C.c_double)]
+    L.lbfgs_dev_norm.argtypes = [vp, dp, C.POINTER(C.c_double)]
+    L.lbfgs_dev_objective.argtypes = [vp, C.c_int, dp, C.POINTER(C.c_double), vp]
+    L.lbfgs_dev_trial.argtypes = [vp, C.c_int, dp, dp, C.c_double, C.POINTER(C.c_double), vp,
+                                  C.POINTER(C.c_double)]
+    L.lbfgs_dev_twoloop.argtypes = [vp, dp, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), C.c_int,
+                                    dp, C.POINTER(C.c_double)]
+    L.lbfgs_prof_enable.argtypes = [vp, C.c_int]
+    L.lbfgs_prof_enable.restype = None
+    L.lbfgs_prof_reset.argtypes = [vp]
+    L.lbfgs_prof_reset.restype = None
+    L.lbfgs_prof_get.argtypes = [vp, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_int64),
+                                 C.POINTER(C.c_double)]
+    _lib = L
+    return L
+
+
+EXPORTED_SYMBOLS = [
+    "lbfgs_constants_default", "lbfgs_constants_cuda", "lbfgs_ctx_create",
+    "lbfgs_ctx_create_sharded", "lbfgs_unique_id", "lbfgs_ctx_destroy", "lbfgs_last_error",
+    "lbfgs_local_range", "lbfgs_minimize", "lbfgs_solver_init", "lbfgs_solver_step",
+    "lbfgs_get_x", "lbfgs_sync", "lbfgs_messages", "lbfgs_trace_len", "lbfgs_trace_get",
+    "lbfgs_dev_dot", "lbfgs_dev_norm", "lbfgs_dev_objective", "lbfgs_dev_trial",
+    "lbfgs_dev_twoloop", "lbfgs_prof_enable", "lbfgs_prof_reset", "lbfgs_prof_get",
+]
+
+
+def constants(profile="config"):
+    k = Constants()
+    (lib().lbfgs_constants_cuda if profile == "cuda" else lib().lbfgs_constants_default)(C.byref(k))
+    return k
+
+
+def unique_id():
+    buf = C.create_string_buffer(128)
+    rc = lib().lbfgs_unique_id(buf)
+    if rc != 0:
+        raise LbfgsError(f"lbfgs_unique_id failed ({rc})")
+    return buf.raw
+
+
+def x0_uniform(n, seed=42, lo=-2.0, hi=2.0):
+    """x0 exactly as std::mt19937(seed) + std::uniform_real_distribution<double>(lo, hi)
+    (libstdc++: generate_canonical<double,53> from two 32-bit draws), main.cpp:36-43."""
+    rs = np.random.RandomState(seed)  # MT19937 with init_genrand(seed) == std::mt19937(seed)
+    out = np.empty(n, dtype=np.float64)
+    chunk = 1 << 22
+    for s in range(0, n, chunk):
+        k = min(chunk, n - s)
+        raw = rs.randint(0, 1 << 32, size=2 * k, dtype=np.uint64).reshape(k, 2).astype(np.float64)
+        u = (raw[:, 0] + raw[:, 1] * 4294967296.0) / 18446744073709551616.0
+        u[u >= 1.0] = np.nextafter(1.0, 0.0)
+        out[s:s + k] = u * (hi - lo) + lo
+    return out
+
+
+class Context:
+    """A persistent solver context: device vectors for n (or this rank's shard of n) and the
+    m-pair history ring stay resident across calls."""
+
+    def __init__(self, n, m=10, device=0, rank=0, world=1, uid=None):
+        self.n, self.m = int(n), int(m)
+        h = C.c_void_p()
+        if world == 1:
+            rc = lib().lbfgs_ctx_create(C.byref(h), self.n, self.m, device)
+        else:
+            rc = lib().lbfgs_ctx_create_sharded(C.byref(h), self.n, self.m, device, rank, world, uid)
+        if rc != 0:
+            raise LbfgsError(f"lbfgs_ctx_create failed ({rc})")
+        self.h = h
+        lo, nl = C.c_int64(), C.c_int64()
+        lib().lbfgs_local_range(self.h, C.byref(lo), C.byref(nl))
+        self.elem_lo, self.n_loc = lo.value, nl.value
+        self._cb = None
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().lbfgs_ctx_destroy(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _err(self, what, rc):
+        msg = lib().lbfgs_last_error(self.h)
+        raise LbfgsError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+
+    def _host_fn(self, f, grad):
+        def cf(xp, n, user):
+            return float(f(np.ctypeslib.as_array(xp, shape=(n,)).copy()))
+
+        def cg(xp, n, gp, user):
+            g = np.asarray(grad(np.ctypeslib.as_array(xp, shape=(n,)).copy()), dtype=np.float64)
+            np.ctypeslib.as_array(gp, shape=(n,))[:] = g
+
+        self._cb = (HOST_F(cf), HOST_G(cg))
+        return HostFn(self._cb[0], self._cb[1], None)
+
+    def minimize(self, objective, x0, line_search="backtracking", max_iterations=1000, m=None,
+                 tolerance=1e-5, verbose=False, quiet=True, trace=False, consts=None,
+                 f=None, grad=None):
+        assert m is None or m == self.m
+        x0 = np.ascontiguousarray(x0, dtype=np.float64)
+        assert x0.shape == (self.n,)
+        x = np.zeros(self.n)
+        res = Result()
+        flags = (FLAG_VERBOSE if verbose else 0) | (FLAG_QUIET if quiet else 0) | \
+                (FLAG_TRACE if trace else 0)
+        cb = self._host_fn(f, grad) if objective == "host" else None
+        k = consts if consts is not None else constants()
+        rc = lib().lbfgs_minimize(self.h, OBJECTIVES[objective], C.byref(cb) if cb else None,
+                                  LINE_SEARCHES[line_search], C.byref(k), x0, x,
+                                  int(max_iterations), float(tolerance), flags, C.byref(res))
+        if rc < 0:
+            self._err("lbfgs_minimize", rc)
+        out = res.as_dict()
+        out["x"] = x
+        out["messages"] = self.messages()
+        if trace:
+            out.update(self.trace())
+        return out
+
+    def init(self, objective, x0, line_search="backtracking", tolerance=1e-5, quiet=True,
+             trace=False, consts=None):
+        x0 = np.ascontiguousarray(x0, dtype=np.float64)
+        flags = (FLAG_QUIET if quiet else 0) | (FLAG_TRACE if trace else 0)
+        k = consts if consts is not None else constants()
+        rc = lib().lbfgs_solver_init(self.h, OBJECTIVES[objective], None,
+                                     LINE_SEARCHES[line_search], C.byref(k), x0, float(tolerance),
+                                     flags)
+        if rc != 0:
+            self._err("lbfgs_solver_init", rc)
+
+    def step(self, steps):
+        res = Result()
+        rc = lib().lbfgs_solver_step(self.h, int(steps), C.byref(res))
+        if rc < 0:
+            self._err("lbfgs_solver_step", rc)
+        return res.as_dict()
+
+    def sync(self):
+        rc = lib().lbfgs_sync(self.h)
+        if rc != 0:
+            self._err("lbfgs_sync", rc)
+
+    def get_x(self):
+        x = np.zeros(self.n)
+        rc = lib().lbfgs_get_x(self.h, x)
+        if rc != 0:
+            self._err("lbfgs_get_x", rc)
+        return x
+
+    def messages(self):
+        buf = C.create_string_buffer(1 << 20)
+        lib().lbfgs_messages(self.h, buf, len(buf))
+        return buf.value.decode()
+
+    def trace(self):
+        n = lib().lbfgs_trace_len(self.h)
+        f, g, a = np.empty(max(n, 1)), np.empty(max(n, 1)), np.empty(max(n, 1))
+        c1, c2 = np.empty(max(n, 1), np.uint64), np.empty(max(n, 1), np.uint64)
+        lib().lbfgs_trace_get(self.h, f, g, a, c1, c2, n)
+        return dict(tr_f=f[:n], tr_gnorm=g[:n], tr_alpha=a[:n], tr_c1=c1[:n], tr_c2=c2[:n])
+
+    # ---- primitives ----
+    def dot(self, a, b):
+        out = C.c_double()
+        rc = lib().lbfgs_dev_dot(self.h, np.ascontiguousarray(a, np.float64),
+                                 np.ascontiguousarray(b, np.float64), C.byref(out))
+        if rc != 0:
+            self._err("lbfgs_dev_dot", rc)
+        return out.value
+
+    def objective(self, objective, x, with_grad=True):
+        f = C.c_double()
+        g = np.zeros(self.n) if with_grad else None
+        rc = lib().lbfgs_dev_objective(self.h, OBJECTIVES[objective],
+                                       np.ascontiguousarray(x, np.float64), C.byref(f),
+                                       g.ctypes.data_as(C.c_void_p) if with_grad else None)
+        if rc != 0:
+            self._err("lbfgs_dev_objective", rc)
+        return f.value, g
+
+    def trial(self, objective, x, d, alpha, with_grad=True):
+        f, dphi = C.c_double(), C.c_double()
+        g = np.zeros(self.n) if with_grad else None
+        rc = lib().lbfgs_dev_trial(self.h, OBJECTIVES[objective],
+                                   np.ascontiguousarray(x, np.float64),
+                                   np.ascontiguousarray(d, np.float64), float(alpha), C.byref(f),
+                                   g.ctypes.data_as(C.c_void_p) if with_grad else None,
+                                   C.byref(dphi))
+        if rc != 0:
+            self._err("lbfgs_dev_trial", rc)
+        return f.value, g, dphi.value
+
+    def twoloop(self, g, S, Y):
+        h = len(S)
+        S = [np.ascontiguousarray(s, np.float64) for s in S]
+        Y = [np.ascontiguousarray(y, np.float64) for y in Y]
+        sp = (C.c_void_p * h)(*[s.ctypes.data for s in S])
+        yp = (C.c_void_p * h)(*[y.ctypes.data for y in Y])
+        d = np.zeros(self.n)
+        gd = C.c_double()
+        rc = lib().lbfgs_dev_twoloop(self.h, np.ascontiguousarray(g, np.float64), sp, yp, h, d,
+                                     C.byref(gd))
+        if rc != 0:
+            self._err("lbfgs_dev_twoloop", rc)
+        return d, gd.value
+
+    # ---- profiling ----
+    def prof_enable(self, on=True):
+        lib().lbfgs_prof_enable(self.h, int(on))
+
+    def prof_reset(self):
+        lib().lbfgs_prof_reset(self.h)
+
+    def prof_get(self, kind):
+        ms, n, b = C.c_double(), C.c_int64(), C.c_double()
+        rc = lib().lbfgs_prof_get(self.h, KERNELS.index(kind), C.byref(ms), C.byref(n), C.byref(b))
+        if rc != 0:
+            self._err("lbfgs_prof_get", rc)
+        return dict(ms=ms.value, launches=n.value, bytes=b.value)

@@ -1,0 +1,37 @@
+/* lbfgs.h — C++ drop-in for the reference's L-BFGS entry points, same signatures:
+ *   LBFGS(...)       sequential-implementation/lbfgs.h:17-25 (defaults as in the header)
+ *   LBFGS_CUDA(...)  parallel-implementation/L-BFGS.cu:105-112 (with method string) and the
+ *                    string-less form of the four variants, e.g. L-BFGS-Backtracking.cu:139-145
+ * implemented on the GPU through the C ABI in lbfgs_hip.h (no CPU fallback).
+ *
+ * Behaviour as in the reference: an unknown line-search name throws std::invalid_argument
+ * ("Unknown line search method: <name>", lbfgs.cpp:69); the status messages ("Converged!",
+ * "Maximum iterations reached", warnings) go to stdout; non-convergence returns the current x.
+ * A HIP/RCCL failure throws std::runtime_error (the reference exit()s, L-BFGS.cu:76-92).
+ * Objectives from benchmark.h are evaluated on the GPU; other callables are called on the host
+ * with the trial points. Device selection: env LBFGS_DEVICE (default 0). */
+#ifndef LBFGS_AMD_LBFGS_H
+#define LBFGS_AMD_LBFGS_H
+#include <functional>
+#include <string>
+#include <vector>
+
+std::vector<double> LBFGS(const std::function<double(std::vector<double>)> f,
+                          const std::function<std::vector<double>(std::vector<double>)> grad,
+                          const std::vector<double> x0, const std::string line_search_method,
+                          const int max_iterations = 1000, const int m = 10,
+                          const double tolerance = 1e-5, bool verbose = false);
+
+std::vector<double> LBFGS_CUDA(const std::function<double(std::vector<double>)> f,
+                               const std::function<std::vector<double>(std::vector<double>)> grad,
+                               const std::vector<double> x0, const std::string line_search_method,
+                               const int max_iterations, const int m, const double tolerance);
+
+/* the variants' form without a method string (L-BFGS-Backtracking.cu:139-145 and siblings);
+ * uses the backtracking line search of the prebuilt lbfgs_cuda variant */
+std::vector<double> LBFGS_CUDA(const std::function<double(std::vector<double>)> f,
+                               const std::function<std::vector<double>(std::vector<double>)> grad,
+                               const std::vector<double> x0, const int max_iterations, const int m,
+                               const double tolerance);
+
+#endif

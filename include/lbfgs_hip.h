@@ -1,0 +1,180 @@
+/* lbfgs_hip.h — public C ABI of the MI355X-native L-BFGS solver (liblbfgs_hip.so).
+ *
+ * Drop-in boundary for the reference's L-BFGS path (ndzajic1/cuda-lbfgs @ 2025-03-02):
+ *   - lbfgs_minimize()          replaces LBFGS(f, grad, x0, method, max_iterations, m, tol,
+ *                               verbose)  sequential-implementation/lbfgs.h:17-25 (def.
+ *                               lbfgs.cpp:17-203), and LBFGS_CUDA(...)
+ *                               parallel-implementation/L-BFGS.cu:105-112 (and the 4 variants'
+ *                               string-less form, e.g. L-BFGS-Backtracking.cu:139-145).
+ *   - LBFGS_LS_*                the line-search names accepted at lbfgs.cpp:40-70 /
+ *                               L-BFGS.cu:120-153 ("backtracking", "interpolation", "wolfe",
+ *                               "backtracking_wolfe"); line_search.h:10-26.
+ *   - lbfgs_constants           config.h:5-17 (lbfgs_constants_default) and the CUDA path's
+ *                               constants.h:5-21 (lbfgs_constants_cuda, C2 = 0.7).
+ *   - LBFGS_OBJ_*               the benchmark objectives rosenbrock/rosenbrock_grad
+ *                               (benchmark.cpp:58-81 = functions.cpp:26-49),
+ *                               generate_quadratic_function/_gradient (benchmark.cpp:16-56),
+ *                               quadratic/quadratic_grad (main.cpp:7-21 = functions.cpp:6-24),
+ *                               evaluated on the GPU; LBFGS_OBJ_HOST calls user callbacks.
+ *   - lbfgs_dev_*               the BLAS-1 primitives of vector_utils.cpp:32-86 on the device.
+ *
+ * Differences in form, not in semantics: the reference takes std::vector / std::function by
+ * value and allocates device memory per call; here a persistent context owns the device
+ * memory (allocation amortised) and x0 / x are caller-owned host buffers. Errors are status
+ * codes, never exit() (reference: checkCudaError -> exit, L-BFGS.cu:76-92) and never C++
+ * exceptions across the ABI; the C++ header lbfgs.h restores the reference's exceptions.
+ * Non-convergence and line-search failure are not errors, as in the reference: the status
+ * says why, and the same messages as the reference are printed unless LBFGS_FLAG_QUIET.
+ *
+ * Threading: one host thread per context. All vectors are fp64.
+ */
+#ifndef LBFGS_HIP_H
+#define LBFGS_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LBFGS_HIP_ABI_VERSION 1
+
+typedef struct lbfgs_ctx lbfgs_ctx;
+
+/* objectives */
+enum {
+    LBFGS_OBJ_ROSENBROCK = 0,     /* benchmark.cpp:58-81 */
+    LBFGS_OBJ_QUAD_TRIDIAG = 1,   /* generate_quadratic_function(n), benchmark.cpp:16-56 */
+    LBFGS_OBJ_QUAD_SEPARABLE = 2, /* main.cpp:7-21 */
+    LBFGS_OBJ_HOST = 3            /* user callbacks (lbfgs_host_fn) */
+};
+
+/* line searches, lbfgs.cpp:40-70 */
+enum {
+    LBFGS_LS_BACKTRACKING = 0,      /* "backtracking"       line_search.cpp:19-30 */
+    LBFGS_LS_INTERPOLATION = 1,     /* "interpolation"      line_search.cpp:57-121 */
+    LBFGS_LS_WOLFE = 2,             /* "wolfe"              line_search.cpp:125-189 */
+    LBFGS_LS_BACKTRACKING_WOLFE = 3 /* "backtracking_wolfe" line_search.cpp:33-55 */
+};
+
+/* status (>= 0) and errors (< 0) */
+enum {
+    LBFGS_STATUS_CONVERGED = 0, /* "Converged!"                          lbfgs.cpp:80-84 */
+    LBFGS_STATUS_MAX_ITER = 1,  /* "Maximum iterations reached"          lbfgs.cpp:201-202 */
+    LBFGS_STATUS_LS_FAILED = 2, /* "Warning: Line search failed ..."     lbfgs.cpp:164-168 */
+    LBFGS_STATUS_RUNNING = 3,   /* lbfgs_solver_step budget used, not finished */
+    LBFGS_ERR_BAD_ARG = -1,     /* incl. unknown line search (lbfgs.cpp:69 invalid_argument) */
+    LBFGS_ERR_HIP = -2,
+    LBFGS_ERR_RCCL = -3,
+    LBFGS_ERR_NOMEM = -4,
+    LBFGS_ERR_STATE = -5,
+    LBFGS_ERR_CALLBACK = -6
+};
+
+/* flags */
+#define LBFGS_FLAG_VERBOSE 1u /* print "Iteration k, f = .., |grad| = .." (lbfgs.cpp:76-78) */
+#define LBFGS_FLAG_QUIET 2u   /* suppress the reference's stdout messages */
+#define LBFGS_FLAG_TRACE 4u   /* record per-iteration f, |g|, alpha, x checksums (tests) */
+
+typedef struct {
+    double c1;                 /* C1 = 1e-4                  config.h:5 */
+    double c2;                 /* C2 = 0.9 (constants.h: 0.7) config.h:6 */
+    double initial_step;       /* INITIAL_STEP_SIZE = 1.0    config.h:9 */
+    double backtracking_alpha; /* BACKTRACKING_ALPHA = 0.5   config.h:12 */
+    double backtracking_tol;   /* BACKTRACKING_TOL = 1e-8    config.h:13 */
+    double wolfe_interp_min;   /* WOLFE_INTERP_MIN = 1e-10   config.h:16 */
+    double wolfe_interp_max;   /* WOLFE_INTERP_MAX = 10.0    config.h:17 (unused, as in ref) */
+} lbfgs_constants;
+
+void lbfgs_constants_default(lbfgs_constants* k); /* sequential-implementation/config.h */
+void lbfgs_constants_cuda(lbfgs_constants* k);    /* parallel-implementation/constants.h */
+
+/* Host-callback objective (LBFGS_OBJ_HOST). x has n entries (global vector). */
+typedef double (*lbfgs_host_f)(const double* x, int64_t n, void* user);
+typedef void (*lbfgs_host_grad)(const double* x, int64_t n, double* g_out, void* user);
+typedef struct {
+    lbfgs_host_f f;
+    lbfgs_host_grad grad;
+    void* user;
+} lbfgs_host_fn;
+
+typedef struct {
+    int iterations;      /* iterations performed (k at exit) */
+    int status;          /* LBFGS_STATUS_* */
+    double f;            /* f at the returned x's iterate (f_current) */
+    double gnorm;        /* |g| at the last convergence test */
+    int64_t trials_f;    /* extra f-only trial passes */
+    int64_t trials_fg;   /* extra f+grad trial passes */
+    int64_t commits;     /* commit passes (incl. the fused speculative ones) */
+    int64_t passes;      /* device kernel launches */
+    double bytes;        /* algorithmic HBM bytes moved by all launches (this rank) */
+    double seconds;      /* wall time of the solve / step call */
+} lbfgs_result;
+
+/* ---- context ---------------------------------------------------------------------------- */
+/* n: global problem size; m: history length (1..64); device: HIP device ordinal. */
+int lbfgs_ctx_create(lbfgs_ctx** out, int64_t n, int m, int device);
+/* One process per GPU: shard the vectors across 'world' ranks (world | 8) with an RCCL
+ * communicator created from 'unique_id' (128 bytes, from lbfgs_unique_id on rank 0). */
+int lbfgs_ctx_create_sharded(lbfgs_ctx** out, int64_t n, int m, int device, int rank, int world,
+                             const void* unique_id);
+int lbfgs_unique_id(void* out128);
+void lbfgs_ctx_destroy(lbfgs_ctx* ctx);
+const char* lbfgs_last_error(const lbfgs_ctx* ctx);
+/* this rank's slice [elem_lo, elem_lo + n_loc) of the global vector */
+int lbfgs_local_range(const lbfgs_ctx* ctx, int64_t* elem_lo, int64_t* n_loc);
+
+/* ---- solve (drop-in for LBFGS / LBFGS_CUDA) ------------------------------------------- */
+/* x0_host / x_out_host: global vectors of n doubles (each rank passes the full vector; a
+ * sharded rank writes only its slice of x_out_host). cb may be NULL unless objective is
+ * LBFGS_OBJ_HOST; k may be NULL (config.h constants). */
+int lbfgs_minimize(lbfgs_ctx* ctx, int objective, const lbfgs_host_fn* cb, int line_search,
+                   const lbfgs_constants* k, const double* x0_host, double* x_out_host,
+                   int max_iterations, double tolerance, unsigned flags, lbfgs_result* out);
+
+/* stepping API: init once, then run iterations in chunks (benchmarks, checkpoints) */
+int lbfgs_solver_init(lbfgs_ctx* ctx, int objective, const lbfgs_host_fn* cb, int line_search,
+                      const lbfgs_constants* k, const double* x0_host, double tolerance,
+                      unsigned flags);
+int lbfgs_solver_step(lbfgs_ctx* ctx, int max_steps, lbfgs_result* out);
+int lbfgs_get_x(lbfgs_ctx* ctx, double* x_out_host);
+int lbfgs_sync(lbfgs_ctx* ctx);
+
+/* messages printed by the last solve (the reference's stdout lines), NUL-terminated */
+int lbfgs_messages(const lbfgs_ctx* ctx, char* buf, int cap);
+/* per-iteration trace (LBFGS_FLAG_TRACE): entry k = state at the top of iteration k */
+int lbfgs_trace_len(const lbfgs_ctx* ctx);
+int lbfgs_trace_get(const lbfgs_ctx* ctx, double* f, double* gnorm, double* alpha,
+                    uint64_t* c1, uint64_t* c2, int cap);
+
+/* ---- device primitives (vector_utils.cpp:32-86 on the GPU) ----------------------------- */
+/* Host-buffer convenience forms over the context's n (global vectors). Results are the
+ * canonical fixed-order device reductions. */
+int lbfgs_dev_dot(lbfgs_ctx* ctx, const double* a_host, const double* b_host, double* out);
+int lbfgs_dev_norm(lbfgs_ctx* ctx, const double* v_host, double* out);
+int lbfgs_dev_objective(lbfgs_ctx* ctx, int objective, const double* x_host, double* f_out,
+                        double* g_out_host /* nullable */);
+/* trial evaluation at x + alpha d: f, and (g_out_host != NULL) g_t and g_t . d */
+int lbfgs_dev_trial(lbfgs_ctx* ctx, int objective, const double* x_host, const double* d_host,
+                    double alpha, double* f_out, double* g_out_host, double* dphi_out);
+/* one full device two-loop recursion (lbfgs.cpp:94-143) for a given history, oldest first.
+ * S_host/Y_host: arrays of h pointers to n-vectors. Writes d and g.d. */
+int lbfgs_dev_twoloop(lbfgs_ctx* ctx, const double* g_host, const double* const* S_host,
+                      const double* const* Y_host, int h, double* d_out_host, double* gd_out);
+
+/* ---- profiling (benchmarks) ------------------------------------------------------------ */
+enum {
+    LBFGS_KERNEL_DOT = 0, LBFGS_KERNEL_AXPY_DOT, LBFGS_KERNEL_MID, LBFGS_KERNEL_AXPY2_DOT,
+    LBFGS_KERNEL_LAST, LBFGS_KERNEL_NEGDOT, LBFGS_KERNEL_EVAL, LBFGS_KERNEL_TRIAL_F,
+    LBFGS_KERNEL_TRIAL_FG, LBFGS_KERNEL_COMMIT, LBFGS_KERNEL_POINT, LBFGS_KERNEL_CHECKSUM,
+    LBFGS_KERNEL_COUNT
+};
+void lbfgs_prof_enable(lbfgs_ctx* ctx, int on);
+void lbfgs_prof_reset(lbfgs_ctx* ctx);
+/* HIP-event time on the solver stream, launches and algorithmic bytes for a kernel kind */
+int lbfgs_prof_get(lbfgs_ctx* ctx, int kind, double* ms, int64_t* launches, double* bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

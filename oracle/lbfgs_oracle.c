@@ -604,3 +604,33 @@ done:
     free(hy);
     return 0;
 }
+
+/* ------------------------------------------------------------------------------------------
+ * Two-loop recursion alone (lbfgs.cpp:94-143) for a given history S[0..h-1] (oldest first),
+ * used to check the device two-loop primitive. Returns g.d.
+ * ---------------------------------------------------------------------------------------- */
+double orc_twoloop(const double* g, const double* const* S, const double* const* Y, int h,
+                   int64_t n, int mode, double* d) {
+    double* q = (double*)malloc(sizeof(double) * (size_t)n);
+    double* r = (double*)malloc(sizeof(double) * (size_t)n);
+    double* al = (double*)malloc(sizeof(double) * (size_t)h);
+    memcpy(q, g, sizeof(double) * (size_t)n);
+    for (int i = h - 1; i >= 0; --i) {
+        double rho = 1.0 / orc_dot(Y[i], S[i], n, mode);
+        al[i] = rho * orc_dot(S[i], q, n, mode);
+        for (int64_t j = 0; j < n; ++j) q[j] -= al[i] * Y[i][j];
+    }
+    double gamma = orc_dot(S[h - 1], Y[h - 1], n, mode) / orc_dot(Y[h - 1], Y[h - 1], n, mode);
+    for (int64_t i = 0; i < n; ++i) r[i] = q[i] * gamma;
+    for (int i = 0; i < h; ++i) {
+        double rho = 1.0 / orc_dot(Y[i], S[i], n, mode);
+        double beta = rho * orc_dot(Y[i], r, n, mode);
+        for (int64_t j = 0; j < n; ++j) r[j] += S[i][j] * (al[i] - beta);
+    }
+    for (int64_t j = 0; j < n; ++j) d[j] = -r[j];
+    double gd = orc_dot(g, d, n, mode);
+    free(q);
+    free(r);
+    free(al);
+    return gd;
+}

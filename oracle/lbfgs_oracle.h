@@ -66,6 +66,10 @@ int orc_lbfgs(const orc_opts* o, const double* x0, double* x_out,
 
 void orc_checksum(const double* x, int64_t n, uint64_t* c1, uint64_t* c2);
 
+/* two-loop recursion alone for history S/Y[0..h-1] (oldest first); writes d, returns g.d */
+double orc_twoloop(const double* g, const double* const* S, const double* const* Y, int h,
+                   int64_t n, int mode, double* d);
+
 #ifdef __cplusplus
 }
 #endif

@@ -160,3 +160,18 @@ def load_golden(name):
 def golden_cases():
     return sorted(f[:-5] for f in os.listdir(GOLDEN)
                   if f.endswith(".json") and not f.startswith("kat_"))
+
+
+def twoloop(g, S, Y, mode=CANON):
+    L = lib()
+    L.orc_twoloop.argtypes = [np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS"),
+                              C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), C.c_int, C.c_int64,
+                              C.c_int, np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")]
+    L.orc_twoloop.restype = C.c_double
+    S = [np.ascontiguousarray(s, np.float64) for s in S]
+    Y = [np.ascontiguousarray(y, np.float64) for y in Y]
+    sp = (C.c_void_p * len(S))(*[s.ctypes.data for s in S])
+    yp = (C.c_void_p * len(Y))(*[y.ctypes.data for y in Y])
+    d = np.empty(len(g))
+    gd = L.orc_twoloop(np.ascontiguousarray(g, np.float64), sp, yp, len(S), len(g), mode, d)
+    return d, gd

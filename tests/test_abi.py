@@ -1,0 +1,98 @@
+"""CPU-side checks of the product boundary (no GPU compute): the C-ABI library loads and
+exports every symbol the public headers declare; the host-side helpers agree with the oracle."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "cuda-lbfgs_amd")
+import sys  # noqa: E402
+
+sys.path.insert(0, PKG)
+import lbfgs_amd as L  # noqa: E402
+import oracle_lib as O  # noqa: E402
+
+
+def _ensure_built():
+    if not os.path.exists(L.LIB_PATH):
+        subprocess.run(["make", "-C", PKG, "-j8"], check=True, capture_output=True)
+
+
+def _declared_c_symbols():
+    src = open(os.path.join(ROOT, "include", "lbfgs_hip.h")).read()
+    return sorted(set(re.findall(r"\b(lbfgs_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    _ensure_built()
+    lib = ctypes.CDLL(L.LIB_PATH)
+    declared = _declared_c_symbols()
+    assert len(declared) >= 20
+    missing = [s for s in declared if not hasattr(lib, s)]
+    assert not missing, missing
+    assert set(L.EXPORTED_SYMBOLS) <= set(declared)
+
+
+def test_cxx_dropin_symbols_exported():
+    _ensure_built()
+    out = subprocess.run(["nm", "-DC", L.LIB_PATH], check=True, capture_output=True, text=True).stdout
+    for sig in ["LBFGS(std::function<double (std::vector<double",
+                "LBFGS_CUDA(std::function<double (std::vector<double",
+                "rosenbrock(std::vector<double", "rosenbrock_grad(std::vector<double",
+                "generate_quadratic_function(int)", "generate_quadratic_gradient(int)",
+                "quadratic(std::vector<double", "quadratic_grad(std::vector<double"]:
+        assert sig in out, sig
+
+
+def test_library_has_gfx950_code_object():
+    _ensure_built()
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", L.LIB_PATH],
+                         capture_output=True, text=True)
+    text = out.stdout + out.stderr
+    if "gfx950" not in text:  # fall back to a raw scan of the fat binary
+        assert b"gfx950" in open(L.LIB_PATH, "rb").read()
+
+
+def test_constants_match_reference_headers():
+    k = L.constants()
+    assert (k.c1, k.c2, k.initial_step, k.backtracking_alpha, k.backtracking_tol,
+            k.wolfe_interp_min, k.wolfe_interp_max) == (1e-4, 0.9, 1.0, 0.5, 1e-8, 1e-10, 10.0)
+    kc = L.constants("cuda")
+    assert kc.c2 == 0.7 and kc.c1 == 1e-4  # parallel-implementation/constants.h:5-6
+
+
+def test_x0_generator_matches_std_mt19937():
+    for n, seed, lo, hi in [(1000, 42, -2.0, 2.0), (333, 7, -1000.0, 1000.0), (5, 3, -2.0, 2.0)]:
+        assert np.array_equal(L.x0_uniform(n, seed, lo, hi), O.x0_uniform(n, seed, lo, hi))
+    meta, g = O.load_golden("kat_n1000")
+    assert np.array_equal(L.x0_uniform(1000, 7, -2.0, 2.0), g["x"])
+
+
+def test_headers_compile_as_reference_dropin(tmp_path):
+    """A reference-style caller (main.cpp shape) compiles and links against our headers."""
+    _ensure_built()
+    src = tmp_path / "caller.cpp"
+    src.write_text(r'''
+#include <random>
+#include <vector>
+#include <benchmark.h>
+#include <lbfgs.h>
+#include <config.h>
+int main() {
+    std::mt19937 gen(42);
+    std::uniform_real_distribution<> dis(-2, 2);
+    std::vector<double> x0(100);
+    for (double& v : x0) v = dis(gen);
+    if (C2 != 0.9) return 3;
+    std::vector<double> x = LBFGS(rosenbrock, rosenbrock_grad, x0, "backtracking", 5, 5, 1e-5, false);
+    return x.size() == 100 ? 0 : 1;
+}
+''')
+    exe = tmp_path / "caller"
+    subprocess.run(["g++", "-std=c++17", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe),
+                    L.LIB_PATH, "-Wl,-rpath," + PKG], check=True, capture_output=True)
+    assert exe.exists()
