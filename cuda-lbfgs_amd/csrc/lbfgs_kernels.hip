@@ -33,6 +33,7 @@
 #include <rccl/rccl.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -40,6 +41,7 @@
 #include "lbfgs_device.h"
 
 #define LB_BLOCK 256
+#define LBK_FRONT 32
 
 namespace {
 
@@ -56,6 +58,30 @@ struct Red {
 
 __device__ __forceinline__ double2 ld2(const double* p) {
     return *reinterpret_cast<const double2*>(p);
+}
+
+// Streaming loads/stores; NT = non-temporal (the vectors are touched once per pass and, at
+// the benchmark sizes, are far larger than the 256 MiB Infinity Cache): +6 % on the 3-read /
+// 1-write pass mix on MI355X (profiles/r01/bwprobe_v2.txt).
+typedef double dvec2 __attribute__((ext_vector_type(2)));
+template <bool NT>
+__device__ __forceinline__ double2 ldv(const double* p) {
+    if (NT) {
+        const dvec2 v = __builtin_nontemporal_load(reinterpret_cast<const dvec2*>(p));
+        return make_double2(v.x, v.y);
+    }
+    return *reinterpret_cast<const double2*>(p);
+}
+template <bool NT>
+__device__ __forceinline__ void stv(double* p, double2 v) {
+    if (NT) {
+        dvec2 w;
+        w.x = v.x;
+        w.y = v.y;
+        __builtin_nontemporal_store(w, reinterpret_cast<dvec2*>(p));
+    } else {
+        *reinterpret_cast<double2*>(p) = v;
+    }
 }
 __device__ __forceinline__ void st2m(double* p, double2 v, bool v0, bool v1) {
     if (v1) {
@@ -223,215 +249,268 @@ __device__ __forceinline__ double obj_grad(double zm, double zc, double zp, bool
 }
 
 // Neighbour exchange inside a row: lane l holds z[2l], z[2l+1]; the halo value zh is
-// z[-1] on lane 0 and z[128] on lane 63.
-__device__ __forceinline__ void neighbours(double z0, double z1, double zh, int lane, double& zl, double& zr) {
-    zl = __shfl_up(z1, 1, 64);
-    zr = __shfl_down(z0, 1, 64);
-    if (lane == 0) zl = zh;
-    if (lane == 63) zr = zh;
+// z[-1] on lane 0 and z[128] on lane 63. Returned by value (selects): a by-reference form
+// made hipcc place both outputs in scratch and pick one with a dynamic store.
+struct Nb {
+    double l, r;
+};
+__device__ __forceinline__ Nb neighbours(double z0, double z1, double zh, int lane) {
+    Nb nb;
+    const double up = __shfl_up(z1, 1, 64);
+    const double dn = __shfl_down(z0, 1, 64);
+    nb.l = (lane == 0) ? zh : up;
+    nb.r = (lane == 63) ? zh : dn;
+    return nb;
+}
+
+// ---------------------------------------------------------------------------------------
+// Streaming framework. A kernel is a policy Op with
+//   typename Op::Row                      registers of one row (128 elements) of this lane
+//   op.load(Row&, int64_t i)              issue the loads of local elements i, i+1 (+ halo)
+//   op.apply<MASK>(Row&, i, e0, v0, v1, acc)  compute, store, accumulate (elements < len)
+// and every kernel walks its segment as: full segments (all but the last) in groups of
+// 4 / 2 / 1 rows with every load of a group issued before any use and no element masks;
+// the last, partial segment row by row with masks. The accumulation order (row u
+// ascending, v = 0 then 1) is the canonical one in both paths.
+// ---------------------------------------------------------------------------------------
+template <bool MASK, int UN, int K, class Op>
+__device__ __forceinline__ void rows(const Op& op, const Seg& s, int u0, double (&acc)[K]) {
+    typename Op::Row r[UN];
+#pragma unroll
+    for (int j = 0; j < UN; ++j) op.load(r[j], s.lb + row_off(s, u0 + j));
+#pragma unroll
+    for (int j = 0; j < UN; ++j) {
+        const int64_t o = row_off(s, u0 + j);
+        const bool v0 = MASK ? o < s.len : true;
+        const bool v1 = MASK ? o + 1 < s.len : true;
+        op.template apply<MASK>(r[j], s.lb + o, s.sbeg + o, v0, v1, acc);
+    }
+}
+
+template <int K, class Op>
+__device__ __forceinline__ void stream(const Op& op, const Seg& s, const Geo& geo, double (&acc)[K]) {
+    int u0 = 0;
+    if (s.len == geo.L) {
+        for (; u0 + 4 <= s.nrows; u0 += 4) rows<false, 4>(op, s, u0, acc);
+        if (u0 + 2 <= s.nrows) {
+            rows<false, 2>(op, s, u0, acc);
+            u0 += 2;
+        }
+        if (u0 < s.nrows) rows<false, 1>(op, s, u0, acc);
+    } else {
+        for (; u0 < s.nrows; ++u0) rows<true, 1>(op, s, u0, acc);
+    }
+}
+
+template <bool MASK, bool NT>
+__device__ __forceinline__ void st2(double* p, double2 v, bool v0, bool v1) {
+    if (MASK)
+        st2m(p, v, v0, v1);
+    else
+        stv<NT>(p, v);
+}
+
+// acc = fma(a, b, acc) for the valid elements of a lane pair
+template <bool MASK>
+__device__ __forceinline__ double fma2(double2 a, double2 b, double acc, bool v0, bool v1) {
+    if (!MASK || v0) acc = fma(a.x, b.x, acc);
+    if (!MASK || v1) acc = fma(a.y, b.y, acc);
+    return acc;
 }
 
 // ---------------------------------------------------------------------------------------
 // Two-loop recursion passes
 // ---------------------------------------------------------------------------------------
-constexpr int U2 = 4;  // rows in flight per wave for the BLAS-1 passes
-
-__global__ __launch_bounds__(LB_BLOCK) void k_dot(const double* __restrict__ a, const double* __restrict__ b,
-                                                  Geo geo, Red red) {
-    const Seg s = seg_setup(geo);
-    double acc[1] = {0.0};
-    for (int u0 = 0; u0 < s.nrows; u0 += U2) {
-        double2 av[U2], bv[U2];
-#pragma unroll
-        for (int j = 0; j < U2; ++j) {
-            if (u0 + j < s.nrows) {
-                const int64_t i = s.lb + row_off(s, u0 + j);
-                av[j] = ld2(a + i);
-                bv[j] = ld2(b + i);
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < U2; ++j) {
-            if (u0 + j < s.nrows) {
-                const int64_t o = row_off(s, u0 + j);
-                if (o < s.len) acc[0] = fma(av[j].x, bv[j].x, acc[0]);
-                if (o + 1 < s.len) acc[0] = fma(av[j].y, bv[j].y, acc[0]);
-            }
-        }
+template <bool NT>
+struct OpDot {  // acc += a . b
+    const double* __restrict__ a;
+    const double* __restrict__ b;
+    struct Row {
+        double2 a, b;
+    };
+    __device__ void load(Row& r, int64_t i) const {
+        r.a = ldv<NT>(a + i);
+        r.b = ldv<NT>(b + i);
     }
-    reduce_publish<1>(acc, geo, red);
+    template <bool MASK>
+    __device__ void apply(Row& r, int64_t, int64_t, bool v0, bool v1, double (&acc)[1]) const {
+        acc[0] = fma2<MASK>(r.a, r.b, acc[0], v0, v1);
+    }
+};
+
+template <bool NT>
+struct OpAxpyDot {  // q = qin - alpha y;  acc += s . q       (lbfgs.cpp:133-137)
+    double* qout;
+    const double* qin;
+    const double* __restrict__ y;
+    const double* __restrict__ s;
+    double alpha;
+    struct Row {
+        double2 q, y, s;
+    };
+    __device__ void load(Row& r, int64_t i) const {
+        r.q = ldv<NT>(qin + i);
+        r.y = ldv<NT>(y + i);
+        r.s = ldv<NT>(s + i);
+    }
+    template <bool MASK>
+    __device__ void apply(Row& r, int64_t i, int64_t, bool v0, bool v1, double (&acc)[1]) const {
+        double2 qn;
+        qn.x = r.q.x - alpha * r.y.x;
+        qn.y = r.q.y - alpha * r.y.y;
+        st2<MASK, NT>(qout + i, qn, v0, v1);
+        acc[0] = fma2<MASK>(r.s, qn, acc[0], v0, v1);
+    }
+};
+
+template <bool NT>
+struct OpMid {  // r = (qin - alpha0 y0) * gamma;  acc += y0 . r      (:134-137, :150-154, :160)
+    double* __restrict__ rout;
+    const double* __restrict__ qin;
+    const double* __restrict__ y0;
+    double alpha, gamma;
+    struct Row {
+        double2 q, y;
+    };
+    __device__ void load(Row& r, int64_t i) const {
+        r.q = ldv<NT>(qin + i);
+        r.y = ldv<NT>(y0 + i);
+    }
+    template <bool MASK>
+    __device__ void apply(Row& r, int64_t i, int64_t, bool v0, bool v1, double (&acc)[1]) const {
+        double2 rr;
+        rr.x = (r.q.x - alpha * r.y.x) * gamma;
+        rr.y = (r.q.y - alpha * r.y.y) * gamma;
+        st2<MASK, NT>(rout + i, rr, v0, v1);
+        acc[0] = fma2<MASK>(r.y, rr, acc[0], v0, v1);
+    }
+};
+
+template <bool NT>
+struct OpAxpy2Dot {  // r += s (alpha - beta);  acc += ynext . r      (:159-164)
+    double* r;
+    const double* __restrict__ s;
+    const double* __restrict__ yn;
+    double coef;
+    struct Row {
+        double2 r, s, y;
+    };
+    __device__ void load(Row& w, int64_t i) const {
+        w.r = ldv<NT>(r + i);
+        w.s = ldv<NT>(s + i);
+        w.y = ldv<NT>(yn + i);
+    }
+    template <bool MASK>
+    __device__ void apply(Row& w, int64_t i, int64_t, bool v0, bool v1, double (&acc)[1]) const {
+        double2 rn;
+        rn.x = w.r.x + w.s.x * coef;
+        rn.y = w.r.y + w.s.y * coef;
+        st2<MASK, NT>(r + i, rn, v0, v1);
+        acc[0] = fma2<MASK>(w.y, rn, acc[0], v0, v1);
+    }
+};
+
+template <bool NT>
+struct OpLast {  // d = -(r + s (alpha - beta));  acc += g . d        (:163-171)
+    double* __restrict__ dout;
+    const double* __restrict__ r;
+    const double* __restrict__ s;
+    const double* __restrict__ g;
+    double coef;
+    struct Row {
+        double2 r, s, g;
+    };
+    __device__ void load(Row& w, int64_t i) const {
+        w.r = ldv<NT>(r + i);
+        w.s = ldv<NT>(s + i);
+        w.g = ldv<NT>(g + i);
+    }
+    template <bool MASK>
+    __device__ void apply(Row& w, int64_t i, int64_t, bool v0, bool v1, double (&acc)[1]) const {
+        double2 d;
+        d.x = -(w.r.x + w.s.x * coef);
+        d.y = -(w.r.y + w.s.y * coef);
+        st2<MASK, NT>(dout + i, d, v0, v1);
+        acc[0] = fma2<MASK>(w.g, d, acc[0], v0, v1);
+    }
+};
+
+template <bool NT>
+struct OpNegDot {  // d = -g;  acc += g . d                          (:90, :151-152)
+    double* __restrict__ dout;
+    const double* __restrict__ g;
+    struct Row {
+        double2 g;
+    };
+    __device__ void load(Row& w, int64_t i) const { w.g = ldv<NT>(g + i); }
+    template <bool MASK>
+    __device__ void apply(Row& w, int64_t i, int64_t, bool v0, bool v1, double (&acc)[1]) const {
+        double2 d;
+        d.x = -w.g.x;
+        d.y = -w.g.y;
+        st2<MASK, NT>(dout + i, d, v0, v1);
+        acc[0] = fma2<MASK>(w.g, d, acc[0], v0, v1);
+    }
+};
+
+template <class Op, int K>
+__device__ __forceinline__ void run_pass(const Op& op, const Geo& geo, const Red& red) {
+    const Seg s = seg_setup(geo);
+    double acc[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) acc[k] = 0.0;
+    stream(op, s, geo, acc);
+    reduce_publish<K>(acc, geo, red);
 }
 
-// q = qin - alpha y;  acc += s . q     with alpha = rho * total(prev)
+template <bool NT>
+__global__ __launch_bounds__(LB_BLOCK) void k_dot(const double* __restrict__ a, const double* __restrict__ b,
+                                                  Geo geo, Red red) {
+    run_pass<OpDot<NT>, 1>(OpDot<NT>{a, b}, geo, red);
+}
+
+// alpha = rho * total(prev)
+template <bool NT>
 __global__ __launch_bounds__(LB_BLOCK) void k_axpy_dot(double* qout, const double* qin, const double* __restrict__ y,
                                                        const double* __restrict__ sv, double rho,
                                                        const double* __restrict__ prev, Geo geo, Red red) {
     const double alpha = rho * slot_total(prev);
-    const Seg s = seg_setup(geo);
-    double acc[1] = {0.0};
-    for (int u0 = 0; u0 < s.nrows; u0 += U2) {
-        double2 qv[U2], yv[U2], ss[U2];
-#pragma unroll
-        for (int j = 0; j < U2; ++j) {
-            if (u0 + j < s.nrows) {
-                const int64_t i = s.lb + row_off(s, u0 + j);
-                qv[j] = ld2(qin + i);
-                yv[j] = ld2(y + i);
-                ss[j] = ld2(sv + i);
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < U2; ++j) {
-            if (u0 + j < s.nrows) {
-                const int64_t o = row_off(s, u0 + j);
-                const bool v0 = o < s.len, v1 = o + 1 < s.len;
-                double2 qn;
-                qn.x = qv[j].x - alpha * yv[j].x;
-                qn.y = qv[j].y - alpha * yv[j].y;
-                st2m(qout + s.lb + o, qn, v0, v1);
-                if (v0) acc[0] = fma(ss[j].x, qn.x, acc[0]);
-                if (v1) acc[0] = fma(ss[j].y, qn.y, acc[0]);
-            }
-        }
-    }
-    reduce_publish<1>(acc, geo, red);
+    run_pass<OpAxpyDot<NT>, 1>(OpAxpyDot<NT>{qout, qin, y, sv, alpha}, geo, red);
 }
 
-// r = (qin - alpha0 y0) * gamma;  acc += y0 . r
+template <bool NT>
 __global__ __launch_bounds__(LB_BLOCK) void k_mid(double* __restrict__ rout, const double* __restrict__ qin,
                                                   const double* __restrict__ y0, double rho0, double gamma,
                                                   const double* __restrict__ prev, Geo geo, Red red) {
     const double alpha = rho0 * slot_total(prev);
-    const Seg s = seg_setup(geo);
-    double acc[1] = {0.0};
-    for (int u0 = 0; u0 < s.nrows; u0 += U2) {
-        double2 qv[U2], yv[U2];
-#pragma unroll
-        for (int j = 0; j < U2; ++j) {
-            if (u0 + j < s.nrows) {
-                const int64_t i = s.lb + row_off(s, u0 + j);
-                qv[j] = ld2(qin + i);
-                yv[j] = ld2(y0 + i);
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < U2; ++j) {
-            if (u0 + j < s.nrows) {
-                const int64_t o = row_off(s, u0 + j);
-                const bool v0 = o < s.len, v1 = o + 1 < s.len;
-                double2 r;
-                r.x = (qv[j].x - alpha * yv[j].x) * gamma;
-                r.y = (qv[j].y - alpha * yv[j].y) * gamma;
-                st2m(rout + s.lb + o, r, v0, v1);
-                if (v0) acc[0] = fma(yv[j].x, r.x, acc[0]);
-                if (v1) acc[0] = fma(yv[j].y, r.y, acc[0]);
-            }
-        }
-    }
-    reduce_publish<1>(acc, geo, red);
+    run_pass<OpMid<NT>, 1>(OpMid<NT>{rout, qin, y0, alpha, gamma}, geo, red);
 }
 
-// r += s (alpha - beta);  acc += ynext . r    beta = rho*total(pb), alpha = rho*total(pa)
+// beta = rho * total(pb), alpha = rho * total(pa)
+template <bool NT>
 __global__ __launch_bounds__(LB_BLOCK) void k_axpy2_dot(double* r, const double* __restrict__ sv,
                                                         const double* __restrict__ yn, double rho,
                                                         const double* __restrict__ pb, const double* __restrict__ pa,
                                                         Geo geo, Red red) {
     const double beta = rho * slot_total(pb);
     const double alpha = rho * slot_total(pa);
-    const double coef = alpha - beta;
-    const Seg s = seg_setup(geo);
-    double acc[1] = {0.0};
-    for (int u0 = 0; u0 < s.nrows; u0 += U2) {
-        double2 rv[U2], ss[U2], yv[U2];
-#pragma unroll
-        for (int j = 0; j < U2; ++j) {
-            if (u0 + j < s.nrows) {
-                const int64_t i = s.lb + row_off(s, u0 + j);
-                rv[j] = ld2(r + i);
-                ss[j] = ld2(sv + i);
-                yv[j] = ld2(yn + i);
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < U2; ++j) {
-            if (u0 + j < s.nrows) {
-                const int64_t o = row_off(s, u0 + j);
-                const bool v0 = o < s.len, v1 = o + 1 < s.len;
-                double2 rn;
-                rn.x = rv[j].x + ss[j].x * coef;
-                rn.y = rv[j].y + ss[j].y * coef;
-                st2m(r + s.lb + o, rn, v0, v1);
-                if (v0) acc[0] = fma(yv[j].x, rn.x, acc[0]);
-                if (v1) acc[0] = fma(yv[j].y, rn.y, acc[0]);
-            }
-        }
-    }
-    reduce_publish<1>(acc, geo, red);
+    run_pass<OpAxpy2Dot<NT>, 1>(OpAxpy2Dot<NT>{r, sv, yn, alpha - beta}, geo, red);
 }
 
-// d = -(r + s (alpha - beta));  acc += g . d
+template <bool NT>
 __global__ __launch_bounds__(LB_BLOCK) void k_last(double* __restrict__ dout, const double* __restrict__ r,
                                                    const double* __restrict__ sv, const double* __restrict__ g,
                                                    double rho, const double* __restrict__ pb,
                                                    const double* __restrict__ pa, Geo geo, Red red) {
     const double beta = rho * slot_total(pb);
     const double alpha = rho * slot_total(pa);
-    const double coef = alpha - beta;
-    const Seg s = seg_setup(geo);
-    double acc[1] = {0.0};
-    for (int u0 = 0; u0 < s.nrows; u0 += U2) {
-        double2 rv[U2], ss[U2], gv[U2];
-#pragma unroll
-        for (int j = 0; j < U2; ++j) {
-            if (u0 + j < s.nrows) {
-                const int64_t i = s.lb + row_off(s, u0 + j);
-                rv[j] = ld2(r + i);
-                ss[j] = ld2(sv + i);
-                gv[j] = ld2(g + i);
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < U2; ++j) {
-            if (u0 + j < s.nrows) {
-                const int64_t o = row_off(s, u0 + j);
-                const bool v0 = o < s.len, v1 = o + 1 < s.len;
-                double2 d;
-                d.x = -(rv[j].x + ss[j].x * coef);
-                d.y = -(rv[j].y + ss[j].y * coef);
-                st2m(dout + s.lb + o, d, v0, v1);
-                if (v0) acc[0] = fma(gv[j].x, d.x, acc[0]);
-                if (v1) acc[0] = fma(gv[j].y, d.y, acc[0]);
-            }
-        }
-    }
-    reduce_publish<1>(acc, geo, red);
+    run_pass<OpLast<NT>, 1>(OpLast<NT>{dout, r, sv, g, alpha - beta}, geo, red);
 }
 
-// d = -g;  acc += g . d
+template <bool NT>
 __global__ __launch_bounds__(LB_BLOCK) void k_negdot(double* __restrict__ dout, const double* __restrict__ g,
                                                      Geo geo, Red red) {
-    const Seg s = seg_setup(geo);
-    double acc[1] = {0.0};
-    for (int u0 = 0; u0 < s.nrows; u0 += U2) {
-        double2 gv[U2];
-#pragma unroll
-        for (int j = 0; j < U2; ++j)
-            if (u0 + j < s.nrows) gv[j] = ld2(g + s.lb + row_off(s, u0 + j));
-#pragma unroll
-        for (int j = 0; j < U2; ++j) {
-            if (u0 + j < s.nrows) {
-                const int64_t o = row_off(s, u0 + j);
-                const bool v0 = o < s.len, v1 = o + 1 < s.len;
-                double2 d;
-                d.x = -gv[j].x;
-                d.y = -gv[j].y;
-                st2m(dout + s.lb + o, d, v0, v1);
-                if (v0) acc[0] = fma(gv[j].x, d.x, acc[0]);
-                if (v1) acc[0] = fma(gv[j].y, d.y, acc[0]);
-            }
-        }
-    }
-    reduce_publish<1>(acc, geo, red);
+    run_pass<OpNegDot<NT>, 1>(OpNegDot<NT>{dout, g}, geo, red);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -447,17 +526,17 @@ struct DirArgs {
     double rho;
 };
 
-template <int DMODE>
+template <int DMODE, bool NT>
 __device__ __forceinline__ double2 load_dir(const DirArgs& da, int64_t i, double2 gv) {
     double2 d;
     if (DMODE == LBK_D_BUF) {
-        d = ld2(da.dsrc + i);
+        d = ldv<NT>(da.dsrc + i);
     } else if (DMODE == LBK_D_NEG_G) {
         d.x = -gv.x;
         d.y = -gv.y;
     } else {
-        const double2 rv = ld2(da.dsrc + i);
-        const double2 sv = ld2(da.s + i);
+        const double2 rv = ldv<NT>(da.dsrc + i);
+        const double2 sv = ldv<NT>(da.s + i);
         d.x = -(rv.x + sv.x * da.coef);
         d.y = -(rv.y + sv.y * da.coef);
     }
@@ -470,77 +549,137 @@ __device__ __forceinline__ double load_dir1(const DirArgs& da, int64_t i) {
     return -(da.dsrc[i] + da.s[i] * da.coef);
 }
 
-constexpr int UO = 2;  // rows in flight per wave for the objective passes
+template <int OBJ>
+__device__ __forceinline__ bool needs_halo() {
+    return OBJ == LBK_OBJ_ROSENBROCK || OBJ == LBK_OBJ_QUAD_TRIDIAG;
+}
 
-// Evaluate f (and optionally g) at z = x + alpha*d.
-//   EVAL mode (NO_DIR): z = x; reductions: f, g.g     (lbfgs.cpp:29-30)
-//   TRIAL mode: reductions f, g_t . d                  (line_search.cpp)
-template <int OBJ, bool NO_DIR, bool WITH_G>
-__global__ __launch_bounds__(LB_BLOCK) void k_objective(const double* __restrict__ x, DirArgs da, double alpha,
-                                                        double* __restrict__ gout, Geo geo, Red red) {
-    const Seg s = seg_setup(geo);
-    double acc[2] = {0.0, 0.0};
-    const int64_t n = geo.n;
-    for (int u0 = 0; u0 < s.nrows; u0 += UO) {
-        double2 z[UO], dd[UO];
-        double zh[UO];
-#pragma unroll
-        for (int j = 0; j < UO; ++j) {
-            if (u0 + j < s.nrows) {
-                const int64_t i = s.lb + row_off(s, u0 + j);
-                const double2 xv = ld2(x + i);
-                if (NO_DIR) {
-                    z[j] = xv;
-                } else {
-                    dd[j] = load_dir<LBK_D_BUF>(da, i, xv);
-                    z[j].x = xv.x + alpha * dd[j].x;
-                    z[j].y = xv.y + alpha * dd[j].y;
-                }
-                zh[j] = 0.0;
-                if (OBJ != LBK_OBJ_QUAD_SEPARABLE && (s.lane == 0 || s.lane == 63)) {
-                    const int64_t hi = (s.lane == 0) ? i - 1 : i + 2;
-                    if (hi >= -1 && hi <= geo.n_loc) {
-                        zh[j] = NO_DIR ? x[hi] : x[hi] + alpha * load_dir1<LBK_D_BUF>(da, hi);
-                    }
-                }
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < UO; ++j) {
-            if (u0 + j < s.nrows) {
-                const int64_t o = row_off(s, u0 + j);
-                const int64_t e0 = s.sbeg + o;
-                const bool v0 = o < s.len, v1 = o + 1 < s.len;
-                double zl, zr;
-                neighbours(z[j].x, z[j].y, zh[j], s.lane, zl, zr);
-                // element e0: (zl, z.x, z.y); element e0+1: (z.x, z.y, zr)
-                const bool p0 = e0 + 1 < n, p1 = e0 + 2 < n;
-                const bool m0 = e0 > 0;
-                if (v0 && obj_has_term<OBJ>(p0)) acc[0] = acc[0] + obj_term<OBJ>(z[j].x, z[j].y, p0);
-                if (v1 && obj_has_term<OBJ>(p1)) acc[0] = acc[0] + obj_term<OBJ>(z[j].y, zr, p1);
-                if (WITH_G) {
-                    double2 gv;
-                    gv.x = obj_grad<OBJ>(zl, z[j].x, z[j].y, m0, p0);
-                    gv.y = obj_grad<OBJ>(z[j].x, z[j].y, zr, true, p1);
-                    if (gout) st2m(gout + s.lb + o, gv, v0, v1);
-                    if (NO_DIR) {
-                        if (v0) acc[1] = fma(gv.x, gv.x, acc[1]);
-                        if (v1) acc[1] = fma(gv.y, gv.y, acc[1]);
-                    } else {
-                        if (v0) acc[1] = fma(gv.x, dd[j].x, acc[1]);
-                        if (v1) acc[1] = fma(gv.y, dd[j].y, acc[1]);
-                    }
-                }
-            }
+// halo value z = x + alpha d at local index i-1 (lane 0) or i+2 (lane 63)
+template <int OBJ, bool NO_DIR, int DMODE>
+__device__ __forceinline__ double halo_z(const double* __restrict__ x, const DirArgs& da, double alpha,
+                                         int64_t i, int64_t n_loc) {
+    double zh = 0.0;
+    if (needs_halo<OBJ>()) {
+        const int lane = threadIdx.x & 63;
+        if (lane == 0 || lane == 63) {
+            const int64_t hi = (lane == 0) ? i - 1 : i + 2;
+            if (hi >= -1 && hi <= n_loc) zh = NO_DIR ? x[hi] : x[hi] + alpha * load_dir1<DMODE>(da, hi);
         }
     }
-    reduce_publish<2>(acc, geo, red);
+    return zh;
+}
+
+// f terms and gradient of the two elements of a lane at z (neighbours from the row)
+template <int OBJ, bool MASK>
+__device__ __forceinline__ double2 objective_pair(double2 z, double zh, int64_t e0, int64_t n, bool v0, bool v1,
+                                                  double& facc, bool with_g) {
+    const int lane = threadIdx.x & 63;
+    const Nb nb = neighbours(z.x, z.y, zh, lane);
+    const bool p0 = e0 + 1 < n, p1 = e0 + 2 < n;
+    if ((!MASK || v0) && obj_has_term<OBJ>(p0)) facc = facc + obj_term<OBJ>(z.x, z.y, p0);
+    if ((!MASK || v1) && obj_has_term<OBJ>(p1)) facc = facc + obj_term<OBJ>(z.y, nb.r, p1);
+    double2 g;
+    if (with_g) {
+        g.x = obj_grad<OBJ>(nb.l, z.x, z.y, e0 > 0, p0);
+        g.y = obj_grad<OBJ>(z.x, z.y, nb.r, true, p1);
+    }
+    return g;
+}
+
+// Evaluate f (and optionally g) at z = x (NO_DIR, reductions f, g.g; lbfgs.cpp:29-30) or at
+// z = x + alpha d (reductions f, g_t . d; line_search.cpp trials).
+template <int OBJ, bool NO_DIR, bool WITH_G, bool NT>
+struct OpObjective {
+    const double* __restrict__ x;
+    DirArgs da;
+    double alpha;
+    double* __restrict__ gout;
+    int64_t n, n_loc;
+    struct Row {
+        double2 z, d;
+        double zh;
+    };
+    __device__ void load(Row& r, int64_t i) const {
+        const double2 xv = ldv<NT>(x + i);
+        if (NO_DIR) {
+            r.z = xv;
+        } else {
+            r.d = ldv<NT>(da.dsrc + i);
+            r.z.x = xv.x + alpha * r.d.x;
+            r.z.y = xv.y + alpha * r.d.y;
+        }
+        r.zh = halo_z<OBJ, NO_DIR, LBK_D_BUF>(x, da, alpha, i, n_loc);
+    }
+    template <bool MASK>
+    __device__ void apply(Row& r, int64_t i, int64_t e0, bool v0, bool v1, double (&acc)[2]) const {
+        const double2 g = objective_pair<OBJ, MASK>(r.z, r.zh, e0, n, v0, v1, acc[0], WITH_G);
+        if (WITH_G) {
+            if (gout) st2<MASK, NT>(gout + i, g, v0, v1);
+            acc[1] = NO_DIR ? fma2<MASK>(g, g, acc[1], v0, v1) : fma2<MASK>(g, r.d, acc[1], v0, v1);
+        }
+    }
+};
+
+template <int OBJ, bool NO_DIR, bool WITH_G, bool NT>
+__global__ __launch_bounds__(LB_BLOCK) void k_objective(const double* __restrict__ x, DirArgs da, double alpha,
+                                                        double* __restrict__ gout, Geo geo, Red red) {
+    run_pass<OpObjective<OBJ, NO_DIR, WITH_G, NT>, 2>(OpObjective<OBJ, NO_DIR, WITH_G, NT>{x, da, alpha, gout, geo.n, geo.n_loc},
+                                                  geo, red);
 }
 
 // The commit: d per DMODE, x_new = x + alpha d, f(x_new), g_new = grad f(x_new) (or read
 // from gn for OBJ == NONE), s = x_new - x, y = g_new - g, and the dots
 //   [GD] g.d  [F] f  [SY] s.y  [YY] y.y  [GG] g_new.g_new  [SG] s.g_new  [DPHI] g_new.d
-template <int OBJ, int DMODE>
+template <int OBJ, int DMODE, bool NT>
+struct OpCommit {
+    const double* __restrict__ x;
+    DirArgs da;
+    double alpha;
+    double* __restrict__ xn;
+    double* __restrict__ gn;
+    double* __restrict__ so;
+    double* __restrict__ yo;
+    int64_t n, n_loc;
+    struct Row {
+        double2 x, g, d, z, gx;
+        double zh;
+    };
+    __device__ void load(Row& r, int64_t i) const {
+        r.x = ldv<NT>(x + i);
+        r.g = ldv<NT>(da.g + i);
+        r.d = load_dir<DMODE, NT>(da, i, r.g);
+        if (OBJ == LBK_OBJ_NONE) r.gx = ldv<NT>(gn + i);
+        r.z.x = r.x.x + alpha * r.d.x;
+        r.z.y = r.x.y + alpha * r.d.y;
+        r.zh = (OBJ == LBK_OBJ_NONE) ? 0.0 : halo_z<OBJ, false, DMODE>(x, da, alpha, i, n_loc);
+    }
+    template <bool MASK>
+    __device__ void apply(Row& r, int64_t i, int64_t e0, bool v0, bool v1, double (&acc)[7]) const {
+        double2 g2;
+        if (OBJ == LBK_OBJ_NONE) {
+            g2 = r.gx;
+        } else {
+            g2 = objective_pair<OBJ, MASK>(r.z, r.zh, e0, n, v0, v1, acc[LBK_C_F], true);
+            st2<MASK, NT>(gn + i, g2, v0, v1);
+        }
+        st2<MASK, NT>(xn + i, r.z, v0, v1);
+        double2 sv, yv;
+        sv.x = r.z.x - r.x.x;
+        sv.y = r.z.y - r.x.y;
+        yv.x = g2.x - r.g.x;
+        yv.y = g2.y - r.g.y;
+        st2<MASK, NT>(so + i, sv, v0, v1);
+        st2<MASK, NT>(yo + i, yv, v0, v1);
+        acc[LBK_C_GD] = fma2<MASK>(r.g, r.d, acc[LBK_C_GD], v0, v1);
+        acc[LBK_C_SY] = fma2<MASK>(sv, yv, acc[LBK_C_SY], v0, v1);
+        acc[LBK_C_YY] = fma2<MASK>(yv, yv, acc[LBK_C_YY], v0, v1);
+        acc[LBK_C_GG] = fma2<MASK>(g2, g2, acc[LBK_C_GG], v0, v1);
+        acc[LBK_C_SG] = fma2<MASK>(sv, g2, acc[LBK_C_SG], v0, v1);
+        acc[LBK_C_DPHI] = fma2<MASK>(g2, r.d, acc[LBK_C_DPHI], v0, v1);
+    }
+};
+
+template <int OBJ, int DMODE, bool NT>
 __global__ __launch_bounds__(LB_BLOCK) void k_commit(const double* __restrict__ x, DirArgs da, double alpha,
                                                      double* __restrict__ xn, double* __restrict__ gn,
                                                      double* __restrict__ so, double* __restrict__ yo,
@@ -550,78 +689,7 @@ __global__ __launch_bounds__(LB_BLOCK) void k_commit(const double* __restrict__ 
         const double alph = da.rho * slot_total(da.pa);
         da.coef = alph - beta;  // r[j] += s[j] * (alpha[i] - beta)  (lbfgs.cpp:137)
     }
-    const Seg s = seg_setup(geo);
-    double acc[7] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-    const int64_t n = geo.n;
-    const double* __restrict__ g = da.g;
-    for (int u0 = 0; u0 < s.nrows; u0 += UO) {
-        double2 xv[UO], gv[UO], dd[UO], z[UO], gx[UO];
-        double zh[UO];
-#pragma unroll
-        for (int j = 0; j < UO; ++j) {
-            if (u0 + j < s.nrows) {
-                const int64_t i = s.lb + row_off(s, u0 + j);
-                xv[j] = ld2(x + i);
-                gv[j] = ld2(g + i);
-                dd[j] = load_dir<DMODE>(da, i, gv[j]);
-                if (OBJ == LBK_OBJ_NONE) gx[j] = ld2(gn + i);
-                z[j].x = xv[j].x + alpha * dd[j].x;
-                z[j].y = xv[j].y + alpha * dd[j].y;
-                zh[j] = 0.0;
-                if (OBJ != LBK_OBJ_NONE && OBJ != LBK_OBJ_QUAD_SEPARABLE && (s.lane == 0 || s.lane == 63)) {
-                    const int64_t hi = (s.lane == 0) ? i - 1 : i + 2;
-                    if (hi >= -1 && hi <= geo.n_loc) zh[j] = x[hi] + alpha * load_dir1<DMODE>(da, hi);
-                }
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < UO; ++j) {
-            if (u0 + j < s.nrows) {
-                const int64_t o = row_off(s, u0 + j);
-                const int64_t e0 = s.sbeg + o;
-                const int64_t i = s.lb + o;
-                const bool v0 = o < s.len, v1 = o + 1 < s.len;
-                double2 g2;
-                if (OBJ == LBK_OBJ_NONE) {
-                    g2 = gx[j];
-                } else {
-                    double zl, zr;
-                    neighbours(z[j].x, z[j].y, zh[j], s.lane, zl, zr);
-                    const bool p0 = e0 + 1 < n, p1 = e0 + 2 < n;
-                    if (v0 && obj_has_term<OBJ>(p0)) acc[LBK_C_F] = acc[LBK_C_F] + obj_term<OBJ>(z[j].x, z[j].y, p0);
-                    if (v1 && obj_has_term<OBJ>(p1)) acc[LBK_C_F] = acc[LBK_C_F] + obj_term<OBJ>(z[j].y, zr, p1);
-                    g2.x = obj_grad<OBJ>(zl, z[j].x, z[j].y, e0 > 0, p0);
-                    g2.y = obj_grad<OBJ>(z[j].x, z[j].y, zr, true, p1);
-                    st2m(gn + i, g2, v0, v1);
-                }
-                st2m(xn + i, z[j], v0, v1);
-                double2 sv, yv;
-                sv.x = z[j].x - xv[j].x;
-                sv.y = z[j].y - xv[j].y;
-                yv.x = g2.x - gv[j].x;
-                yv.y = g2.y - gv[j].y;
-                st2m(so + i, sv, v0, v1);
-                st2m(yo + i, yv, v0, v1);
-                if (v0) {
-                    acc[LBK_C_GD] = fma(gv[j].x, dd[j].x, acc[LBK_C_GD]);
-                    acc[LBK_C_SY] = fma(sv.x, yv.x, acc[LBK_C_SY]);
-                    acc[LBK_C_YY] = fma(yv.x, yv.x, acc[LBK_C_YY]);
-                    acc[LBK_C_GG] = fma(g2.x, g2.x, acc[LBK_C_GG]);
-                    acc[LBK_C_SG] = fma(sv.x, g2.x, acc[LBK_C_SG]);
-                    acc[LBK_C_DPHI] = fma(g2.x, dd[j].x, acc[LBK_C_DPHI]);
-                }
-                if (v1) {
-                    acc[LBK_C_GD] = fma(gv[j].y, dd[j].y, acc[LBK_C_GD]);
-                    acc[LBK_C_SY] = fma(sv.y, yv.y, acc[LBK_C_SY]);
-                    acc[LBK_C_YY] = fma(yv.y, yv.y, acc[LBK_C_YY]);
-                    acc[LBK_C_GG] = fma(g2.y, g2.y, acc[LBK_C_GG]);
-                    acc[LBK_C_SG] = fma(sv.y, g2.y, acc[LBK_C_SG]);
-                    acc[LBK_C_DPHI] = fma(g2.y, dd[j].y, acc[LBK_C_DPHI]);
-                }
-            }
-        }
-    }
-    reduce_publish<7>(acc, geo, red);
+    run_pass<OpCommit<OBJ, DMODE, NT>, 7>(OpCommit<OBJ, DMODE, NT>{x, da, alpha, xn, gn, so, yo, geo.n, geo.n_loc}, geo, red);
 }
 
 // z = x + alpha d over the whole local range incl. ghosts (host-callback objectives)
@@ -683,6 +751,7 @@ struct lbk_ctx {
     int64_t prof_n[LBK_K_COUNT];
     double prof_bytes[LBK_K_COUNT];
     double bytes_total;
+    int nt;  // non-temporal streaming loads/stores
 };
 
 namespace {
@@ -814,8 +883,13 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
     G.elem_lo = std::min<int64_t>(G.seg_lo * G.L, n);
     const int64_t elem_hi = std::min<int64_t>(G.seg_hi * G.L, n);
     G.n_loc = elem_hi - G.elem_lo;
-    // front pad 2 (ghost at -1, 16-B alignment of element 0), back: whole rows + halo
-    c->vec_doubles = 2 + ((G.n_loc + 511) / 512) * 512 + 512;
+    // front pad 32 doubles: ghost at [-1] and element 0 on a 256-B boundary, so every 1-KiB
+    // row load/store covers whole cache lines; back: whole rows + halo
+    // non-temporal streaming once a vector no longer fits comfortably in the 256 MiB Infinity
+    // Cache (override: LBFGS_NT=0/1)
+    c->nt = (G.n_loc * 8 > (64ll << 20)) ? 1 : 0;
+    if (const char* e = getenv("LBFGS_NT")) c->nt = atoi(e) != 0;
+    c->vec_doubles = LBK_FRONT + ((G.n_loc + 511) / 512) * 512 + 512;
     *out = c;
 #define CK(expr)                                                                             \
     do {                                                                                     \
@@ -880,12 +954,12 @@ double* lbk_vec_alloc(lbk_ctx* c) {
         (void)hipFree(p);
         return nullptr;
     }
-    return p + 2;
+    return p + LBK_FRONT;
 }
 
 void lbk_vec_free(lbk_ctx* c, double* v) {
     (void)c;
-    if (v) (void)hipFree(v - 2);
+    if (v) (void)hipFree(v - LBK_FRONT);
 }
 
 int lbk_upload(lbk_ctx* c, double* dst, const double* host_global) {
@@ -923,11 +997,22 @@ int lbk_copy(lbk_ctx* c, double* dst, const double* src) {
     return 0;
 }
 
+#define NT_DISPATCH(c, ...)                            \
+    do {                                               \
+        if ((c)->nt) {                                 \
+            constexpr bool NT_ = true;                 \
+            __VA_ARGS__;                               \
+        } else {                                       \
+            constexpr bool NT_ = false;                \
+            __VA_ARGS__;                               \
+        }                                              \
+    } while (0)
+
 int lbk_dot(lbk_ctx* c, const double* a, const double* b, int slot) {
     Geo g = kgeo(c);
     Red r = kred(c, slot);
     return launch(c, LBK_K_DOT, 2, slot, [&] {
-        hipLaunchKernelGGL(k_dot, dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, a, b, g, r);
+        NT_DISPATCH(c, hipLaunchKernelGGL(k_dot<NT_>, dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, a, b, g, r));
     });
 }
 
@@ -937,7 +1022,7 @@ int lbk_axpy_dot(lbk_ctx* c, double* qout, const double* qin, const double* y, c
     Red r = kred(c, slot);
     const double* pa = sref(c, ref_alpha);
     return launch(c, LBK_K_AXPY_DOT, 4, slot, [&] {
-        hipLaunchKernelGGL(k_axpy_dot, dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, qout, qin, y, s, rho, pa, g, r);
+        NT_DISPATCH(c, hipLaunchKernelGGL(k_axpy_dot<NT_>, dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, qout, qin, y, s, rho, pa, g, r));
     });
 }
 
@@ -947,7 +1032,7 @@ int lbk_mid(lbk_ctx* c, double* rout, const double* qin, const double* y0, doubl
     Red r = kred(c, slot);
     const double* pa = sref(c, ref_alpha);
     return launch(c, LBK_K_MID, 3, slot, [&] {
-        hipLaunchKernelGGL(k_mid, dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, rout, qin, y0, rho0, gamma, pa, g, r);
+        NT_DISPATCH(c, hipLaunchKernelGGL(k_mid<NT_>, dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, rout, qin, y0, rho0, gamma, pa, g, r));
     });
 }
 
@@ -958,7 +1043,7 @@ int lbk_axpy2_dot(lbk_ctx* c, double* rr, const double* s, const double* ynext, 
     const double* pb = sref(c, ref_beta);
     const double* pa = sref(c, ref_alpha);
     return launch(c, LBK_K_AXPY2_DOT, 4, slot, [&] {
-        hipLaunchKernelGGL(k_axpy2_dot, dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, rr, s, ynext, rho, pb, pa, g, r);
+        NT_DISPATCH(c, hipLaunchKernelGGL(k_axpy2_dot<NT_>, dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, rr, s, ynext, rho, pb, pa, g, r));
     });
 }
 
@@ -969,7 +1054,7 @@ int lbk_last(lbk_ctx* c, double* dout, const double* rr, const double* s, const 
     const double* pb = sref(c, ref_beta);
     const double* pa = sref(c, ref_alpha);
     return launch(c, LBK_K_LAST, 4, slot, [&] {
-        hipLaunchKernelGGL(k_last, dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, dout, rr, s, gg, rho, pb, pa, g, r);
+        NT_DISPATCH(c, hipLaunchKernelGGL(k_last<NT_>, dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, dout, rr, s, gg, rho, pb, pa, g, r));
     });
 }
 
@@ -977,16 +1062,24 @@ int lbk_negdot(lbk_ctx* c, double* dout, const double* gg, int slot) {
     Geo g = kgeo(c);
     Red r = kred(c, slot);
     return launch(c, LBK_K_NEGDOT, 2, slot, [&] {
-        hipLaunchKernelGGL(k_negdot, dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, dout, gg, g, r);
+        NT_DISPATCH(c, hipLaunchKernelGGL(k_negdot<NT_>, dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, dout, gg, g, r));
     });
 }
 
-#define OBJ_DISPATCH(obj, TEMPLATE_CALL)                                      \
+#define OBJ_DISPATCH1(obj, ...)                                      \
     switch (obj) {                                                            \
-        case LBK_OBJ_ROSENBROCK: { constexpr int O_ = LBK_OBJ_ROSENBROCK; TEMPLATE_CALL; } break;         \
-        case LBK_OBJ_QUAD_TRIDIAG: { constexpr int O_ = LBK_OBJ_QUAD_TRIDIAG; TEMPLATE_CALL; } break;     \
-        case LBK_OBJ_QUAD_SEPARABLE: { constexpr int O_ = LBK_OBJ_QUAD_SEPARABLE; TEMPLATE_CALL; } break; \
+        case LBK_OBJ_ROSENBROCK: { constexpr int O_ = LBK_OBJ_ROSENBROCK; __VA_ARGS__; } break;         \
+        case LBK_OBJ_QUAD_TRIDIAG: { constexpr int O_ = LBK_OBJ_QUAD_TRIDIAG; __VA_ARGS__; } break;     \
+        case LBK_OBJ_QUAD_SEPARABLE: { constexpr int O_ = LBK_OBJ_QUAD_SEPARABLE; __VA_ARGS__; } break; \
         default: return -1;                                                   \
+    }
+#define OBJ_DISPATCH(obj, ...)                             \
+    if (c->nt) {                                           \
+        constexpr bool NT_ = true;                         \
+        OBJ_DISPATCH1(obj, __VA_ARGS__);                   \
+    } else {                                               \
+        constexpr bool NT_ = false;                        \
+        OBJ_DISPATCH1(obj, __VA_ARGS__);                   \
     }
 
 int lbk_eval(lbk_ctx* c, int obj, const double* x, double* gout, int slot) {
@@ -994,7 +1087,7 @@ int lbk_eval(lbk_ctx* c, int obj, const double* x, double* gout, int slot) {
     Red r = kred(c, slot);
     DirArgs da = {nullptr, nullptr, nullptr, 0.0, nullptr, nullptr, 0.0};
     return launch(c, LBK_K_EVAL, gout ? 2 : 1, slot, [&] {
-        OBJ_DISPATCH(obj, hipLaunchKernelGGL((k_objective<O_, true, true>), dim3(nblocks(c)), dim3(LB_BLOCK), 0,
+        OBJ_DISPATCH(obj, hipLaunchKernelGGL((k_objective<O_, true, true, NT_>), dim3(nblocks(c)), dim3(LB_BLOCK), 0,
                                              c->stream, x, da, 0.0, gout, g, r));
         return 0;
     });
@@ -1007,10 +1100,10 @@ int lbk_trial(lbk_ctx* c, int obj, const double* x, const double* d, double alph
     const int kind = gout ? LBK_K_TRIAL_FG : LBK_K_TRIAL_F;
     return launch(c, kind, gout ? 3 : 2, slot, [&] {
         if (gout) {
-            OBJ_DISPATCH(obj, hipLaunchKernelGGL((k_objective<O_, false, true>), dim3(nblocks(c)), dim3(LB_BLOCK),
+            OBJ_DISPATCH(obj, hipLaunchKernelGGL((k_objective<O_, false, true, NT_>), dim3(nblocks(c)), dim3(LB_BLOCK),
                                                  0, c->stream, x, da, alpha, gout, g, r));
         } else {
-            OBJ_DISPATCH(obj, hipLaunchKernelGGL((k_objective<O_, false, false>), dim3(nblocks(c)), dim3(LB_BLOCK),
+            OBJ_DISPATCH(obj, hipLaunchKernelGGL((k_objective<O_, false, false, NT_>), dim3(nblocks(c)), dim3(LB_BLOCK),
                                                  0, c->stream, x, da, alpha, gout, g, r));
         }
         return 0;
@@ -1030,22 +1123,22 @@ int lbk_commit(lbk_ctx* c, int obj, int dmode, const double* x, const double* ds
     double passes = 4.0 + (dmode == LBK_D_BUF ? 3.0 : dmode == LBK_D_NEG_G ? 2.0 : 4.0);
     return launch(c, LBK_K_COMMIT, passes, slot, [&] {
         if (obj == LBK_OBJ_NONE) {
-            switch (dmode) {
-                case LBK_D_BUF: hipLaunchKernelGGL((k_commit<LBK_OBJ_NONE, LBK_D_BUF>), dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, x, da, alpha, xn, gn, s_out, y_out, g, r); break;
-                case LBK_D_NEG_G: hipLaunchKernelGGL((k_commit<LBK_OBJ_NONE, LBK_D_NEG_G>), dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, x, da, alpha, xn, gn, s_out, y_out, g, r); break;
-                default: hipLaunchKernelGGL((k_commit<LBK_OBJ_NONE, LBK_D_TWOLOOP>), dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, x, da, alpha, xn, gn, s_out, y_out, g, r); break;
-            }
+            NT_DISPATCH(c, switch (dmode) {
+                case LBK_D_BUF: hipLaunchKernelGGL((k_commit<LBK_OBJ_NONE, LBK_D_BUF, NT_>), dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, x, da, alpha, xn, gn, s_out, y_out, g, r); break;
+                case LBK_D_NEG_G: hipLaunchKernelGGL((k_commit<LBK_OBJ_NONE, LBK_D_NEG_G, NT_>), dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, x, da, alpha, xn, gn, s_out, y_out, g, r); break;
+                default: hipLaunchKernelGGL((k_commit<LBK_OBJ_NONE, LBK_D_TWOLOOP, NT_>), dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, x, da, alpha, xn, gn, s_out, y_out, g, r); break;
+            });
             return 0;
         }
         switch (dmode) {
             case LBK_D_BUF:
-                OBJ_DISPATCH(obj, hipLaunchKernelGGL((k_commit<O_, LBK_D_BUF>), dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, x, da, alpha, xn, gn, s_out, y_out, g, r));
+                OBJ_DISPATCH(obj, hipLaunchKernelGGL((k_commit<O_, LBK_D_BUF, NT_>), dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, x, da, alpha, xn, gn, s_out, y_out, g, r));
                 break;
             case LBK_D_NEG_G:
-                OBJ_DISPATCH(obj, hipLaunchKernelGGL((k_commit<O_, LBK_D_NEG_G>), dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, x, da, alpha, xn, gn, s_out, y_out, g, r));
+                OBJ_DISPATCH(obj, hipLaunchKernelGGL((k_commit<O_, LBK_D_NEG_G, NT_>), dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, x, da, alpha, xn, gn, s_out, y_out, g, r));
                 break;
             default:
-                OBJ_DISPATCH(obj, hipLaunchKernelGGL((k_commit<O_, LBK_D_TWOLOOP>), dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, x, da, alpha, xn, gn, s_out, y_out, g, r));
+                OBJ_DISPATCH(obj, hipLaunchKernelGGL((k_commit<O_, LBK_D_TWOLOOP, NT_>), dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, x, da, alpha, xn, gn, s_out, y_out, g, r));
                 break;
         }
         return 0;

@@ -178,7 +178,8 @@ def test_trajectory_vs_reference_golden(name):
 
 
 def test_reference_x_trajectory_small():
-    """n=100: the full iterate x_k of the reference for k <= 40 within 1e-10 relative."""
+    """n=100: the full iterate x_k of the reference for k < 40 (its measured x horizon)
+    within 1e-10 relative."""
     meta, g = O.load_golden("rosen_n100_m5_bt")
     n = meta["n"]
     c = ctx(n, meta["m"])

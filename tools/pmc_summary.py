@@ -1,0 +1,56 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 outputs into profiles/: kernel stats (trace) and PMC byte counters.
+
+usage: python tools/pmc_summary.py <trace_dir> <fetch_dir> <write_dir> <out.json> [n]
+
+FETCH_SIZE / WRITE_SIZE are in KiB per dispatch. On gfx950 FETCH_SIZE counts half of the bytes
+of wide (16 B/lane) coalesced streaming reads (MI355X_MICROARCH.md §HBM), so the corrected HBM
+read bytes are 2 * FETCH_SIZE * 1024; WRITE_SIZE is exact for 16-B streaming stores.
+"""
+import collections
+import csv
+import json
+import re
+import sys
+
+
+def short(name):
+    name = name.replace("(anonymous namespace)::", "")
+    name = re.sub(r"^void ", "", name)
+    m = re.match(r"([A-Za-z_0-9]+(?:<[^>]*>)?)", name)
+    return m.group(1) if m else name[:40]
+
+
+def main(trace_dir, fetch_dir, write_dir, out, n=None):
+    res = collections.OrderedDict()
+    for r in csv.DictReader(open(f"{trace_dir}/run_kernel_stats.csv")):
+        k = short(r["Name"])
+        res.setdefault(k, {})
+        res[k].update(calls=int(r["Calls"]), avg_us=float(r["AverageNs"]) / 1e3,
+                      total_pct=float(r["Percentage"]))
+    for tag, d in [("FETCH_SIZE", fetch_dir), ("WRITE_SIZE", write_dir)]:
+        agg = collections.defaultdict(list)
+        for r in csv.DictReader(open(f"{d}/run_counter_collection.csv")):
+            agg[short(r["Kernel_Name"])].append(float(r["Counter_Value"]))
+        for k, v in agg.items():
+            res.setdefault(k, {})[tag + "_KiB"] = sum(v) / len(v)
+    for k, v in res.items():
+        if "FETCH_SIZE_KiB" in v and "WRITE_SIZE_KiB" in v:
+            rd = 2 * v["FETCH_SIZE_KiB"] * 1024
+            wr = v["WRITE_SIZE_KiB"] * 1024
+            v["hbm_read_bytes_corrected"] = rd
+            v["hbm_write_bytes"] = wr
+            v["hbm_bytes_per_launch"] = rd + wr
+            if n:
+                v["read_vectors"] = rd / (8 * n)
+                v["write_vectors"] = wr / (8 * n)
+            if "avg_us" in v:
+                v["measured_GBps"] = (rd + wr) / (v["avg_us"] * 1e-6) / 1e9
+    json.dump(res, open(out, "w"), indent=1)
+    for k, v in res.items():
+        print(f"{k:34s} " + " ".join(f"{kk}={vv:.4g}" if isinstance(vv, float) else f"{kk}={vv}"
+                                      for kk, vv in v.items()))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2], sys.argv[3], sys.argv[4], float(sys.argv[5]) if len(sys.argv) > 5 else None)
