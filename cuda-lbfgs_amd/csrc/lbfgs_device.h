@@ -62,9 +62,17 @@ typedef struct {
 } lbk_geo;
 
 typedef struct lbk_ctx lbk_ctx;
+typedef struct lbk_group lbk_group; /* host exchange group for emulated ranks (tests) */
 
-/* lifecycle */
-int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const void* nccl_id);
+/* lifecycle. world > 1: RCCL communicator from nccl_id, or the host group grp */
+int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const void* nccl_id,
+               lbk_group* grp);
+/* canonical geometry and this rank's shard, no device needed (0, or < 0 if not shardable) */
+int lbk_geometry_plan(int64_t n, int rank, int world, lbk_geo* out);
+lbk_group* lbk_group_create(int world);
+void lbk_group_destroy(lbk_group* g);
+/* sharded: the slot whose all-gather carries the neighbours' edge d (after lbk_last/negdot) */
+void lbk_set_ghost_slot(lbk_ctx* c, int slot);
 void lbk_destroy(lbk_ctx* c);
 const lbk_geo* lbk_geometry(const lbk_ctx* c);
 const char* lbk_last_error(const lbk_ctx* c);

@@ -188,18 +188,43 @@ static void free_vectors(lbfgs_ctx* c) {
     }
 }
 
-int lbfgs_ctx_create_sharded(lbfgs_ctx** out, int64_t n, int m, int device, int rank, int world,
-                             const void* unique_id) {
+struct lbfgs_host_group {
+    lbk_group* g;
+    int world;
+};
+
+int lbfgs_host_group_create(lbfgs_host_group** out, int world) {
+    if (!out || world < 1 || world > 8 || (8 % world) != 0) return LBFGS_ERR_BAD_ARG;
+    lbfgs_host_group* h = (lbfgs_host_group*)calloc(1, sizeof *h);
+    if (!h) return LBFGS_ERR_NOMEM;
+    h->g = lbk_group_create(world);
+    h->world = world;
+    if (!h->g) {
+        free(h);
+        return LBFGS_ERR_NOMEM;
+    }
+    *out = h;
+    return 0;
+}
+
+void lbfgs_host_group_destroy(lbfgs_host_group* h) {
+    if (!h) return;
+    lbk_group_destroy(h->g);
+    free(h);
+}
+
+static int ctx_create(lbfgs_ctx** out, int64_t n, int m, int device, int rank, int world,
+                      const void* unique_id, lbk_group* grp) {
     if (!out) return LBFGS_ERR_BAD_ARG;
     *out = NULL;
     if (n < 1 || m < 1 || m > MMAX || world < 1 || (8 % world) != 0 || rank < 0 || rank >= world)
         return LBFGS_ERR_BAD_ARG;
-    if (world > 1 && !unique_id) return LBFGS_ERR_BAD_ARG;
+    if (world > 1 && !unique_id && !grp) return LBFGS_ERR_BAD_ARG;
     lbfgs_ctx* c = (lbfgs_ctx*)calloc(1, sizeof(lbfgs_ctx));
     if (!c) return LBFGS_ERR_NOMEM;
     c->n = n;
     c->m = m;
-    int rc = lbk_create(&c->dev, device, n, rank, world, unique_id);
+    int rc = lbk_create(&c->dev, device, n, rank, world, unique_id, grp);
     if (rc != 0) {
         if (c->dev) {
             snprintf(c->err, sizeof c->err, "%s", lbk_last_error(c->dev));
@@ -229,8 +254,19 @@ int lbfgs_ctx_create_sharded(lbfgs_ctx** out, int64_t n, int m, int device, int 
     return 0;
 }
 
+int lbfgs_ctx_create_sharded(lbfgs_ctx** out, int64_t n, int m, int device, int rank, int world,
+                             const void* unique_id) {
+    return ctx_create(out, n, m, device, rank, world, unique_id, NULL);
+}
+
+int lbfgs_ctx_create_emulated(lbfgs_ctx** out, int64_t n, int m, int device, int rank,
+                              lbfgs_host_group* grp) {
+    if (!grp) return LBFGS_ERR_BAD_ARG;
+    return ctx_create(out, n, m, device, rank, grp->world, NULL, grp->g);
+}
+
 int lbfgs_ctx_create(lbfgs_ctx** out, int64_t n, int m, int device) {
-    return lbfgs_ctx_create_sharded(out, n, m, device, 0, 1, NULL);
+    return ctx_create(out, n, m, device, 0, 1, NULL, NULL);
 }
 
 void lbfgs_ctx_destroy(lbfgs_ctx* c) {
@@ -249,6 +285,14 @@ void lbfgs_ctx_destroy(lbfgs_ctx* c) {
 }
 
 const char* lbfgs_last_error(const lbfgs_ctx* c) { return c ? c->err : "null context"; }
+
+int lbfgs_shard_range(int64_t n, int rank, int world, int64_t* elem_lo, int64_t* n_loc) {
+    lbk_geo g;
+    if (lbk_geometry_plan(n, rank, world, &g) != 0) return LBFGS_ERR_BAD_ARG;
+    if (elem_lo) *elem_lo = g.elem_lo;
+    if (n_loc) *n_loc = g.n_loc;
+    return 0;
+}
 
 int lbfgs_local_range(const lbfgs_ctx* c, int64_t* elem_lo, int64_t* n_loc) {
     if (!c) return LBFGS_ERR_BAD_ARG;
@@ -293,6 +337,7 @@ static int materialize_d(lbfgs_ctx* c) {
     } else if (c->dmode == LBK_D_NEG_G) {
         DEV(lbk_negdot(c->dev, c->d, c->g, SLOT_LAST(m)));
     }
+    lbk_set_ghost_slot(c->dev, SLOT_LAST(m)); /* sharded: neighbours' edge d rides this slot */
     c->dmode = LBK_D_BUF;
     c->d_ready = 1;
     return 0;
@@ -572,16 +617,27 @@ static int iterate(lbfgs_ctx* c) {
     double tot[LBK_KMAX];
     double gd;
     c->a0 = c->K.initial_step;
+    const int sharded = c->geo->world > 1;
     if (c->obj != LBFGS_OBJ_HOST) {
-        /* fused: last two-loop pass + first trial at a0 + commit */
-        rc = commit(c, dmode, c->a0, cslot, tot);
+        /* single GPU: last two-loop pass + first trial at a0 + commit fused in one pass.
+         * Sharded: d is materialised first so that its edge values reach the neighbouring
+         * ranks (halo of the stencil) through the all-gather of its reduction slot. */
+        if (sharded) {
+            rc = materialize_d(c);
+            if (rc) return rc;
+        }
+        rc = commit(c, c->dmode, c->a0, cslot, tot);
         if (rc) return rc;
         gd = tot[LBK_C_GD];
         if (gd >= 0) {
             say(c, "Warning: Not a descent direction, using gradient\n");
             c->dmode = dmode = LBK_D_NEG_G;
             c->d_ready = 0;
-            rc = commit(c, dmode, c->a0, cslot, tot);
+            if (sharded) {
+                rc = materialize_d(c);
+                if (rc) return rc;
+            }
+            rc = commit(c, c->dmode, c->a0, cslot, tot);
             if (rc) return rc;
             gd = tot[LBK_C_GD];
         }

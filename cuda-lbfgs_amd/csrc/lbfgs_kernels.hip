@@ -17,7 +17,7 @@
 // slot and the consuming kernel forms the fixed-order total in its prologue.
 //
 // Canonical reduction order (restated in oracle/lbfgs_oracle.c for checking):
-//   segment s = [s L, min((s+1) L, n)), L = roundup(ceil(n/8192), 512), one 256-thread
+//   segment s = [s L, min((s+1) L, n)), L = max(512, roundup(ceil(n/8192), 128)), one 256-thread
 //   workgroup per segment; thread (w, lane) visits rows 4u + w (128 elements each), two
 //   elements per lane (one 16-B load), accumulating with v_fma_f64 (dots) / v_add_f64 (sums);
 //   wave butterfly (shfl_xor 1..32) -> ((w0 + w1) + (w2 + w3)) = segment partial;
@@ -34,6 +34,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <pthread.h>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -47,7 +48,8 @@ namespace {
 
 struct Geo {
     int64_t n, L, nseg, seg_lo, elem_lo, n_loc;
-    int g_lo;
+    int g_lo, g_hi;
+    double* edge_slot;  // sharded: where d[0] / d[n_loc-1] of this rank are published
 };
 
 struct Red {
@@ -55,10 +57,6 @@ struct Red {
     unsigned* cnt;     // [LBK_GROUPS] tickets
     double* slot;      // this launch's result slot [LBK_GROUPS][LBK_KMAX]
 };
-
-__device__ __forceinline__ double2 ld2(const double* p) {
-    return *reinterpret_cast<const double2*>(p);
-}
 
 // Streaming loads/stores; NT = non-temporal (the vectors are touched once per pass and, at
 // the benchmark sizes, are far larger than the 256 MiB Infinity Cache): +6 % on the 3-read /
@@ -410,6 +408,17 @@ struct OpAxpy2Dot {  // r += s (alpha - beta);  acc += ynext . r      (:159-164)
     }
 };
 
+// Sharded runs: the rank's first and last d are written into spare components of the
+// result slot (group g_lo comp 1, group g_hi-1 comp 2), which the slot all-gather delivers
+// to the neighbouring ranks as their halo of d.
+__device__ __forceinline__ void publish_edges(double* edge_slot, int64_t i, int64_t n_loc, int g_lo, int g_hi,
+                                              double2 d, bool v0, bool v1) {
+    if (!edge_slot) return;
+    if (i == 0 && v0) edge_slot[g_lo * LBK_KMAX + 1] = d.x;
+    if (i + 1 == n_loc - 1 && v1) edge_slot[(g_hi - 1) * LBK_KMAX + 2] = d.y;
+    if (i == n_loc - 1 && v0) edge_slot[(g_hi - 1) * LBK_KMAX + 2] = d.x;
+}
+
 template <bool NT>
 struct OpLast {  // d = -(r + s (alpha - beta));  acc += g . d        (:163-171)
     double* __restrict__ dout;
@@ -417,6 +426,9 @@ struct OpLast {  // d = -(r + s (alpha - beta));  acc += g . d        (:163-171)
     const double* __restrict__ s;
     const double* __restrict__ g;
     double coef;
+    double* edge_slot;
+    int64_t n_loc;
+    int g_lo, g_hi;
     struct Row {
         double2 r, s, g;
     };
@@ -431,6 +443,7 @@ struct OpLast {  // d = -(r + s (alpha - beta));  acc += g . d        (:163-171)
         d.x = -(w.r.x + w.s.x * coef);
         d.y = -(w.r.y + w.s.y * coef);
         st2<MASK, NT>(dout + i, d, v0, v1);
+        publish_edges(edge_slot, i, n_loc, g_lo, g_hi, d, v0, v1);
         acc[0] = fma2<MASK>(w.g, d, acc[0], v0, v1);
     }
 };
@@ -439,6 +452,9 @@ template <bool NT>
 struct OpNegDot {  // d = -g;  acc += g . d                          (:90, :151-152)
     double* __restrict__ dout;
     const double* __restrict__ g;
+    double* edge_slot;
+    int64_t n_loc;
+    int g_lo, g_hi;
     struct Row {
         double2 g;
     };
@@ -449,6 +465,7 @@ struct OpNegDot {  // d = -g;  acc += g . d                          (:90, :151-
         d.x = -w.g.x;
         d.y = -w.g.y;
         st2<MASK, NT>(dout + i, d, v0, v1);
+        publish_edges(edge_slot, i, n_loc, g_lo, g_hi, d, v0, v1);
         acc[0] = fma2<MASK>(w.g, d, acc[0], v0, v1);
     }
 };
@@ -504,13 +521,14 @@ __global__ __launch_bounds__(LB_BLOCK) void k_last(double* __restrict__ dout, co
                                                    const double* __restrict__ pa, Geo geo, Red red) {
     const double beta = rho * slot_total(pb);
     const double alpha = rho * slot_total(pa);
-    run_pass<OpLast<NT>, 1>(OpLast<NT>{dout, r, sv, g, alpha - beta}, geo, red);
+    run_pass<OpLast<NT>, 1>(OpLast<NT>{dout, r, sv, g, alpha - beta, geo.edge_slot, geo.n_loc, geo.g_lo, geo.g_hi},
+                             geo, red);
 }
 
 template <bool NT>
 __global__ __launch_bounds__(LB_BLOCK) void k_negdot(double* __restrict__ dout, const double* __restrict__ g,
                                                      Geo geo, Red red) {
-    run_pass<OpNegDot<NT>, 1>(OpNegDot<NT>{dout, g}, geo, red);
+    run_pass<OpNegDot<NT>, 1>(OpNegDot<NT>{dout, g, geo.edge_slot, geo.n_loc, geo.g_lo, geo.g_hi}, geo, red);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -524,6 +542,8 @@ struct DirArgs {
     const double* pa;    // D_TWOLOOP: slot of s_{h-1} . q   (alpha = rho * total)
     const double* pb;    // D_TWOLOOP: slot of y_{h-1} . r   (beta  = rho * total)
     double rho;
+    const double* ghost;  // sharded, D_BUF: all-gathered slot holding the neighbours' edge d
+    int g_lo, g_hi;
 };
 
 template <int DMODE, bool NT>
@@ -549,6 +569,13 @@ __device__ __forceinline__ double load_dir1(const DirArgs& da, int64_t i) {
     return -(da.dsrc[i] + da.s[i] * da.coef);
 }
 
+// neighbour rank's edge d, from the all-gathered slot (see publish_edges)
+__device__ __forceinline__ double ghost_d(const DirArgs& da, int64_t hi, int64_t n_loc) {
+    // left ghost = last d of the rank owning group g_lo-1; right ghost = first d of group g_hi
+    return hi < 0 ? da.ghost[(da.g_lo - 1) * LBK_KMAX + 2] : da.ghost[da.g_hi * LBK_KMAX + 1];
+    (void)n_loc;
+}
+
 template <int OBJ>
 __device__ __forceinline__ bool needs_halo() {
     return OBJ == LBK_OBJ_ROSENBROCK || OBJ == LBK_OBJ_QUAD_TRIDIAG;
@@ -563,7 +590,18 @@ __device__ __forceinline__ double halo_z(const double* __restrict__ x, const Dir
         const int lane = threadIdx.x & 63;
         if (lane == 0 || lane == 63) {
             const int64_t hi = (lane == 0) ? i - 1 : i + 2;
-            if (hi >= -1 && hi <= n_loc) zh = NO_DIR ? x[hi] : x[hi] + alpha * load_dir1<DMODE>(da, hi);
+            if (hi >= -1 && hi <= n_loc) {
+                if (NO_DIR) {
+                    zh = x[hi];
+                } else {
+                    double dh;
+                    if (DMODE == LBK_D_BUF && da.ghost && (hi == -1 || hi == n_loc))
+                        dh = ghost_d(da, hi, n_loc);
+                    else
+                        dh = load_dir1<DMODE>(da, hi);
+                    zh = x[hi] + alpha * dh;
+                }
+            }
         }
     }
     return zh;
@@ -689,6 +727,12 @@ __global__ __launch_bounds__(LB_BLOCK) void k_commit(const double* __restrict__ 
         const double alph = da.rho * slot_total(da.pa);
         da.coef = alph - beta;  // r[j] += s[j] * (alpha[i] - beta)  (lbfgs.cpp:137)
     }
+    // sharded: keep the x ghosts current (x_new = x + alpha d at the neighbours' edge elements)
+    if (DMODE == LBK_D_BUF && da.ghost && threadIdx.x == 0) {
+        if (blockIdx.x == 0 && geo.elem_lo > 0) xn[-1] = x[-1] + alpha * ghost_d(da, -1, geo.n_loc);
+        if (blockIdx.x == gridDim.x - 1 && geo.elem_lo + geo.n_loc < geo.n)
+            xn[geo.n_loc] = x[geo.n_loc] + alpha * ghost_d(da, geo.n_loc, geo.n_loc);
+    }
     run_pass<OpCommit<OBJ, DMODE, NT>, 7>(OpCommit<OBJ, DMODE, NT>{x, da, alpha, xn, gn, so, yo, geo.n, geo.n_loc}, geo, red);
 }
 
@@ -725,6 +769,16 @@ __global__ void k_checksum(const double* __restrict__ x, int64_t n_loc, int64_t 
 // =========================================================================================
 // Host side of the device layer
 // =========================================================================================
+// Host exchange group: ranks of one process (threads, one stream each, possibly on one GPU)
+// exchange the result-slot group partials through host memory instead of RCCL. Used to test
+// the sharded path on a single GPU; same data layout as the RCCL all-gather.
+struct lbk_group {
+    int world;
+    pthread_barrier_t bar;
+    double table[LBK_SLOT];
+    unsigned long long ck[LBK_GROUPS][2];
+};
+
 struct lbk_ctx {
     lbk_geo geo;
     int device;
@@ -751,7 +805,9 @@ struct lbk_ctx {
     int64_t prof_n[LBK_K_COUNT];
     double prof_bytes[LBK_K_COUNT];
     double bytes_total;
-    int nt;  // non-temporal streaming loads/stores
+    int nt;          // non-temporal streaming loads/stores
+    int ghost_slot;  // sharded: slot holding the all-gathered edge d values (-1: none)
+    lbk_group* grp;  // emulated ranks: host exchange group (tests; NULL with RCCL)
 };
 
 namespace {
@@ -775,6 +831,8 @@ Geo kgeo(const lbk_ctx* c) {
     g.elem_lo = c->geo.elem_lo;
     g.n_loc = c->geo.n_loc;
     g.g_lo = c->geo.g_lo;
+    g.g_hi = c->geo.g_hi;
+    g.edge_slot = nullptr;
     return g;
 }
 
@@ -791,6 +849,11 @@ const double* sref(const lbk_ctx* c, int ref) {
 }
 
 int nblocks(const lbk_ctx* c) { return (int)(c->geo.seg_hi - c->geo.seg_lo); }
+
+const double* ghost_ptr(const lbk_ctx* c) {
+    if (c->geo.world <= 1 || c->ghost_slot < 0) return nullptr;
+    return c->slots + (int64_t)c->ghost_slot * LBK_SLOT;
+}
 
 hipEvent_t ev_get(lbk_ctx* c) {
     if (!c->ev_free.empty()) {
@@ -818,6 +881,30 @@ int prof_flush(lbk_ctx* c) {
     return 0;
 }
 
+// Sharded runs: each rank owns groups [g_lo, g_hi) of every result slot; gather them so
+// every rank holds all 8 (one RCCL all-gather of (8/world) x KMAX doubles per reduction, in
+// place, on the solver stream), or through the host group for emulated ranks.
+int exchange_slot(lbk_ctx* c, int slot) {
+    const int per = (c->geo.g_hi - c->geo.g_lo) * LBK_KMAX;
+    double* base = c->slots + (int64_t)slot * LBK_SLOT;
+    if (c->grp) {
+        lbk_group* G = c->grp;
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        HIPCHK(c, hipMemcpy(G->table + c->geo.g_lo * LBK_KMAX, base + c->geo.g_lo * LBK_KMAX,
+                            sizeof(double) * per, hipMemcpyDeviceToHost));
+        pthread_barrier_wait(&G->bar);
+        HIPCHK(c, hipMemcpy(base, G->table, sizeof(double) * LBK_SLOT, hipMemcpyHostToDevice));
+        pthread_barrier_wait(&G->bar);
+        return 0;
+    }
+    ncclResult_t r = ncclAllGather(base + c->geo.g_lo * LBK_KMAX, base, (size_t)per, ncclDouble, c->comm, c->stream);
+    if (r != ncclSuccess) {
+        snprintf(c->err, sizeof c->err, "ncclAllGather: %s", ncclGetErrorString(r));
+        return -3;
+    }
+    return 0;
+}
+
 // launch wrapper: byte accounting, optional event timing, all-gather of group partials
 template <class F>
 int launch(lbk_ctx* c, int kind, double vec_passes, int slot, F&& fn) {
@@ -838,16 +925,7 @@ int launch(lbk_ctx* c, int kind, double vec_passes, int slot, F&& fn) {
         HIPCHK(c, hipEventRecord(b, c->stream));
         c->pending.push_back({kind, a, b, bytes});
     }
-    if (c->geo.world > 1 && slot >= 0) {
-        // each rank owns groups [g_lo, g_hi): gather them so every rank holds all 8
-        const int per = (c->geo.g_hi - c->geo.g_lo) * LBK_KMAX;
-        double* base = c->slots + (int64_t)slot * LBK_SLOT;
-        ncclResult_t r = ncclAllGather(base + c->geo.g_lo * LBK_KMAX, base, (size_t)per, ncclDouble, c->comm, c->stream);
-        if (r != ncclSuccess) {
-            snprintf(c->err, sizeof c->err, "ncclAllGather: %s", ncclGetErrorString(r));
-            return -3;
-        }
-    }
+    if (c->geo.world > 1 && slot >= 0) return exchange_slot(c, slot);
     return 0;
 }
 
@@ -862,16 +940,14 @@ int lbk_unique_id(void* out128) {
     return 0;
 }
 
-int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const void* nccl_id) {
-    *out = nullptr;
+int lbk_geometry_plan(int64_t n, int rank, int world, lbk_geo* out) {
     if (n < 1 || world < 1 || (LBK_GROUPS % world) != 0 || rank < 0 || rank >= world) return -1;
-    lbk_ctx* c = new (std::nothrow) lbk_ctx();
-    if (!c) return -4;
-    c->device = device;
-    lbk_geo& G = c->geo;
+    lbk_geo& G = *out;
     G.n = n;
+    // segment length: whole 128-element rows, at least 512 (one row per wave); rows rather
+    // than 512-multiples keep all 8 groups populated for n >= 7.3e6 (sharding over 8 ranks)
     const int64_t per = (n + LBK_SEGS - 1) / LBK_SEGS;
-    G.L = ((per + 511) / 512) * 512;
+    G.L = ((per + 127) / 128) * 128;
     if (G.L < 512) G.L = 512;
     G.nseg = (n + G.L - 1) / G.L;
     G.rank = rank;
@@ -883,11 +959,30 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
     G.elem_lo = std::min<int64_t>(G.seg_lo * G.L, n);
     const int64_t elem_hi = std::min<int64_t>(G.seg_hi * G.L, n);
     G.n_loc = elem_hi - G.elem_lo;
+    // every rank must own at least one segment (n > (8 - 8/world) * 1024 * L)
+    if (world > 1 && (G.nseg <= (int64_t)(LBK_GROUPS - LBK_GROUPS / world) * LBK_SEG_PER_GROUP)) return -7;
+    return 0;
+}
+
+int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const void* nccl_id, lbk_group* grp) {
+    *out = nullptr;
+    lbk_ctx* c = new (std::nothrow) lbk_ctx();
+    if (!c) return -4;
+    c->device = device;
+    lbk_geo& G = c->geo;
+    const int prc = lbk_geometry_plan(n, rank, world, &G);
+    c->ghost_slot = -1;
+    c->grp = grp;
+    if (prc != 0) {
+        snprintf(c->err, sizeof c->err, "cannot shard n=%lld over %d ranks (rank %d)", (long long)n, world, rank);
+        *out = c;
+        return -1;
+    }
     // front pad 32 doubles: ghost at [-1] and element 0 on a 256-B boundary, so every 1-KiB
     // row load/store covers whole cache lines; back: whole rows + halo
     // non-temporal streaming once a vector no longer fits comfortably in the 256 MiB Infinity
-    // Cache (override: LBFGS_NT=0/1)
-    c->nt = (G.n_loc * 8 > (64ll << 20)) ? 1 : 0;
+    // Cache: +4 % at n=1e8, -1 % at n=1e7 (profiles/r01); override: LBFGS_NT=0/1
+    c->nt = (G.n_loc * 8 > (128ll << 20)) ? 1 : 0;
     if (const char* e = getenv("LBFGS_NT")) c->nt = atoi(e) != 0;
     c->vec_doubles = LBK_FRONT + ((G.n_loc + 511) / 512) * 512 + 512;
     *out = c;
@@ -912,7 +1007,7 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
     CK(hipMemset(c->slots, 0, sizeof(double) * LBK_NSLOTS * LBK_SLOT));
     CK(hipDeviceSynchronize());
 #undef CK
-    if (world > 1) {
+    if (world > 1 && !grp) {
         ncclUniqueId id;
         memcpy(&id, nccl_id, sizeof id);
         ncclResult_t r = ncclCommInitRank(&c->comm, world, id, rank);
@@ -1053,6 +1148,7 @@ int lbk_last(lbk_ctx* c, double* dout, const double* rr, const double* s, const 
     Red r = kred(c, slot);
     const double* pb = sref(c, ref_beta);
     const double* pa = sref(c, ref_alpha);
+    if (c->geo.world > 1) g.edge_slot = r.slot;
     return launch(c, LBK_K_LAST, 4, slot, [&] {
         NT_DISPATCH(c, hipLaunchKernelGGL(k_last<NT_>, dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, dout, rr, s, gg, rho, pb, pa, g, r));
     });
@@ -1061,6 +1157,7 @@ int lbk_last(lbk_ctx* c, double* dout, const double* rr, const double* s, const 
 int lbk_negdot(lbk_ctx* c, double* dout, const double* gg, int slot) {
     Geo g = kgeo(c);
     Red r = kred(c, slot);
+    if (c->geo.world > 1) g.edge_slot = r.slot;
     return launch(c, LBK_K_NEGDOT, 2, slot, [&] {
         NT_DISPATCH(c, hipLaunchKernelGGL(k_negdot<NT_>, dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, dout, gg, g, r));
     });
@@ -1085,7 +1182,7 @@ int lbk_negdot(lbk_ctx* c, double* dout, const double* gg, int slot) {
 int lbk_eval(lbk_ctx* c, int obj, const double* x, double* gout, int slot) {
     Geo g = kgeo(c);
     Red r = kred(c, slot);
-    DirArgs da = {nullptr, nullptr, nullptr, 0.0, nullptr, nullptr, 0.0};
+    DirArgs da = {nullptr, nullptr, nullptr, 0.0, nullptr, nullptr, 0.0, nullptr, c->geo.g_lo, c->geo.g_hi};
     return launch(c, LBK_K_EVAL, gout ? 2 : 1, slot, [&] {
         OBJ_DISPATCH(obj, hipLaunchKernelGGL((k_objective<O_, true, true, NT_>), dim3(nblocks(c)), dim3(LB_BLOCK), 0,
                                              c->stream, x, da, 0.0, gout, g, r));
@@ -1096,7 +1193,7 @@ int lbk_eval(lbk_ctx* c, int obj, const double* x, double* gout, int slot) {
 int lbk_trial(lbk_ctx* c, int obj, const double* x, const double* d, double alpha, double* gout, int slot) {
     Geo g = kgeo(c);
     Red r = kred(c, slot);
-    DirArgs da = {d, nullptr, nullptr, 0.0, nullptr, nullptr, 0.0};
+    DirArgs da = {d, nullptr, nullptr, 0.0, nullptr, nullptr, 0.0, ghost_ptr(c), c->geo.g_lo, c->geo.g_hi};
     const int kind = gout ? LBK_K_TRIAL_FG : LBK_K_TRIAL_F;
     return launch(c, kind, gout ? 3 : 2, slot, [&] {
         if (gout) {
@@ -1115,7 +1212,8 @@ int lbk_commit(lbk_ctx* c, int obj, int dmode, const double* x, const double* ds
                double* s_out, double* y_out, int slot) {
     Geo g = kgeo(c);
     Red r = kred(c, slot);
-    DirArgs da = {dsrc, s_last, gg, 0.0, nullptr, nullptr, rho};
+    DirArgs da = {dsrc, s_last, gg, 0.0, nullptr, nullptr, rho,
+                  dmode == LBK_D_BUF ? ghost_ptr(c) : nullptr, c->geo.g_lo, c->geo.g_hi};
     if (dmode == LBK_D_TWOLOOP) {
         da.pa = sref(c, ref_alpha);
         da.pb = sref(c, ref_beta);
@@ -1161,7 +1259,7 @@ int lbk_checksum(lbk_ctx* c, const double* x, uint64_t* c1, uint64_t* c2) {
         hipLaunchKernelGGL(k_checksum, dim3(nb), dim3(256), 0, c->stream, x, c->geo.n_loc, c->geo.elem_lo, c->d_ck);
         HIPCHK(c, hipGetLastError());
     }
-    if (c->geo.world > 1) {
+    if (c->geo.world > 1 && !c->grp) {
         ncclResult_t r = ncclAllReduce(c->d_ck, c->d_ck, 2, ncclUint64, ncclSum, c->comm, c->stream);
         if (r != ncclSuccess) return -3;
     }
@@ -1169,6 +1267,20 @@ int lbk_checksum(lbk_ctx* c, const double* x, uint64_t* c1, uint64_t* c2) {
     HIPCHK(c, hipStreamSynchronize(c->stream));
     *c1 = c->h_ck[0];
     *c2 = c->h_ck[1];
+    if (c->grp) {  // integer sums: exact in any order
+        lbk_group* G = c->grp;
+        G->ck[c->geo.rank][0] = *c1;
+        G->ck[c->geo.rank][1] = *c2;
+        pthread_barrier_wait(&G->bar);
+        unsigned long long a = 0, b = 0;
+        for (int k = 0; k < G->world; ++k) {
+            a += G->ck[k][0];
+            b += G->ck[k][1];
+        }
+        pthread_barrier_wait(&G->bar);
+        *c1 = a;
+        *c2 = b;
+    }
     return 0;
 }
 
@@ -1221,5 +1333,25 @@ void lbk_prof_reset(lbk_ctx* c) {
 }
 
 double lbk_bytes_moved(const lbk_ctx* c) { return c->bytes_total; }
+
+void lbk_set_ghost_slot(lbk_ctx* c, int slot) { c->ghost_slot = slot; }
+
+lbk_group* lbk_group_create(int world) {
+    if (world < 1 || world > LBK_GROUPS) return nullptr;
+    lbk_group* G = new (std::nothrow) lbk_group();
+    if (!G) return nullptr;
+    G->world = world;
+    if (pthread_barrier_init(&G->bar, nullptr, (unsigned)world) != 0) {
+        delete G;
+        return nullptr;
+    }
+    return G;
+}
+
+void lbk_group_destroy(lbk_group* G) {
+    if (!G) return;
+    pthread_barrier_destroy(&G->bar);
+    delete G;
+}
 
 }  // extern "C"

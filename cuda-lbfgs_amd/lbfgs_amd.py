@@ -72,11 +72,17 @@ def lib():
     L.lbfgs_ctx_create_sharded.argtypes = [C.POINTER(vp), C.c_int64, C.c_int, C.c_int, C.c_int,
                                            C.c_int, C.c_char_p]
     L.lbfgs_unique_id.argtypes = [C.c_char_p]
+    L.lbfgs_host_group_create.argtypes = [C.POINTER(vp), C.c_int]
+    L.lbfgs_host_group_destroy.argtypes = [vp]
+    L.lbfgs_host_group_destroy.restype = None
+    L.lbfgs_ctx_create_emulated.argtypes = [C.POINTER(vp), C.c_int64, C.c_int, C.c_int, C.c_int, vp]
     L.lbfgs_ctx_destroy.argtypes = [vp]
     L.lbfgs_ctx_destroy.restype = None
     L.lbfgs_last_error.argtypes = [vp]
     L.lbfgs_last_error.restype = C.c_char_p
     L.lbfgs_local_range.argtypes = [vp, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
+    L.lbfgs_shard_range.argtypes = [C.c_int64, C.c_int, C.c_int, C.POINTER(C.c_int64),
+                                    C.POINTER(C.c_int64)]
     L.lbfgs_constants_default.argtypes = [C.POINTER(Constants)]
     L.lbfgs_constants_default.restype = None
     L.lbfgs_constants_cuda.argtypes = [C.POINTER(Constants)]
@@ -111,8 +117,9 @@ def lib():
 
 EXPORTED_SYMBOLS = [
     "lbfgs_constants_default", "lbfgs_constants_cuda", "lbfgs_ctx_create",
-    "lbfgs_ctx_create_sharded", "lbfgs_unique_id", "lbfgs_ctx_destroy", "lbfgs_last_error",
-    "lbfgs_local_range", "lbfgs_minimize", "lbfgs_solver_init", "lbfgs_solver_step",
+    "lbfgs_ctx_create_sharded", "lbfgs_unique_id", "lbfgs_host_group_create",
+    "lbfgs_host_group_destroy", "lbfgs_ctx_create_emulated", "lbfgs_ctx_destroy", "lbfgs_last_error",
+    "lbfgs_local_range", "lbfgs_shard_range", "lbfgs_minimize", "lbfgs_solver_init", "lbfgs_solver_step",
     "lbfgs_get_x", "lbfgs_sync", "lbfgs_messages", "lbfgs_trace_len", "lbfgs_trace_get",
     "lbfgs_dev_dot", "lbfgs_dev_norm", "lbfgs_dev_objective", "lbfgs_dev_trial",
     "lbfgs_dev_twoloop", "lbfgs_prof_enable", "lbfgs_prof_reset", "lbfgs_prof_get",
@@ -123,6 +130,15 @@ def constants(profile="config"):
     k = Constants()
     (lib().lbfgs_constants_cuda if profile == "cuda" else lib().lbfgs_constants_default)(C.byref(k))
     return k
+
+
+def shard_range(n, rank, world):
+    """(elem_lo, n_loc) of `rank` when n is sharded over `world` ranks (no device needed)."""
+    lo, nl = C.c_int64(), C.c_int64()
+    rc = lib().lbfgs_shard_range(int(n), int(rank), int(world), C.byref(lo), C.byref(nl))
+    if rc != 0:
+        raise LbfgsError(f"cannot shard n={n} over {world} ranks")
+    return lo.value, nl.value
 
 
 def unique_id():
@@ -148,14 +164,38 @@ def x0_uniform(n, seed=42, lo=-2.0, hi=2.0):
     return out
 
 
+class HostGroup:
+    """Exchange group for emulated ranks (threads of one process, e.g. on one GPU)."""
+
+    def __init__(self, world):
+        h = C.c_void_p()
+        rc = lib().lbfgs_host_group_create(C.byref(h), int(world))
+        if rc != 0:
+            raise LbfgsError(f"lbfgs_host_group_create failed ({rc})")
+        self.h, self.world = h, int(world)
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().lbfgs_host_group_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class Context:
     """A persistent solver context: device vectors for n (or this rank's shard of n) and the
     m-pair history ring stay resident across calls."""
 
-    def __init__(self, n, m=10, device=0, rank=0, world=1, uid=None):
+    def __init__(self, n, m=10, device=0, rank=0, world=1, uid=None, group=None):
         self.n, self.m = int(n), int(m)
         h = C.c_void_p()
-        if world == 1:
+        if group is not None:
+            rc = lib().lbfgs_ctx_create_emulated(C.byref(h), self.n, self.m, device, rank, group.h)
+        elif world == 1:
             rc = lib().lbfgs_ctx_create(C.byref(h), self.n, self.m, device)
         else:
             rc = lib().lbfgs_ctx_create_sharded(C.byref(h), self.n, self.m, device, rank, world, uid)

@@ -119,10 +119,21 @@ int lbfgs_ctx_create(lbfgs_ctx** out, int64_t n, int m, int device);
 int lbfgs_ctx_create_sharded(lbfgs_ctx** out, int64_t n, int m, int device, int rank, int world,
                              const void* unique_id);
 int lbfgs_unique_id(void* out128);
+/* Emulated ranks: 'world' contexts driven by threads of ONE process (e.g. on one GPU, one
+ * stream each) exchange their reductions through host memory instead of RCCL. Same data path
+ * and results as the RCCL shards; used to test sharding on a single GPU. */
+typedef struct lbfgs_host_group lbfgs_host_group;
+int lbfgs_host_group_create(lbfgs_host_group** out, int world);
+void lbfgs_host_group_destroy(lbfgs_host_group* grp);
+int lbfgs_ctx_create_emulated(lbfgs_ctx** out, int64_t n, int m, int device, int rank,
+                              lbfgs_host_group* grp);
 void lbfgs_ctx_destroy(lbfgs_ctx* ctx);
 const char* lbfgs_last_error(const lbfgs_ctx* ctx);
 /* this rank's slice [elem_lo, elem_lo + n_loc) of the global vector */
 int lbfgs_local_range(const lbfgs_ctx* ctx, int64_t* elem_lo, int64_t* n_loc);
+/* the shard plan without a device: rank's slice for (n, world); LBFGS_ERR_BAD_ARG when some
+ * rank would own no segment (n <= (8 - 8/world) * 1024 * L) or world does not divide 8 */
+int lbfgs_shard_range(int64_t n, int rank, int world, int64_t* elem_lo, int64_t* n_loc);
 
 /* ---- solve (drop-in for LBFGS / LBFGS_CUDA) ------------------------------------------- */
 /* x0_host / x_out_host: global vectors of n doubles (each rank passes the full vector; a

@@ -78,7 +78,7 @@ void orc_checksum(const double* x, int64_t n, uint64_t* c1, uint64_t* c2) {
  * Reductions.
  * ORC_SEQ  : vector_utils.cpp:32-41 (dotProduct), :78-86 (vectorNorm) — left to right.
  * ORC_CANON: the device order:
- *   seg_len L = roundup(ceil(n/8192), 512); segment s = [sL, min((s+1)L, n));
+ *   seg_len L = max(512, roundup(ceil(n/8192), 128)); segment s = [sL, min((s+1)L, n));
  *   thread t = 64w + lane (256 per segment); thread t visits, for u = 0.., row r = 4u + w,
  *   elements sL + 128r + 2 lane + v (v = 0,1) that are < segment end and < limit;
  *   dot: acc = fma(a, b, acc); sum: acc = acc + t.
@@ -93,7 +93,7 @@ void orc_checksum(const double* x, int64_t n, uint64_t* c1, uint64_t* c2) {
 
 void orc_canon_geometry(int64_t n, int64_t* seg_len, int64_t* nseg) {
     int64_t per = (n + CANON_SEGS - 1) / CANON_SEGS;
-    int64_t L = ((per + 511) / 512) * 512;
+    int64_t L = ((per + 127) / 128) * 128;
     if (L < 512) L = 512;
     *seg_len = L;
     *nseg = (n + L - 1) / L;
@@ -119,7 +119,7 @@ static void canon_groups(const double* a, const double* b, int64_t n, int64_t li
         for (int t = 0; t < 256; ++t) {
             int w = t >> 6, lane = t & 63;
             double v = 0.0;
-            for (int64_t u = 0; u < L / 512; ++u) {
+            for (int64_t u = 0; 128 * (4 * u + w) < L; ++u) { /* rows r = 4u + w of the segment */
                 int64_t base = sbeg + 128 * (4 * u + w) + 2 * lane;
                 for (int k = 0; k < 2; ++k) {
                     int64_t e = base + k;
