@@ -110,6 +110,33 @@ def cpu_baseline(n_sample, m, steps_for_h):
     return dict(per_iter_s=float(np.mean(steady)), iters_timed=len(steady), total_s=float(t[-1]))
 
 
+def ntag(n):
+    """100000000 -> '1e8' (file tags of profiles/)."""
+    e = len(str(n)) - 1
+    return f"1e{e}" if n == 10 ** e else str(n)
+
+
+def pmc_traffic(kernel, n, world):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of this
+    workload (profiles/*/pmc_bench_n<n>.json, produced by tools/pmc_summary.py from separate
+    FETCH_SIZE and WRITE_SIZE passes, gfx950 FETCH_SIZE x2 correction applied), or None."""
+    import glob
+
+    if world != 1:
+        return None, None
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", f"pmc_bench_n{ntag(n)}.json")))
+    for fn in reversed(files):
+        try:
+            d = json.load(open(fn))
+        except (OSError, ValueError):
+            continue
+        for k, v in d.items():
+            if k.startswith("k_" + kernel + "<") or k == "k_" + kernel:
+                if "hbm_bytes_per_launch" in v:
+                    return v["hbm_bytes_per_launch"], os.path.relpath(fn, ROOT)
+    return None, None
+
+
 def cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -134,9 +161,7 @@ def main():
     ctx.step(a.warmup)
     ctx.sync()
 
-    if not a.no_prof:
-        ctx.prof_reset()
-        ctx.prof_enable(True)
+    # timed region: exactly K steps, barrier + device sync on both sides, no instrumentation
     D.barrier()
     ctx.sync()
     t0 = time.perf_counter()
@@ -144,12 +169,19 @@ def main():
     ctx.sync()
     t_local = time.perf_counter() - t0
     D.barrier()
-    ctx.prof_enable(False)
     T = D.allreduce(t_local, "max")
     bytes_all = D.allreduce(res["bytes"], "sum")
 
+    # roofline region: the same kind of steps again with a HIP event pair around every launch
+    # on the solver stream (per-kernel durations; the events add a few us per launch, which
+    # is why they are kept out of the timed region above)
     prof = {}
-    if not a.no_prof:
+    if not a.no_prof and res["status"] == "running":
+        ctx.prof_reset()
+        ctx.prof_enable(True)
+        ctx.step(min(a.steps, 20))
+        ctx.sync()
+        ctx.prof_enable(False)
         for kname in L.KERNELS:
             p = ctx.prof_get(kname)
             if p["launches"]:
@@ -168,8 +200,10 @@ def main():
             avg_s = p["ms"] / p["launches"] / 1e3
             per_launch = p["bytes"] / p["launches"]  # this rank's algorithmic bytes per launch
             achieved = per_launch / avg_s / 1e9
+            traffic, tsrc = pmc_traffic(dom, n, world)
             roof = dict(bound="hbm", kernel=dom, achieved=round(achieved, 1), peak=HBM_PEAK_GBPS,
-                        unit="GB/s", frac=round(achieved / HBM_PEAK_GBPS, 4), traffic=None,
+                        unit="GB/s", frac=round(achieved / HBM_PEAK_GBPS, 4), traffic=traffic,
+                        traffic_unit="bytes/launch", traffic_source=tsrc,
                         bytes_per_launch=per_launch, avg_launch_us=round(avg_s * 1e6, 2),
                         launches=p["launches"],
                         kernel_share={k: round(v["ms"] / sum(q["ms"] for q in prof.values()), 4)

@@ -56,6 +56,7 @@ struct Red {
     double* partials;  // [LBK_KMAX][LBK_SEGS], local segment index
     unsigned* cnt;     // [LBK_GROUPS] tickets
     double* slot;      // this launch's result slot [LBK_GROUPS][LBK_KMAX]
+    int ticket;        // 1: in-launch last-arriver stage 2; 0: k_group_reduce after the launch
 };
 
 // Streaming loads/stores; NT = non-temporal (the vectors are touched once per pass and, at
@@ -138,7 +139,51 @@ __device__ __forceinline__ int64_t row_off(const Seg& s, int u) {
     return (int64_t)(4 * u + s.w) * 128 + 2 * s.lane;
 }
 
-// Segment partials -> tickets -> group partial by the last-arriving workgroup.
+// Stage 2 of the canonical order for group g: balanced tree over its 1024 segment partials
+// (0.0 beyond nseg) = per thread ((p0 + p1) + (p2 + p3)) over 4 consecutive segments, wave
+// butterfly, ((w0 + w1) + (w2 + w3)). ATOMIC: the partials are read with agent-scope (sc1)
+// loads inside the producing launch (ticket mode); otherwise plain loads after a kernel
+// boundary (reduce-kernel mode).
+template <int K, bool ATOMIC>
+__device__ __forceinline__ void group_tree(const double* partials, int64_t lbase, int64_t gseg0, int64_t nseg,
+                                           double* slot_g, double (&lds)[4][K > 0 ? K : 1]) {
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    double q[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        double p[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int64_t j = 4 * t + i;
+            const double* src = partials + (int64_t)k * LBK_SEGS + lbase + j;
+            if (gseg0 + j < nseg)
+                p[i] = ATOMIC ? bitsd(__hip_atomic_load(reinterpret_cast<const unsigned long long*>(src),
+                                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                              : *src;
+            else
+                p[i] = 0.0;
+        }
+        q[k] = wave_sum((p[0] + p[1]) + (p[2] + p[3]));
+    }
+    __syncthreads();  // lds reuse
+    if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) lds[w][k] = q[k];
+    }
+    __syncthreads();
+    if (t == 0) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) slot_g[k] = (lds[0][k] + lds[1][k]) + (lds[2][k] + lds[3][k]);
+    }
+}
+
+// Segment partial (wave butterflies, ((w0 + w1) + (w2 + w3))), then either
+//   red.ticket : write-through store + per-group agent-scope ticket; the last-arriving
+//                workgroup of the group runs stage 2 (one launch; used for small grids), or
+//   otherwise  : a plain store; k_group_reduce runs stage 2 after the kernel boundary. The
+//                ticket's vmcnt(0) has to wait for all the wave's outstanding row stores, which
+//                costs ~2x on short segments (n = 1e7: 3.0 vs 4.7+ TB/s, profiles/r01).
+// Both give the same bits.
 template <int K>
 __device__ __forceinline__ void reduce_publish(double (&acc)[K], const Geo& geo, const Red& red) {
     __shared__ double lds[4][K];
@@ -154,6 +199,14 @@ __device__ __forceinline__ void reduce_publish(double (&acc)[K], const Geo& geo,
     const int64_t b = blockIdx.x;
     const int64_t sg = geo.seg_lo + b;
     const int g = (int)(sg / LBK_SEG_PER_GROUP);
+    if (!red.ticket) {
+        if (t == 0) {
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+                red.partials[(int64_t)k * LBK_SEGS + b] = (lds[0][k] + lds[1][k]) + (lds[2][k] + lds[3][k]);
+        }
+        return;
+    }
     if (t == 0) {
 #pragma unroll
         for (int k = 0; k < K; ++k) {
@@ -171,36 +224,19 @@ __device__ __forceinline__ void reduce_publish(double (&acc)[K], const Geo& geo,
     __syncthreads();
     if (!last_flag) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // stage 2: balanced tree over the group's 1024 segment partials (0.0 beyond nseg)
     const int64_t gseg0 = (int64_t)g * LBK_SEG_PER_GROUP;
-    const int64_t lbase = gseg0 - geo.seg_lo;
-    double q[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-        double p[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int64_t j = 4 * t + i;
-            p[i] = (gseg0 + j < geo.nseg)
-                       ? bitsd(__hip_atomic_load(reinterpret_cast<unsigned long long*>(
-                                                     red.partials + (int64_t)k * LBK_SEGS + lbase + j),
-                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-                       : 0.0;
-        }
-        q[k] = wave_sum((p[0] + p[1]) + (p[2] + p[3]));
-    }
-    __syncthreads();  // lds reuse
-    if (lane == 0) {
-#pragma unroll
-        for (int k = 0; k < K; ++k) lds[w][k] = q[k];
-    }
-    __syncthreads();
-    if (t == 0) {
-#pragma unroll
-        for (int k = 0; k < K; ++k)
-            red.slot[g * LBK_KMAX + k] = (lds[0][k] + lds[1][k]) + (lds[2][k] + lds[3][k]);
-        __hip_atomic_store(red.cnt + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    group_tree<K, true>(red.partials, gseg0 - geo.seg_lo, gseg0, geo.nseg, red.slot + g * LBK_KMAX, lds);
+    if (t == 0) __hip_atomic_store(red.cnt + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Reduce-kernel mode: one workgroup per group of this rank (stage 2 after the boundary).
+template <int K>
+__global__ __launch_bounds__(LB_BLOCK) void k_group_reduce(const double* __restrict__ partials, Geo geo,
+                                                           double* __restrict__ slot) {
+    __shared__ double lds[4][K];
+    const int g = geo.g_lo + (int)blockIdx.x;
+    const int64_t gseg0 = (int64_t)g * LBK_SEG_PER_GROUP;
+    group_tree<K, false>(partials, gseg0 - geo.seg_lo, gseg0, geo.nseg, slot + g * LBK_KMAX, lds);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -807,6 +843,7 @@ struct lbk_ctx {
     double bytes_total;
     int nt;          // non-temporal streaming loads/stores
     int ghost_slot;  // sharded: slot holding the all-gathered edge d values (-1: none)
+    int ticket;      // reduction mode (see reduce_publish)
     lbk_group* grp;  // emulated ranks: host exchange group (tests; NULL with RCCL)
 };
 
@@ -841,6 +878,7 @@ Red kred(const lbk_ctx* c, int slot) {
     r.partials = c->partials;
     r.cnt = c->cnt;
     r.slot = c->slots + (int64_t)slot * LBK_SLOT;
+    r.ticket = c->ticket;
     return r;
 }
 
@@ -907,7 +945,7 @@ int exchange_slot(lbk_ctx* c, int slot) {
 
 // launch wrapper: byte accounting, optional event timing, all-gather of group partials
 template <class F>
-int launch(lbk_ctx* c, int kind, double vec_passes, int slot, F&& fn) {
+int launch(lbk_ctx* c, int kind, double vec_passes, int slot, F&& fn, int K = 1) {
     const double bytes = vec_passes * 8.0 * (double)c->geo.n_loc;
     c->bytes_total += bytes;
     hipEvent_t a = nullptr, b = nullptr;
@@ -919,6 +957,17 @@ int launch(lbk_ctx* c, int kind, double vec_passes, int slot, F&& fn) {
     }
     if (nblocks(c) > 0) {
         fn();
+        HIPCHK(c, hipGetLastError());
+    }
+    if (slot >= 0 && !c->ticket) {
+        const Geo g = kgeo(c);
+        double* sl = c->slots + (int64_t)slot * LBK_SLOT;
+        const dim3 grid(c->geo.g_hi - c->geo.g_lo), blk(LB_BLOCK);
+        switch (K) {
+            case 1: hipLaunchKernelGGL(k_group_reduce<1>, grid, blk, 0, c->stream, c->partials, g, sl); break;
+            case 2: hipLaunchKernelGGL(k_group_reduce<2>, grid, blk, 0, c->stream, c->partials, g, sl); break;
+            default: hipLaunchKernelGGL(k_group_reduce<7>, grid, blk, 0, c->stream, c->partials, g, sl); break;
+        }
         HIPCHK(c, hipGetLastError());
     }
     if (c->prof_on && a && b) {
@@ -984,6 +1033,10 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
     // Cache: +4 % at n=1e8, -1 % at n=1e7 (profiles/r01); override: LBFGS_NT=0/1
     c->nt = (G.n_loc * 8 > (128ll << 20)) ? 1 : 0;
     if (const char* e = getenv("LBFGS_NT")) c->nt = atoi(e) != 0;
+    // stage-2 reduction: separate 8-workgroup kernel by default; in-launch tickets only for
+    // tiny grids where the extra launch dominates (override: LBFGS_TICKET=0/1)
+    c->ticket = (G.seg_hi - G.seg_lo) <= 64 ? 1 : 0;
+    if (const char* e = getenv("LBFGS_TICKET")) c->ticket = atoi(e) != 0;
     c->vec_doubles = LBK_FRONT + ((G.n_loc + 511) / 512) * 512 + 512;
     *out = c;
 #define CK(expr)                                                                             \
@@ -1187,7 +1240,7 @@ int lbk_eval(lbk_ctx* c, int obj, const double* x, double* gout, int slot) {
         OBJ_DISPATCH(obj, hipLaunchKernelGGL((k_objective<O_, true, true, NT_>), dim3(nblocks(c)), dim3(LB_BLOCK), 0,
                                              c->stream, x, da, 0.0, gout, g, r));
         return 0;
-    });
+    }, 2);
 }
 
 int lbk_trial(lbk_ctx* c, int obj, const double* x, const double* d, double alpha, double* gout, int slot) {
@@ -1204,7 +1257,7 @@ int lbk_trial(lbk_ctx* c, int obj, const double* x, const double* d, double alph
                                                  0, c->stream, x, da, alpha, gout, g, r));
         }
         return 0;
-    });
+    }, 2);
 }
 
 int lbk_commit(lbk_ctx* c, int obj, int dmode, const double* x, const double* dsrc, const double* s_last,
@@ -1240,7 +1293,7 @@ int lbk_commit(lbk_ctx* c, int obj, int dmode, const double* x, const double* ds
                 break;
         }
         return 0;
-    });
+    }, 7);
 }
 
 int lbk_point(lbk_ctx* c, double* z, const double* x, const double* d, double alpha) {

@@ -141,6 +141,73 @@ __global__ __launch_bounds__(256) void k_seg_r3w1(double* q, const double* __res
     if (acc == 12345.678) out[0] = acc;
 }
 
+// the solver's pass shape with S segments of length L per workgroup, rows interleaved over 4
+// waves, NT loads/stores, optional ticket tail (wave sums -> LDS -> atomic add), to price
+// the per-workgroup reduction tail and the workgroup granularity
+template <bool TICKET>
+__global__ __launch_bounds__(256) void k_segS(double* q, const double* __restrict__ y, const double* __restrict__ s,
+                                              double c, int64_t n, int64_t L, int S, double* part, unsigned* cnt) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    __shared__ double lds[4][8];
+    __shared__ int last;
+    for (int k = 0; k < S; ++k) {
+        const int64_t base = ((int64_t)blockIdx.x * S + k) * L;
+        const int nrows_tot = (int)(L / 128);
+        double acc = 0;
+        int u0 = 0;
+        for (; 4 * (u0 + 3) + w < nrows_tot; u0 += 4) {
+            double2 qv[4], yv[4], sv[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int64_t i = base + (int64_t)(4 * (u0 + j) + w) * 128 + 2 * lane;
+                if (i < n) { qv[j] = ld<true>(q + i); yv[j] = ld<true>(y + i); sv[j] = ld<true>(s + i); }
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int64_t i = base + (int64_t)(4 * (u0 + j) + w) * 128 + 2 * lane;
+                if (i < n) {
+                    double2 r;
+                    r.x = qv[j].x - c * yv[j].x;
+                    r.y = qv[j].y - c * yv[j].y;
+                    st<true>(q + i, r);
+                    acc = fma(sv[j].x, r.x, fma(sv[j].y, r.y, acc));
+                }
+            }
+        }
+        for (; 4 * u0 + w < nrows_tot; ++u0) {
+            const int64_t i = base + (int64_t)(4 * u0 + w) * 128 + 2 * lane;
+            if (i < n) {
+                double2 qv = ld<true>(q + i), yv = ld<true>(y + i), sv = ld<true>(s + i);
+                double2 r;
+                r.x = qv.x - c * yv.x;
+                r.y = qv.y - c * yv.y;
+                st<true>(q + i, r);
+                acc = fma(sv.x, r.x, fma(sv.y, r.y, acc));
+            }
+        }
+        if (TICKET) {
+            for (int m = 1; m < 64; m <<= 1) acc += __shfl_xor(acc, m, 64);
+            if (lane == 0) lds[w][k & 7] = acc;
+        }
+    }
+    if (TICKET) {
+        __syncthreads();
+        if (threadIdx.x < S) {
+            const int k = threadIdx.x;
+            const double p = (lds[0][k] + lds[1][k]) + (lds[2][k] + lds[3][k]);
+            __hip_atomic_store(reinterpret_cast<unsigned long long*>(part + (int64_t)blockIdx.x * S + k),
+                               (unsigned long long)__double_as_longlong(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (threadIdx.x == 0) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            unsigned old = __hip_atomic_fetch_add(cnt + (blockIdx.x & 7), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            last = (old == 0xffffffffu);
+        }
+        __syncthreads();
+        if (last) part[0] = 1.0;
+    }
+}
+
 int main(int argc, char** argv) {
     const int64_t n = argc > 1 ? atoll(argv[1]) : 100000000LL;
     const int reps = argc > 2 ? atoi(argv[2]) : 10;
@@ -202,6 +269,25 @@ int main(int argc, char** argv) {
         snprintf(nm, sizeof nm, "seg_nt2 p%lld", (long long)pad);
         run(nm, 4, nb, [&](int gr) { hipLaunchKernelGGL((k_seg_r3w1<true, true, 4>), dim3(gr), dim3(256), 0, 0, q, y, sv, 0.5, n, L, out); });
         CK(hipFree(slab));
+    }
+    // workgroup granularity and ticket tail at the solver's geometry for this n
+    {
+        double* part;
+        unsigned* cnt;
+        CK(hipMalloc(&part, 8192 * 8 * sizeof(double)));
+        CK(hipMalloc(&cnt, 64));
+        CK(hipMemset(cnt, 0, 64));
+        int64_t per = (n + 8191) / 8192;
+        int64_t Lc = std::max<int64_t>(512, ((per + 127) / 128) * 128);
+        int64_t nseg = (n + Lc - 1) / Lc;
+        for (int S : {1, 2, 4, 8}) {
+            int nbS = (int)((nseg + S - 1) / S);
+            char nm[64];
+            snprintf(nm, sizeof nm, "segS%d_L%lld_nt", S, (long long)Lc);
+            run(nm, 4, nbS, [&](int gr) { hipLaunchKernelGGL((k_segS<false>), dim3(gr), dim3(256), 0, 0, v[0], v[1], v[2], 0.5, n, Lc, S, part, cnt); });
+            snprintf(nm, sizeof nm, "segS%d_L%lld_ticket", S, (long long)Lc);
+            run(nm, 4, nbS, [&](int gr) { hipLaunchKernelGGL((k_segS<true>), dim3(gr), dim3(256), 0, 0, v[0], v[1], v[2], 0.5, n, Lc, S, part, cnt); });
+        }
     }
     // larger segments (fewer, longer-lived blocks)
     for (int64_t L2 : {(int64_t)49152, (int64_t)196608}) {
