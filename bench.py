@@ -25,7 +25,11 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "cuda-lbfgs_amd"))
-import lbfgs_amd as L  # noqa: E402  (load the HIP library before anything else touches HIP)
+import lbfgs_amd as L  # noqa: E402
+
+# load liblbfgs_hip.so (and through it /opt/rocm's HIP runtime and RCCL) before torch can load its
+# bundled copies: libraries with the same soname are then shared, not duplicated
+L.lib()
 
 import numpy as np  # noqa: E402
 
@@ -37,8 +41,9 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=100)
     p.add_argument("--warmup", type=int, default=20)
-    p.add_argument("--n", type=float, default=1e8)
-    p.add_argument("--m", type=int, default=10)
+    # (not --n / --m: torch.distributed.run would take them as its own abbreviated options)
+    p.add_argument("--size", type=float, default=1e8, help="problem size n")
+    p.add_argument("--history", type=int, default=10, help="L-BFGS memory m")
     p.add_argument("--objective", default="rosenbrock")
     p.add_argument("--line-search", default="backtracking")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -149,13 +154,15 @@ def cpu_model():
 
 def main():
     a = parse()
-    n = int(a.n)
+    n = int(a.size)
     D = Dist(a.gpus)
     world, rank = a.gpus, D.rank
     uid = D.broadcast_bytes(L.unique_id() if (world > 1 and rank == 0) else None) if world > 1 else None
 
     x0 = L.x0_uniform(n, 42, -2.0, 2.0)
-    ctx = L.Context(n, a.m, device=D.local_rank, rank=rank, world=world, uid=uid)
+    # BENCH_DEVICE_MOD=k maps rank -> device local_rank % k (rehearsing several ranks on fewer GPUs)
+    dev = D.local_rank % int(os.environ["BENCH_DEVICE_MOD"]) if "BENCH_DEVICE_MOD" in os.environ else D.local_rank
+    ctx = L.Context(n, a.history, device=dev, rank=rank, world=world, uid=uid)
     ctx.init(a.objective, x0, a.line_search, tolerance=1e-5)
     del x0
     ctx.step(a.warmup)
@@ -210,13 +217,13 @@ def main():
                                       for k, v in prof.items()})
         cpu = None
         if world == 1 and not a.no_cpu_baseline:
-            cb = cpu_baseline(a.cpu_n, a.m, a.m)
+            cb = cpu_baseline(a.cpu_n, a.history, a.history)
             if cb:
                 scale = n / int(a.cpu_n)
                 cpu = dict(value=round(1.0 / (cb["per_iter_s"] * scale), 6), unit="iters/s", cores=1,
                            kind="reference",
                            sample=(f"reference sequential LBFGS (oracle/_ref, sources compiled -O2 "
-                                   f"-ffp-contract=off), Rosenbrock n={int(a.cpu_n):.0e} m={a.m} "
+                                   f"-ffp-contract=off), Rosenbrock n={int(a.cpu_n):.0e} m={a.history} "
                                    f"backtracking, mean of {cb['iters_timed']} steady iterations "
                                    f"(h=m) = {cb['per_iter_s']:.3f} s/iter, scaled x{scale:g} "
                                    f"linearly in n to n={n:.0e}; 1 of {os.cpu_count()} cores "
@@ -235,10 +242,10 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic: x0 ~ U(-2,2) from std::mt19937(42), as the reference's main.cpp",
-            "config": {"workload": (f"{a.objective} n={n:.0e} m={a.m} {a.line_search}, "
+            "config": {"workload": (f"{a.objective} n={n:.0e} m={a.history} {a.line_search}, "
                                     f"{'sharded over ' + str(world) + ' GPUs' if world > 1 else 'one GPU'}"
                                     " (BASELINE configs[2])"),
-                       "n": n, "m": a.m, "line_search": a.line_search,
+                       "n": n, "m": a.history, "line_search": a.line_search,
                        "parallelism": f"shard{world}" if world > 1 else "single"},
             "achieved_hbm_gbps": round(bytes_all / T / 1e9, 1),
             "bytes_per_step": bytes_all / max(done_steps, 1),
