@@ -13,9 +13,14 @@
 #include <string>
 #include <vector>
 
+#include <cstdio>
+#include <numeric>
+
 #include "benchmark.h"
 #include "lbfgs.h"
 #include "lbfgs_hip.h"
+#include "line_search.h"
+#include "vector_utils.h"
 
 using std::vector;
 
@@ -162,6 +167,58 @@ lbfgs_ctx* context_for(int64_t n, int m) {
     return ctx.get();
 }
 
+// contexts for the utility drop-ins (line searches, vector_utils): m = 1, cached per n
+lbfgs_ctx* util_context(int64_t n) {
+    thread_local std::unique_ptr<lbfgs_ctx, CtxDeleter> ctx;
+    thread_local int64_t cn = -1;
+    if (!ctx || cn != n) {
+        ctx.reset();
+        const char* dev = std::getenv("LBFGS_DEVICE");
+        lbfgs_ctx* c = nullptr;
+        int rc = lbfgs_ctx_create(&c, n, 1, dev ? std::atoi(dev) : 0);
+        if (rc != 0) throw std::runtime_error("lbfgs_ctx_create failed (" + std::to_string(rc) + ")");
+        ctx.reset(c);
+        cn = n;
+    }
+    return ctx.get();
+}
+
+void check(int rc, lbfgs_ctx* c, const char* what) {
+    if (rc < 0) throw std::runtime_error(std::string(what) + " failed: " + lbfgs_last_error(c));
+}
+
+double line_search(int ls, const vector<double>& x, const vector<double>& d, const FnF& f, const FnG* grad,
+                   const vector<double>& gradient) {
+    ensureSameSize(x, d);
+    ensureSameSize(x, gradient);
+    const int64_t n = (int64_t)x.size();
+    static const FnG no_grad;
+    const FnG& g = grad ? *grad : no_grad;
+    const int obj = grad ? identify(f, g, (int)n) : LBFGS_OBJ_HOST;
+    // a device objective is only certain when both f and grad are recognised; with f alone
+    // (backtracking / interpolation) recognise f by itself
+    int o = obj;
+    if (!grad) {
+        const PlainF* pf = f.target<PlainF>();
+        const FnFc* wf = f.target<FnFc>();
+        const lbfgs_amd::QuadTridiagF* qf = wf ? wf->target<lbfgs_amd::QuadTridiagF>() : f.target<lbfgs_amd::QuadTridiagF>();
+        if (pf && *pf == &rosenbrock) o = LBFGS_OBJ_ROSENBROCK;
+        else if (pf && *pf == &quadratic) o = LBFGS_OBJ_QUAD_SEPARABLE;
+        else if (qf && qf->n == (int)n) o = LBFGS_OBJ_QUAD_TRIDIAG;
+    }
+    lbfgs_ctx* c = util_context(n);
+    HostFns hf{&f, grad ? grad : &no_grad, {}};
+    lbfgs_host_fn cb{host_f, grad ? host_g : nullptr, &hf};
+    lbfgs_constants k;
+    lbfgs_constants_default(&k);
+    double alpha = 0.0;
+    int rc = lbfgs_line_search(c, o, o == LBFGS_OBJ_HOST ? &cb : nullptr, ls, &k, x.data(), d.data(),
+                               gradient.data(), &alpha);
+    if (!hf.error.empty()) throw std::runtime_error("objective callback failed: " + hf.error);
+    check(rc, c, "line search");
+    return alpha;
+}
+
 vector<double> run(const FnF& f, const FnG& grad, const vector<double>& x0, int ls, int max_iterations,
                    int m, double tolerance, bool verbose, const lbfgs_constants& k) {
     const int64_t n = (int64_t)x0.size();
@@ -200,4 +257,105 @@ vector<double> LBFGS_CUDA(const FnF f, const FnG grad, const vector<double> x0, 
 vector<double> LBFGS_CUDA(const FnF f, const FnG grad, const vector<double> x0, const int max_iterations,
                           const int m, const double tolerance) {
     return LBFGS_CUDA(f, grad, x0, std::string("backtracking"), max_iterations, m, tolerance);
+}
+
+// ---- line_search.h (line_search.cpp:8-189) --------------------------------------------------
+double cubicInterpolate(double alpha0, double alpha1, double phi0, double dphi0, double phi1, double dphi1) {
+    double d1 = dphi0 + dphi1 - 3 * (phi1 - phi0) / (alpha1 - alpha0);
+    double d2 = std::copysign(std::sqrt(d1 * d1 - dphi0 * dphi1), alpha1 - alpha0);
+    return alpha0 + (alpha1 - alpha0) * (dphi0 + d2 - d1) / (dphi0 - dphi1 + 2 * d2);
+}
+
+double quadraticInterpolate(double alpha0, double, double phi0, double dphi0, double phi1) {
+    return alpha0 - 0.5 * dphi0 * alpha0 * alpha0 / (phi1 - phi0 - dphi0 * alpha0);
+}
+
+double backtrackingLineSearch(const vector<double>& x, const vector<double>& d, const FnF& f,
+                              const vector<double>& gradient) {
+    return line_search(LBFGS_LS_BACKTRACKING, x, d, f, nullptr, gradient);
+}
+
+double backtrackingWolfeLineSearch(const vector<double>& x, const vector<double>& d, const FnF& f, const FnG& grad,
+                                   const vector<double>& gradient) {
+    return line_search(LBFGS_LS_BACKTRACKING_WOLFE, x, d, f, &grad, gradient);
+}
+
+double armijoInterpolationLineSearch(const vector<double>& x, const vector<double>& d, const FnF& f,
+                                     const vector<double>& gradient) {
+    return line_search(LBFGS_LS_INTERPOLATION, x, d, f, nullptr, gradient);
+}
+
+double wolfeInterpolationLineSearch(const vector<double>& x, const vector<double>& d, const FnF& f, const FnG& grad,
+                                    const vector<double>& gradient) {
+    return line_search(LBFGS_LS_WOLFE, x, d, f, &grad, gradient);
+}
+
+// ---- vector_utils.h (vector_utils.cpp:8-109) -----------------------------------------------
+void printMatrix(const vector<vector<double>>& matrix) {
+    for (const vector<double>& row : matrix) {
+        for (double element : row) std::cout << element << " ";
+        std::cout << std::endl;
+    }
+}
+
+void printVector(const vector<double>& v) {
+    for (const double element : v) std::cout << element << " ";
+    std::cout << std::endl;
+}
+
+void ensureSameSize(const vector<double>& v1, const vector<double>& v2) {
+    if (v1.size() != v2.size()) throw std::logic_error("Vectors must be of same size");
+}
+
+double dotProduct(const vector<double>& v1, const vector<double>& v2) {
+    ensureSameSize(v1, v2);
+    if (v1.empty()) return 0.0;
+    lbfgs_ctx* c = util_context((int64_t)v1.size());
+    double out = 0.0;
+    check(lbfgs_dev_dot(c, v1.data(), v2.data(), &out), c, "dotProduct");
+    return out;
+}
+
+vector<double> scalarProduct(const double scalar, const vector<double>& v) {
+    if (v.empty()) return {};
+    lbfgs_ctx* c = util_context((int64_t)v.size());
+    vector<double> out(v.size());
+    check(lbfgs_dev_elementwise(c, 0, v.data(), nullptr, scalar, out.data()), c, "scalarProduct");
+    return out;
+}
+
+vector<double> add(const vector<double>& v1, const vector<double>& v2) {
+    ensureSameSize(v1, v2);
+    if (v1.empty()) return {};
+    lbfgs_ctx* c = util_context((int64_t)v1.size());
+    vector<double> out(v1.size());
+    check(lbfgs_dev_elementwise(c, 1, v1.data(), v2.data(), 0.0, out.data()), c, "add");
+    return out;
+}
+
+vector<double> negative(const vector<double>& v) {
+    if (v.empty()) return {};
+    lbfgs_ctx* c = util_context((int64_t)v.size());
+    vector<double> out(v.size());
+    check(lbfgs_dev_elementwise(c, 2, v.data(), nullptr, 0.0, out.data()), c, "negative");
+    return out;
+}
+
+double vectorNorm(const vector<double>& v) {
+    if (v.empty()) return 0.0;
+    lbfgs_ctx* c = util_context((int64_t)v.size());
+    double out = 0.0;
+    check(lbfgs_dev_norm(c, v.data(), &out), c, "vectorNorm");
+    return out;
+}
+
+double getRho(const vector<double>& s, const vector<double>& y) {
+    ensureSameSize(s, y);
+    return 1. / dotProduct(s, y);
+}
+
+double calculateAverage(std::vector<double>& values) {
+    if (values.empty()) return 0.0;
+    double sum = std::accumulate(values.begin(), values.end(), 0.0);
+    return sum / values.size();
 }

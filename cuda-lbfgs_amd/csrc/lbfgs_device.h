@@ -109,6 +109,8 @@ int lbk_commit(lbk_ctx* c, int obj, int dmode, const double* x, const double* ds
                double alpha, double* xn, double* gn, double* s_out, double* y_out, int slot);
 /* z = x + alpha * d (host-callback objectives) */
 int lbk_point(lbk_ctx* c, double* z, const double* x, const double* d, double alpha);
+/* elementwise primitives (op: 0 alpha*a, 1 a+b, 2 -a, 3 a+alpha*b) over the local range */
+int lbk_elementwise(lbk_ctx* c, int op, double* out, const double* a, const double* b, double alpha);
 int lbk_checksum(lbk_ctx* c, const double* x, uint64_t* c1, uint64_t* c2); /* sync */
 
 /* results */

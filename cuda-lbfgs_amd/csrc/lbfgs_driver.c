@@ -659,7 +659,7 @@ static int iterate(lbfgs_ctx* c) {
         }
     }
 
-    double alpha;
+    double alpha = 0.0;
     switch (c->ls) {
         case LBFGS_LS_BACKTRACKING: rc = ls_backtracking(c, gd, &alpha); break;
         case LBFGS_LS_INTERPOLATION: rc = ls_interpolation(c, gd, &alpha); break;
@@ -937,6 +937,73 @@ int lbfgs_dev_twoloop(lbfgs_ctx* c, const double* g, const double* const* S, con
     DEVNC(lbk_fetch(c->dev, SLOT_LAST(m), 1, &gd));
     if (gd_out) *gd_out = gd;
     if (d_out) DEVNC(lbk_download(c->dev, d_out, c->d));
+    return 0;
+}
+
+/* Line search alone (line_search.cpp:19-189) at x along d with gradient g: the same driver code
+ * as inside lbfgs_minimize, with every trial evaluated on the device (or through the host
+ * callbacks for LBFGS_OBJ_HOST). f(x) and g.d are evaluated once (the reference re-evaluates
+ * them with identical values). Single rank. */
+int lbfgs_line_search(lbfgs_ctx* c, int objective, const lbfgs_host_fn* cb, int line_search,
+                      const lbfgs_constants* k, const double* x, const double* d, const double* g,
+                      double* alpha_out) {
+    if (!c || !x || !d || !g || !alpha_out || c->geo->world != 1) return LBFGS_ERR_BAD_ARG;
+    if (objective < 0 || objective > LBFGS_OBJ_HOST) return LBFGS_ERR_BAD_ARG;
+    if (line_search < 0 || line_search > LBFGS_LS_BACKTRACKING_WOLFE) return LBFGS_ERR_BAD_ARG;
+    if (objective == LBFGS_OBJ_HOST) {
+        if (!cb || !cb->f || (!cb->grad && (line_search == LBFGS_LS_WOLFE || line_search == LBFGS_LS_BACKTRACKING_WOLFE)))
+            return LBFGS_ERR_BAD_ARG;
+        c->cb = *cb;
+        if (host_bufs(c)) return LBFGS_ERR_NOMEM;
+    }
+    c->inited = 0;
+    c->obj = objective;
+    c->ls = line_search;
+    if (k)
+        c->K = *k;
+    else
+        lbfgs_constants_default(&c->K);
+    const int m = c->m;
+    DEVNC(lbk_upload(c->dev, c->x, x));
+    DEVNC(lbk_upload(c->dev, c->d, d));
+    DEVNC(lbk_upload(c->dev, c->g, g));
+    if (objective == LBFGS_OBJ_HOST) {
+        c->f_cur = c->cb.f(x, c->n, c->cb.user);
+    } else {
+        double t[2];
+        DEV(lbk_eval(c->dev, objective, c->x, NULL, SLOT_MISC(m)));
+        DEVNC(lbk_fetch(c->dev, SLOT_MISC(m), 1, t));
+        c->f_cur = t[0];
+    }
+    double gd;
+    DEV(lbk_dot(c->dev, c->g, c->d, SLOT_LAST(m)));
+    DEVNC(lbk_fetch(c->dev, SLOT_LAST(m), 1, &gd));
+    c->dmode = LBK_D_BUF;
+    c->d_ready = 1;
+    c->spec_valid = 0;
+    c->gt_valid = 0;
+    double alpha = 0.0;
+    int rc;
+    switch (line_search) {
+        case LBFGS_LS_BACKTRACKING: rc = ls_backtracking(c, gd, &alpha); break;
+        case LBFGS_LS_INTERPOLATION: rc = ls_interpolation(c, gd, &alpha); break;
+        case LBFGS_LS_WOLFE: rc = ls_wolfe(c, gd, &alpha); break;
+        default: rc = ls_backtracking_wolfe(c, gd, &alpha); break;
+    }
+    if (rc) return rc;
+    *alpha_out = alpha;
+    return 0;
+}
+
+/* vector_utils.cpp:43-73 on the device: op 0 out = alpha*a, 1 out = a+b, 2 out = -a */
+int lbfgs_dev_elementwise(lbfgs_ctx* c, int op, const double* a, const double* b, double alpha,
+                          double* out) {
+    if (!c || !a || !out || op < 0 || op > 2 || (op == 1 && !b)) return LBFGS_ERR_BAD_ARG;
+    c->inited = 0;
+    DEVNC(lbk_upload(c->dev, c->q, a));
+    if (op == 1) DEVNC(lbk_upload(c->dev, c->r, b));
+    DEV(lbk_elementwise(c->dev, op, c->d, c->q, c->r, alpha));
+    DEVNC(lbk_download(c->dev, out, c->d));
     return 0;
 }
 

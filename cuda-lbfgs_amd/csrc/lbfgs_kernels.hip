@@ -779,6 +779,25 @@ __global__ void k_point(double* __restrict__ z, const double* __restrict__ x, co
     if (i < hi) z[i] = x[i] + alpha * d[i];
 }
 
+// elementwise primitives of vector_utils.cpp:43-73 over the local range
+//   op 0: out = alpha * a      (scalarProduct, :43-51)
+//   op 1: out = a + b          (add, :53-63)
+//   op 2: out = -a             (negative, :65-73)
+//   op 3: out = a + alpha * b  (x + (alpha d), the trial point of every line search)
+__global__ void k_elementwise(int op, double* __restrict__ out, const double* __restrict__ a,
+                              const double* __restrict__ b, double alpha, int64_t n_loc) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_loc; i += (int64_t)gridDim.x * blockDim.x) {
+        double v;
+        switch (op) {
+            case 0: v = alpha * a[i]; break;
+            case 1: v = a[i] + b[i]; break;
+            case 2: v = -a[i]; break;
+            default: v = a[i] + alpha * b[i]; break;
+        }
+        out[i] = v;
+    }
+}
+
 // integer checksums of the bit patterns (exact in any order)
 __global__ void k_checksum(const double* __restrict__ x, int64_t n_loc, int64_t elem_lo,
                            unsigned long long* out) {
@@ -1302,6 +1321,13 @@ int lbk_point(lbk_ctx* c, double* z, const double* x, const double* d, double al
     const int nb = (int)((cnt + 255) / 256);
     return launch(c, LBK_K_POINT, 3, -1, [&] {
         hipLaunchKernelGGL(k_point, dim3(nb), dim3(256), 0, c->stream, z, x, d, alpha, lo, hi);
+    });
+}
+
+int lbk_elementwise(lbk_ctx* c, int op, double* out, const double* a, const double* b, double alpha) {
+    const int nb = (int)std::min<int64_t>((c->geo.n_loc + 255) / 256, 4096);
+    return launch(c, LBK_K_POINT, op == 1 || op == 3 ? 3 : 2, -1, [&] {
+        if (nb > 0) hipLaunchKernelGGL(k_elementwise, dim3(nb), dim3(256), 0, c->stream, op, out, a, b, alpha, c->geo.n_loc);
     });
 }
 

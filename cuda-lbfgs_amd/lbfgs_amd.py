@@ -122,7 +122,8 @@ EXPORTED_SYMBOLS = [
     "lbfgs_local_range", "lbfgs_shard_range", "lbfgs_minimize", "lbfgs_solver_init", "lbfgs_solver_step",
     "lbfgs_get_x", "lbfgs_sync", "lbfgs_messages", "lbfgs_trace_len", "lbfgs_trace_get",
     "lbfgs_dev_dot", "lbfgs_dev_norm", "lbfgs_dev_objective", "lbfgs_dev_trial",
-    "lbfgs_dev_twoloop", "lbfgs_prof_enable", "lbfgs_prof_reset", "lbfgs_prof_get",
+    "lbfgs_dev_twoloop", "lbfgs_dev_elementwise", "lbfgs_line_search", "lbfgs_prof_enable",
+    "lbfgs_prof_reset", "lbfgs_prof_get",
 ]
 
 

@@ -9,7 +9,13 @@
 #ifndef LBFGS_AMD_BENCHMARK_H
 #define LBFGS_AMD_BENCHMARK_H
 #include <functional>
+#include <string>
 #include <vector>
+
+#include "lbfgs.h"
+#include "vector_utils.h"
+
+using namespace std;  // as the reference header (benchmark.h:10); main.cpp relies on it
 
 namespace lbfgs_amd {
 /* named callables so that LBFGS() can identify generate_quadratic_*(n) through std::function */

@@ -158,7 +158,17 @@ int lbfgs_trace_len(const lbfgs_ctx* ctx);
 int lbfgs_trace_get(const lbfgs_ctx* ctx, double* f, double* gnorm, double* alpha,
                     uint64_t* c1, uint64_t* c2, int cap);
 
+/* ---- line search alone (line_search.h:10-26 on the GPU) -------------------------------- */
+/* Step size along d from x (gradient g at x) by one of the four line searches, every trial on
+ * the device (or through cb for LBFGS_OBJ_HOST). Single rank; ends any solve in progress. */
+int lbfgs_line_search(lbfgs_ctx* ctx, int objective, const lbfgs_host_fn* cb, int line_search,
+                      const lbfgs_constants* k, const double* x_host, const double* d_host,
+                      const double* g_host, double* alpha_out);
+
 /* ---- device primitives (vector_utils.cpp:32-86 on the GPU) ----------------------------- */
+/* op 0: out = alpha * a (scalarProduct), 1: out = a + b (add), 2: out = -a (negative) */
+int lbfgs_dev_elementwise(lbfgs_ctx* ctx, int op, const double* a_host, const double* b_host,
+                          double alpha, double* out_host);
 /* Host-buffer convenience forms over the context's n (global vectors). Results are the
  * canonical fixed-order device reductions. */
 int lbfgs_dev_dot(lbfgs_ctx* ctx, const double* a_host, const double* b_host, double* out);
