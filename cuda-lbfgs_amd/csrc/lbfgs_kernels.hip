@@ -321,9 +321,58 @@ __device__ __forceinline__ void rows(const Op& op, const Seg& s, int u0, double 
     }
 }
 
+// Software-pipelined full-segment walk: the loads of row group k+1 are issued before group k is
+// computed and stored. The in-place passes (q, r) carry no __restrict__ between input and output,
+// so the compiler cannot hoist the next group's loads above this group's stores by itself.
+template <int UN, int K, class Op>
+__device__ __forceinline__ void load_group(const Op& op, const Seg& s, int u0, typename Op::Row (&r)[UN]) {
+#pragma unroll
+    for (int j = 0; j < UN; ++j) op.load(r[j], s.lb + row_off(s, u0 + j));
+}
+template <int UN, int K, class Op>
+__device__ __forceinline__ void apply_group(const Op& op, const Seg& s, int u0, typename Op::Row (&r)[UN],
+                                            double (&acc)[K]) {
+#pragma unroll
+    for (int j = 0; j < UN; ++j) {
+        const int64_t o = row_off(s, u0 + j);
+        op.template apply<false>(r[j], s.lb + o, s.sbeg + o, true, true, acc);
+    }
+}
+
+template <int K, class Op>
+__device__ __forceinline__ void stream_pipelined(const Op& op, const Seg& s, double (&acc)[K]) {
+    constexpr int G = 2;  // rows per group
+    int u0 = 0;
+    if (s.nrows >= 2 * G) {
+        typename Op::Row a[G], b[G];
+        load_group<G, K>(op, s, 0, a);
+        for (;;) {
+            const bool more_b = u0 + 2 * G <= s.nrows;
+            if (more_b) load_group<G, K>(op, s, u0 + G, b);
+            apply_group<G, K>(op, s, u0, a, acc);
+            u0 += G;
+            if (!more_b) break;
+            const bool more_a = u0 + 2 * G <= s.nrows;
+            if (more_a) load_group<G, K>(op, s, u0 + G, a);
+            apply_group<G, K>(op, s, u0, b, acc);
+            u0 += G;
+            if (!more_a) break;
+        }
+    }
+    for (; u0 < s.nrows; ++u0) rows<false, 1>(op, s, u0, acc);
+}
+
+#ifndef LBK_PIPELINE
+#define LBK_PIPELINE 0
+#endif
+
 template <int K, class Op>
 __device__ __forceinline__ void stream(const Op& op, const Seg& s, const Geo& geo, double (&acc)[K]) {
     int u0 = 0;
+    if (LBK_PIPELINE && s.len == geo.L) {
+        stream_pipelined(op, s, acc);
+        return;
+    }
     if (s.len == geo.L) {
         for (; u0 + 4 <= s.nrows; u0 += 4) rows<false, 4>(op, s, u0, acc);
         if (u0 + 2 <= s.nrows) {

@@ -14,7 +14,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "liblbfgs_hip.so")
+LIB_PATH = os.environ.get("LBFGS_LIB") or os.path.join(HERE, "liblbfgs_hip.so")  # LBFGS_LIB: A/B builds
 
 OBJECTIVES = {"rosenbrock": 0, "quad_tridiag": 1, "quad_sep": 2, "host": 3}
 LINE_SEARCHES = {"backtracking": 0, "interpolation": 1, "wolfe": 2, "backtracking_wolfe": 3}

@@ -1,0 +1,93 @@
+#!/usr/bin/env python3
+"""Run BASELINE.json's configs on one GPU and write one JSON summary (profiles/<round>/configs.json).
+
+  configs[0]  Rosenbrock n=1e4, m=5, backtracking (the reference's CPU case): GPU it/s, and the
+              reference itself (oracle/_ref) on this host's core for the same 1000 iterations
+  configs[1]  Rosenbrock n=1e7, m=10: it/s (20 warm-up + 200 timed)
+  configs[2]  Rosenbrock n=1e8, m=10: it/s (20 warm-up + 100 timed) — bench.py's headline
+  configs[3]  tridiagonal quadratic (generate_quadratic_*) n=1e8, m=20, Wolfe: time to solution
+  configs[4]  Rosenbrock n=1e9, m=10: the 8-GPU problem size, here on ONE GPU (240 GB resident;
+              the sharded 8-GPU run is the driver's), 5 warm-up + 10 timed
+
+usage: python tools/bench_configs.py [out.json] [--skip-1e9]
+"""
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "cuda-lbfgs_amd"))
+import lbfgs_amd as L  # noqa: E402
+
+L.lib()
+import numpy as np  # noqa: E402
+
+
+def timed_steps(n, m, obj, ls, warm, steps, tol=1e-5):
+    x0 = L.x0_uniform(n, 42, -2.0, 2.0)
+    with L.Context(n, m) as c:
+        c.init(obj, x0, ls, tolerance=tol)
+        del x0
+        c.step(warm)
+        c.sync()
+        t0 = time.perf_counter()
+        r = c.step(steps)
+        c.sync()
+        dt = time.perf_counter() - t0
+    done = steps if r["status"] == "running" else max(r["iterations"] - warm, 1)
+    return dict(n=n, m=m, objective=obj, line_search=ls, warmup=warm, steps=done, seconds=dt,
+                iters_per_s=done / dt, ms_per_iter=1e3 * dt / done, gbps=r["bytes"] / dt / 1e9,
+                status=r["status"], f=r["f"], gnorm=r["gnorm"])
+
+
+def to_solution(n, m, obj, ls, maxit, tol=1e-5):
+    x0 = L.x0_uniform(n, 42, -2.0, 2.0)
+    with L.Context(n, m) as c:
+        t0 = time.perf_counter()
+        r = c.minimize(obj, x0, ls, maxit, tolerance=tol)
+        dt = time.perf_counter() - t0
+    return dict(n=n, m=m, objective=obj, line_search=ls, seconds=dt, iterations=r["iterations"],
+                status=r["status"], f=r["f"], gnorm=r["gnorm"], trials_f=r["trials_f"],
+                trials_fg=r["trials_fg"], gbps=r["bytes"] / dt / 1e9,
+                note="includes x0 upload and result download")
+
+
+def cpu_reference(n, m, iters):
+    ref = os.path.join(ROOT, "oracle", "_ref", "ref_lbfgs")
+    if not os.path.exists(ref):
+        return None
+    with tempfile.TemporaryDirectory() as tmp:
+        pre = os.path.join(tmp, "c")
+        subprocess.run([ref, "rosenbrock", str(n), str(m), "backtracking", str(iters), "1e-5", "42", "-2",
+                        "2", pre, "0"], check=True, capture_output=True, timeout=900)
+        g = np.fromfile(pre + ".g.bin", dtype=np.uint64).reshape(-1, 5)
+        t = g[:, 3].copy().view(np.float64)
+    return dict(iters_per_s=(len(t) - 1) / (t[-1] - t[0]), seconds=float(t[-1] - t[0]), iterations=len(t) - 1,
+                kind="reference (oracle/_ref, 1 core)")
+
+
+def main():
+    out = sys.argv[1] if len(sys.argv) > 1 and not sys.argv[1].startswith("--") else None
+    res = {}
+    res["config0_rosen_1e4_m5_bt"] = dict(gpu=timed_steps(10**4, 5, "rosenbrock", "backtracking", 0, 1000),
+                                          cpu=cpu_reference(10**4, 5, 1000))
+    print(json.dumps(res["config0_rosen_1e4_m5_bt"]), flush=True)
+    res["config1_rosen_1e7_m10"] = timed_steps(10**7, 10, "rosenbrock", "backtracking", 20, 200)
+    print(json.dumps(res["config1_rosen_1e7_m10"]), flush=True)
+    res["config2_rosen_1e8_m10"] = timed_steps(10**8, 10, "rosenbrock", "backtracking", 20, 100)
+    print(json.dumps(res["config2_rosen_1e8_m10"]), flush=True)
+    res["config3_qtri_1e8_m20_wolfe"] = to_solution(10**8, 20, "quad_tridiag", "wolfe", 1000)
+    print(json.dumps(res["config3_qtri_1e8_m20_wolfe"]), flush=True)
+    if "--skip-1e9" not in sys.argv:
+        res["config4_rosen_1e9_m10_single_gpu"] = timed_steps(10**9, 10, "rosenbrock", "backtracking", 5, 10)
+        print(json.dumps(res["config4_rosen_1e9_m10_single_gpu"]), flush=True)
+    if out:
+        with open(out, "w") as fp:
+            json.dump(res, fp, indent=1)
+
+
+if __name__ == "__main__":
+    main()
