@@ -277,14 +277,18 @@ static void say(ctx_t* c, const char* fmt, ...) {
 }
 
 static double F(ctx_t* c, const double* x) {
-    double v = orc_f(c->o->obj, x, c->n, c->o->mode);
+    double v = c->o->obj == ORC_OBJ_HOST ? c->o->host_f(x, c->n, c->o->host_user)
+                                          : orc_f(c->o->obj, x, c->n, c->o->mode);
     if (c->flog && c->flog_n < c->flog_cap) c->flog[c->flog_n++] = v;
     c->nf++;
     return v;
 }
 
 static void G(ctx_t* c, const double* x, double* g) {
-    orc_grad(c->o->obj, x, c->n, g);
+    if (c->o->obj == ORC_OBJ_HOST)
+        c->o->host_g(x, c->n, g, c->o->host_user);
+    else
+        orc_grad(c->o->obj, x, c->n, g);
     if (c->glog && c->glog_n + 3 <= c->glog_cap) {
         uint64_t c1, c2, gb;
         double gn = orc_norm(g, c->n, ORC_SEQ); /* the trace driver logs the sequential norm */

@@ -20,7 +20,9 @@
 extern "C" {
 #endif
 
-enum { ORC_OBJ_ROSENBROCK = 0, ORC_OBJ_QUAD_TRIDIAG = 1, ORC_OBJ_QUAD_SEPARABLE = 2 };
+/* ORC_OBJ_HOST: the caller's f/grad callbacks (the reference's LBFGS takes any
+ * std::function objective, lbfgs.h:9-10); used with the dense quadratics of matrices.h */
+enum { ORC_OBJ_ROSENBROCK = 0, ORC_OBJ_QUAD_TRIDIAG = 1, ORC_OBJ_QUAD_SEPARABLE = 2, ORC_OBJ_HOST = 3 };
 enum { ORC_LS_BACKTRACKING = 0, ORC_LS_INTERPOLATION = 1, ORC_LS_WOLFE = 2, ORC_LS_BACKTRACKING_WOLFE = 3 };
 enum { ORC_SEQ = 0, ORC_CANON = 1 };
 enum { ORC_CONVERGED = 0, ORC_MAX_ITER = 1, ORC_LS_FAILED = 2 };
@@ -32,6 +34,10 @@ typedef struct {
     double tol;
     /* config.h:5-17 */
     double c1, c2, initial_step, backtracking_alpha, backtracking_tol, wolfe_interp_min;
+    /* ORC_OBJ_HOST only */
+    double (*host_f)(const double* x, int64_t n, void* user);
+    void (*host_g)(const double* x, int64_t n, double* g, void* user);
+    void* host_user;
 } orc_opts;
 
 typedef struct {

@@ -15,7 +15,7 @@ ORACLE_DIR = os.path.join(ROOT, "oracle")
 ORACLE_SO = os.path.join(ORACLE_DIR, "_build", "liboracle.so")
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 
-OBJ = {"rosenbrock": 0, "quad_tridiag": 1, "quad_sep": 2}
+OBJ = {"rosenbrock": 0, "quad_tridiag": 1, "quad_sep": 2, "host": 3}
 LS = {"backtracking": 0, "interpolation": 1, "wolfe": 2, "backtracking_wolfe": 3}
 SEQ, CANON = 0, 1
 STATUS = {0: "converged", 1: "max_iter", 2: "ls_failed"}
@@ -30,7 +30,24 @@ class Opts(C.Structure):
                 ("n", C.c_int64), ("m", C.c_int), ("maxit", C.c_int), ("tol", C.c_double),
                 ("c1", C.c_double), ("c2", C.c_double), ("initial_step", C.c_double),
                 ("backtracking_alpha", C.c_double), ("backtracking_tol", C.c_double),
-                ("wolfe_interp_min", C.c_double)]
+                ("wolfe_interp_min", C.c_double),
+                ("host_f", C.c_void_p), ("host_g", C.c_void_p), ("host_user", C.c_void_p)]
+
+
+HOST_F = C.CFUNCTYPE(C.c_double, C.POINTER(C.c_double), C.c_int64, C.c_void_p)
+HOST_G = C.CFUNCTYPE(None, C.POINTER(C.c_double), C.c_int64, C.POINTER(C.c_double), C.c_void_p)
+
+
+def host_callbacks(f, grad):
+    """ctypes callbacks for ORC_OBJ_HOST (keep the returned tuple alive during the run)."""
+    def cf(xp, n, user):
+        return float(f(np.ctypeslib.as_array(xp, shape=(n,)).copy()))
+
+    def cg(xp, n, gp, user):
+        np.ctypeslib.as_array(gp, shape=(n,))[:] = np.asarray(
+            grad(np.ctypeslib.as_array(xp, shape=(n,)).copy()), dtype=np.float64)
+
+    return HOST_F(cf), HOST_G(cg)
 
 
 class Result(C.Structure):
@@ -118,8 +135,10 @@ def np_checksum(x):
         return int(u.sum(dtype=np.uint64)), int((u * idx).sum(dtype=np.uint64))
 
 
-def lbfgs(obj, x0, ls, m, maxit, tol, mode=CANON, consts=None, log_calls=False, verbose=False):
-    """Run the oracle; returns a dict with x, trace arrays, call logs and messages."""
+def lbfgs(obj, x0, ls, m, maxit, tol, mode=CANON, consts=None, log_calls=False, verbose=False,
+          f=None, grad=None):
+    """Run the oracle; returns a dict with x, trace arrays, call logs and messages.
+    obj="host" takes the objective from the Python callables f(x) and grad(x)."""
     x0 = np.ascontiguousarray(x0, np.float64)
     n = len(x0)
     k = dict(CONFIG_H)
@@ -127,6 +146,11 @@ def lbfgs(obj, x0, ls, m, maxit, tol, mode=CANON, consts=None, log_calls=False, 
         k.update(consts)
     o = Opts(obj=OBJ[obj], ls=LS[ls], mode=mode, verbose=int(verbose), n=n, m=m, maxit=maxit,
              tol=tol, **k)
+    cbs = None
+    if obj == "host":
+        cbs = host_callbacks(f, grad)
+        o.host_f = C.cast(cbs[0], C.c_void_p)
+        o.host_g = C.cast(cbs[1], C.c_void_p)
     cap = maxit + 2
     x = np.empty(n)
     trf, trg, tra = np.empty(cap), np.empty(cap), np.empty(cap)
