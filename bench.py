@@ -49,6 +49,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-n", type=float, default=1e7, help="CPU baseline sample size")
     p.add_argument("--no-prof", action="store_true", help="no per-kernel HIP events")
+    p.add_argument("--unfused", action="store_true",
+                   help="one launch per BLAS-1 op (BASELINE configs[1] shape), same iterates")
     return p.parse_args()
 
 
@@ -163,7 +165,7 @@ def main():
     # BENCH_DEVICE_MOD=k maps rank -> device local_rank % k (rehearsing several ranks on fewer GPUs)
     dev = D.local_rank % int(os.environ["BENCH_DEVICE_MOD"]) if "BENCH_DEVICE_MOD" in os.environ else D.local_rank
     ctx = L.Context(n, a.history, device=dev, rank=rank, world=world, uid=uid)
-    ctx.init(a.objective, x0, a.line_search, tolerance=1e-5)
+    ctx.init(a.objective, x0, a.line_search, tolerance=1e-5, unfused=a.unfused)
     del x0
     ctx.step(a.warmup)
     ctx.sync()
@@ -244,7 +246,9 @@ def main():
             "data": "synthetic: x0 ~ U(-2,2) from std::mt19937(42), as the reference's main.cpp",
             "config": {"workload": (f"{a.objective} n={n:.0e} m={a.history} {a.line_search}, "
                                     f"{'sharded over ' + str(world) + ' GPUs' if world > 1 else 'one GPU'}"
-                                    " (BASELINE configs[2])"),
+                                    + (", unfused per-vector kernels" if a.unfused else ", fused passes")
+                                    + (" (BASELINE configs[2])" if n == 10 ** 8 else "")),
+                       "kernels": "unfused" if a.unfused else "fused",
                        "n": n, "m": a.history, "line_search": a.line_search,
                        "parallelism": f"shard{world}" if world > 1 else "single"},
             "achieved_hbm_gbps": round(bytes_all / T / 1e9, 1),

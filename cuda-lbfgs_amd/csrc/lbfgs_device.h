@@ -46,7 +46,7 @@ extern "C" {
 enum {
     LBK_K_DOT = 0, LBK_K_AXPY_DOT, LBK_K_MID, LBK_K_AXPY2_DOT, LBK_K_LAST, LBK_K_NEGDOT,
     LBK_K_EVAL, LBK_K_TRIAL_F, LBK_K_TRIAL_FG, LBK_K_COMMIT, LBK_K_POINT, LBK_K_CHECKSUM,
-    LBK_K_COUNT
+    LBK_K_UPDATE, LBK_K_COUNT
 };
 
 typedef struct {
@@ -110,6 +110,10 @@ int lbk_commit(lbk_ctx* c, int obj, int dmode, const double* x, const double* ds
 /* z = x + alpha * d (host-callback objectives) */
 int lbk_point(lbk_ctx* c, double* z, const double* x, const double* d, double alpha);
 /* elementwise primitives (op: 0 alpha*a, 1 a+b, 2 -a, 3 a+alpha*b) over the local range */
+/* unfused mode: out = op(a, b) with device-side coefficients (see k_update) */
+enum { LBK_U_AXPY_Q = 0, LBK_U_AXPY_R, LBK_U_SCALE, LBK_U_NEG, LBK_U_SUB, LBK_U_POINT };
+int lbk_update(lbk_ctx* c, int op, double* out, const double* a, const double* b, double rho, int slot_a,
+               int slot_b, double scal);
 int lbk_elementwise(lbk_ctx* c, int op, double* out, const double* a, const double* b, double alpha);
 int lbk_checksum(lbk_ctx* c, const double* x, uint64_t* c1, uint64_t* c2); /* sync */
 

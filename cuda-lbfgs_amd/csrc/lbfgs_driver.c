@@ -73,6 +73,7 @@ struct lbfgs_ctx {
     double spec_f, spec_dphi, spec_tot[LBK_KMAX];
     int gt_valid;
     double gt_alpha;
+    int unfused; /* LBFGS_FLAG_UNFUSED */
     /* counters */
     int64_t trials_f, trials_fg, commits, passes;
     /* messages / trace */
@@ -334,6 +335,9 @@ static int materialize_d(lbfgs_ctx* c) {
     if (c->dmode == LBK_D_TWOLOOP) {
         DEV(lbk_last(c->dev, c->d, c->r, c->S[c->s_last_pair], c->g, c->rho_last, c->ref_b_last,
                      c->ref_a_last, SLOT_LAST(m)));
+    } else if (c->dmode == LBK_D_NEG_G && c->unfused) {
+        DEV(lbk_update(c->dev, LBK_U_NEG, c->d, c->g, NULL, 0.0, -1, -1, 0.0));
+        DEV(lbk_dot(c->dev, c->g, c->d, SLOT_LAST(m)));
     } else if (c->dmode == LBK_D_NEG_G) {
         DEV(lbk_negdot(c->dev, c->d, c->g, SLOT_LAST(m)));
     }
@@ -351,7 +355,19 @@ static int trial(lbfgs_ctx* c, double alpha, int need_g, double* f, double* dphi
     }
     int rc = materialize_d(c);
     if (rc) return rc;
-    if (c->obj == LBFGS_OBJ_HOST) {
+    if (c->unfused) {
+        /* x_new = x + alpha d materialised, then f (and grad, g_new . d) on it */
+        double t[2];
+        DEV(lbk_update(c->dev, LBK_U_POINT, c->xn, c->x, c->d, 0.0, -1, -1, alpha));
+        DEV(lbk_eval(c->dev, c->obj, c->xn, need_g ? c->gt : NULL, SLOT_TRIAL(c->m)));
+        DEVNC(lbk_fetch(c->dev, SLOT_TRIAL(c->m), 1, t));
+        *f = t[0];
+        if (need_g) {
+            DEV(lbk_dot(c->dev, c->gt, c->d, SLOT_MISC(c->m) + 3));
+            DEVNC(lbk_fetch(c->dev, SLOT_MISC(c->m) + 3, 1, &t[1]));
+            if (dphi) *dphi = t[1];
+        }
+    } else if (c->obj == LBFGS_OBJ_HOST) {
         rc = host_eval_at(c, alpha, f, need_g ? c->gt : NULL);
         if (rc) return rc;
         if (need_g) {
@@ -509,7 +525,51 @@ static int ls_wolfe(lbfgs_ctx* c, double gd, double* out) {
 /* ------------------------------------------------------------------------------------------
  * Commit at step alpha: x_new, g_new, s, y and their reductions into tot[].
  * ---------------------------------------------------------------------------------------- */
+/* unfused commit (LBFGS_FLAG_UNFUSED): lbfgs.cpp:159-181 one operation per launch */
+static int commit_unfused(lbfgs_ctx* c, double alpha, double* tot) {
+    const int pair = c->free_pair, sm = SLOT_MISC(c->m);
+    double t[2];
+    DEV(lbk_update(c->dev, LBK_U_POINT, c->xn, c->x, c->d, 0.0, -1, -1, alpha));
+    DEV(lbk_eval(c->dev, c->obj, c->xn, c->gn, sm)); /* f(x_new), g_new, g_new . g_new */
+    DEV(lbk_update(c->dev, LBK_U_SUB, c->S[pair], c->xn, c->x, 0.0, -1, -1, 0.0));
+    DEV(lbk_update(c->dev, LBK_U_SUB, c->Y[pair], c->gn, c->g, 0.0, -1, -1, 0.0));
+    DEV(lbk_dot(c->dev, c->S[pair], c->Y[pair], sm + 1));
+    DEV(lbk_dot(c->dev, c->Y[pair], c->Y[pair], sm + 2));
+    DEVNC(lbk_fetch(c->dev, sm, 2, t));
+    tot[LBK_C_F] = t[0];
+    tot[LBK_C_GG] = t[1];
+    DEVNC(lbk_fetch(c->dev, sm + 1, 1, &tot[LBK_C_SY]));
+    DEVNC(lbk_fetch(c->dev, sm + 2, 1, &tot[LBK_C_YY]));
+    c->commits++;
+    return 0;
+}
+
+/* unfused two-loop (lbfgs.cpp:127-171): a dot launch and an update launch per pair and
+ * loop, gamma scaling and d = -r as launches of their own; leaves d and g.d (SLOT_LAST) */
+static int twoloop_unfused(lbfgs_ctx* c, const double* rho, double gamma) {
+    const int h = c->h, m = c->m;
+    const double* qsrc = c->g;
+    for (int i = h - 1; i >= 0; --i) {
+        const int sa = i == h - 1 ? SLOT_P0 : SLOT_A0 + i;
+        DEV(lbk_dot(c->dev, c->S[c->ring[i]], qsrc, sa));
+        DEV(lbk_update(c->dev, LBK_U_AXPY_Q, c->q, qsrc, c->Y[c->ring[i]], rho[i], sa, -1, 0.0));
+        qsrc = c->q;
+    }
+    DEV(lbk_update(c->dev, LBK_U_SCALE, c->r, c->q, NULL, 0.0, -1, -1, gamma));
+    for (int i = 0; i < h; ++i) {
+        const int sa = i == h - 1 ? SLOT_P0 : SLOT_A0 + i, sb = SLOT_B0(m) + i;
+        DEV(lbk_dot(c->dev, c->Y[c->ring[i]], c->r, sb));
+        DEV(lbk_update(c->dev, LBK_U_AXPY_R, c->r, c->r, c->S[c->ring[i]], rho[i], sa, sb, 0.0));
+    }
+    DEV(lbk_update(c->dev, LBK_U_NEG, c->d, c->r, NULL, 0.0, -1, -1, 0.0));
+    DEV(lbk_dot(c->dev, c->g, c->d, SLOT_LAST(m)));
+    c->dmode = LBK_D_BUF;
+    c->d_ready = 1;
+    return 0;
+}
+
 static int commit(lbfgs_ctx* c, int dmode, double alpha, int cslot, double* tot) {
+    if (c->unfused) return commit_unfused(c, alpha, tot);
     const int pair = c->free_pair;
     const double* dsrc = dmode == LBK_D_BUF ? c->d : c->r;
     const double* s_last = dmode == LBK_D_TWOLOOP ? c->S[c->s_last_pair] : NULL;
@@ -579,7 +639,13 @@ static int iterate(lbfgs_ctx* c) {
                 dmode = LBK_D_TWOLOOP;
             }
         }
-        if (dmode == LBK_D_TWOLOOP) {
+        if (dmode == LBK_D_TWOLOOP && c->unfused) {
+            double rho[MMAX];
+            for (int i = 0; i < h; ++i) rho[i] = 1.0 / c->sy[c->ring[i]];
+            rc = twoloop_unfused(c, rho, gamma);
+            if (rc) return rc;
+            dmode = LBK_D_BUF;
+        } else if (dmode == LBK_D_TWOLOOP) {
             int refA[MMAX], refB[MMAX];
             double rho[MMAX];
             for (int i = 0; i < h; ++i) rho[i] = 1.0 / c->sy[c->ring[i]];
@@ -611,6 +677,7 @@ static int iterate(lbfgs_ctx* c) {
         }
     }
     c->dmode = dmode;
+    if (c->unfused && dmode == LBK_D_BUF) c->d_ready = 1;
 
     /* ---- descent check (:146-153) and the line search (:156) ---- */
     const int cslot = SLOT_COMMIT0 + (k & 1);
@@ -618,7 +685,7 @@ static int iterate(lbfgs_ctx* c) {
     double gd;
     c->a0 = c->K.initial_step;
     const int sharded = c->geo->world > 1;
-    if (c->obj != LBFGS_OBJ_HOST) {
+    if (c->obj != LBFGS_OBJ_HOST && !c->unfused) {
         /* single GPU: last two-loop pass + first trial at a0 + commit fused in one pass.
          * Sharded: d is materialised first so that its edge values reach the neighbouring
          * ranks (halo of the stencil) through the all-gather of its reduction slot. */
@@ -696,7 +763,7 @@ static int iterate(lbfgs_ctx* c) {
         }
         c->sy[pair] = sy;
         c->yy[pair] = tot[LBK_C_YY];
-        c->sg_valid = 1;
+        c->sg_valid = !c->unfused;
         c->sg_ref = REF(cslot, LBK_C_SG);
     } else {
         say(c, "Warning: Skipping update, sy = %g\n", sy); /* :192-195 */
@@ -726,6 +793,8 @@ int lbfgs_solver_init(lbfgs_ctx* c, int objective, const lbfgs_host_fn* cb, int 
         c->cb = *cb;
         if (host_bufs(c)) return LBFGS_ERR_NOMEM;
     }
+    c->unfused = (flags & LBFGS_FLAG_UNFUSED) != 0;
+    if (c->unfused && (objective == LBFGS_OBJ_HOST || c->geo->world != 1)) return LBFGS_ERR_BAD_ARG;
     c->obj = objective;
     c->ls = line_search;
     if (k)
@@ -957,6 +1026,7 @@ int lbfgs_line_search(lbfgs_ctx* c, int objective, const lbfgs_host_fn* cb, int 
         if (host_bufs(c)) return LBFGS_ERR_NOMEM;
     }
     c->inited = 0;
+    c->unfused = 0;
     c->obj = objective;
     c->ls = line_search;
     if (k)

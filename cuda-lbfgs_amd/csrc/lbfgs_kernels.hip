@@ -847,6 +847,57 @@ __global__ void k_elementwise(int op, double* __restrict__ out, const double* __
     }
 }
 
+// Unfused mode (LBFGS_FLAG_UNFUSED): one elementwise kernel per BLAS-1 update, the shape of
+// the reference's parallel-implementation/L-BFGS.cu:208-280 (cublasDdot / cublasDaxpy /
+// cublasDscal each a launch), with every dot a separate k_dot pass. Coefficients come from the
+// reduction slots on the device with the same formulas and operand order as the fused passes,
+// so both modes give bit-identical iterates.
+//   LBK_U_AXPY_Q  out = a - (rho T(pa)) b                       q -= alpha_i y_i  (lbfgs.cpp:133-137)
+//   LBK_U_AXPY_R  out = a + b ((rho T(pa)) - (rho T(pb)))       r += s_i (alpha_i - beta) (:159-164)
+//   LBK_U_SCALE   out = a * scal                                r = gamma q      (:150-154)
+//   LBK_U_NEG     out = -a                                      d = -r           (:171)
+//   LBK_U_SUB     out = a - b                                   s, y             (:177-178)
+//   LBK_U_POINT   out = a + scal * b                            x + alpha d      (:159)
+template <int OP>
+__device__ __forceinline__ double upd(double a, double b, double coef) {
+    if (OP == LBK_U_AXPY_Q) return a - coef * b;
+    if (OP == LBK_U_AXPY_R) return a + b * coef;
+    if (OP == LBK_U_SCALE) return a * coef;
+    if (OP == LBK_U_NEG) return -a;
+    if (OP == LBK_U_SUB) return a - b;
+    return a + coef * b;
+}
+
+template <int OP, bool NT>
+__global__ __launch_bounds__(256) void k_update(double* out, const double* a,  // in place: out == a
+                                                const double* __restrict__ b, double rho,
+                                                const double* __restrict__ pa, const double* __restrict__ pb,
+                                                double scal, int64_t n_loc) {
+    double coef = scal;
+    if (OP == LBK_U_AXPY_Q) coef = rho * slot_total(pa);
+    if (OP == LBK_U_AXPY_R) {
+        const double beta = rho * slot_total(pb);
+        const double alpha = rho * slot_total(pa);
+        coef = alpha - beta;
+    }
+    const bool has_b = OP == LBK_U_AXPY_Q || OP == LBK_U_AXPY_R || OP == LBK_U_SUB || OP == LBK_U_POINT;
+    const int64_t npair = n_loc >> 1;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < npair; p += stride) {
+        const double2 av = ldv<NT>(a + 2 * p);
+        double2 bv = av;
+        if (has_b) bv = ldv<NT>(b + 2 * p);
+        double2 o;
+        o.x = upd<OP>(av.x, bv.x, coef);
+        o.y = upd<OP>(av.y, bv.y, coef);
+        stv<NT>(out + 2 * p, o);
+    }
+    if ((n_loc & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+        const int64_t i = n_loc - 1;
+        out[i] = upd<OP>(a[i], has_b ? b[i] : 0.0, coef);
+    }
+}
+
 // integer checksums of the bit patterns (exact in any order)
 __global__ void k_checksum(const double* __restrict__ x, int64_t n_loc, int64_t elem_lo,
                            unsigned long long* out) {
@@ -1377,6 +1428,41 @@ int lbk_elementwise(lbk_ctx* c, int op, double* out, const double* a, const doub
     const int nb = (int)std::min<int64_t>((c->geo.n_loc + 255) / 256, 4096);
     return launch(c, LBK_K_POINT, op == 1 || op == 3 ? 3 : 2, -1, [&] {
         if (nb > 0) hipLaunchKernelGGL(k_elementwise, dim3(nb), dim3(256), 0, c->stream, op, out, a, b, alpha, c->geo.n_loc);
+    });
+}
+
+int lbk_update(lbk_ctx* c, int op, double* out, const double* a, const double* b, double rho, int slot_a,
+               int slot_b, double scal) {
+    const int64_t npair = c->geo.n_loc / 2;
+    const int nb = (int)std::max<int64_t>(1, std::min<int64_t>((npair + 255) / 256, 16384));
+    const double* pa = slot_a >= 0 ? c->slots + (int64_t)slot_a * LBK_SLOT : nullptr;
+    const double* pb = slot_b >= 0 ? c->slots + (int64_t)slot_b * LBK_SLOT : nullptr;
+    const bool has_b = op == LBK_U_AXPY_Q || op == LBK_U_AXPY_R || op == LBK_U_SUB || op == LBK_U_POINT;
+    if (op < 0 || op > LBK_U_POINT || ((op == LBK_U_AXPY_Q || op == LBK_U_AXPY_R) && !pa) ||
+        (op == LBK_U_AXPY_R && !pb)) {
+        snprintf(c->err, sizeof c->err, "lbk_update: bad op %d / slots", op);
+        return -1;
+    }
+    return launch(c, LBK_K_UPDATE, has_b ? 3 : 2, -1, [&] {
+        if (c->geo.n_loc <= 0) return;
+#define UPD_CASE(OPC)                                                                                    \
+    case OPC:                                                                                            \
+        if (c->nt)                                                                                       \
+            hipLaunchKernelGGL((k_update<OPC, true>), dim3(nb), dim3(256), 0, c->stream, out, a, b, rho, pa, pb, \
+                               scal, c->geo.n_loc);                                                      \
+        else                                                                                             \
+            hipLaunchKernelGGL((k_update<OPC, false>), dim3(nb), dim3(256), 0, c->stream, out, a, b, rho, pa,   \
+                               pb, scal, c->geo.n_loc);                                                  \
+        break;
+        switch (op) {
+            UPD_CASE(LBK_U_AXPY_Q)
+            UPD_CASE(LBK_U_AXPY_R)
+            UPD_CASE(LBK_U_SCALE)
+            UPD_CASE(LBK_U_NEG)
+            UPD_CASE(LBK_U_SUB)
+            UPD_CASE(LBK_U_POINT)
+        }
+#undef UPD_CASE
     });
 }
 

@@ -75,6 +75,11 @@ enum {
 #define LBFGS_FLAG_VERBOSE 1u /* print "Iteration k, f = .., |grad| = .." (lbfgs.cpp:76-78) */
 #define LBFGS_FLAG_QUIET 2u   /* suppress the reference's stdout messages */
 #define LBFGS_FLAG_TRACE 4u   /* record per-iteration f, |g|, alpha, x checksums (tests) */
+/* one kernel per BLAS-1 operation, as parallel-implementation/L-BFGS.cu:208-280 composes
+ * cuBLAS calls (separate dot and axpy passes, materialised trial points, f re-evaluated at
+ * the commit). Same iterates, bit for bit, as the fused default; single rank, device
+ * objectives only. BASELINE configs[1] ("unfused per-vector kernels"). */
+#define LBFGS_FLAG_UNFUSED 8u
 
 typedef struct {
     double c1;                 /* C1 = 1e-4                  config.h:5 */
@@ -188,7 +193,7 @@ enum {
     LBFGS_KERNEL_DOT = 0, LBFGS_KERNEL_AXPY_DOT, LBFGS_KERNEL_MID, LBFGS_KERNEL_AXPY2_DOT,
     LBFGS_KERNEL_LAST, LBFGS_KERNEL_NEGDOT, LBFGS_KERNEL_EVAL, LBFGS_KERNEL_TRIAL_F,
     LBFGS_KERNEL_TRIAL_FG, LBFGS_KERNEL_COMMIT, LBFGS_KERNEL_POINT, LBFGS_KERNEL_CHECKSUM,
-    LBFGS_KERNEL_COUNT
+    LBFGS_KERNEL_UPDATE, LBFGS_KERNEL_COUNT
 };
 void lbfgs_prof_enable(lbfgs_ctx* ctx, int on);
 void lbfgs_prof_reset(lbfgs_ctx* ctx);

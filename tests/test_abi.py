@@ -49,9 +49,15 @@ def test_cxx_dropin_symbols_exported():
 
 
 def test_library_has_gfx950_code_object():
+    import shutil
+    import tempfile
+
     _ensure_built()
-    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", L.LIB_PATH],
-                         capture_output=True, text=True)
+    # --offloading extracts the code objects next to its input: work on a copy in a temp dir
+    with tempfile.TemporaryDirectory() as tmp:
+        lib = shutil.copy(L.LIB_PATH, tmp)
+        out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", lib],
+                             capture_output=True, text=True, cwd=tmp)
     text = out.stdout + out.stderr
     if "gfx950" not in text:  # fall back to a raw scan of the fat binary
         assert b"gfx950" in open(L.LIB_PATH, "rb").read()

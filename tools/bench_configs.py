@@ -3,7 +3,9 @@
 
   configs[0]  Rosenbrock n=1e4, m=5, backtracking (the reference's CPU case): GPU it/s, and the
               reference itself (oracle/_ref) on this host's core for the same 1000 iterations
-  configs[1]  Rosenbrock n=1e7, m=10: it/s (20 warm-up + 200 timed)
+  configs[1]  Rosenbrock n=1e7, m=10: it/s (20 warm-up + 200 timed), unfused per-vector kernels
+              (LBFGS_FLAG_UNFUSED, as the config names) and the fused default; plus the unfused
+              mode at n=1e8 for the fused/unfused ratio at configs[2]'s size
   configs[2]  Rosenbrock n=1e8, m=10: it/s (20 warm-up + 100 timed) — bench.py's headline
   configs[3]  tridiagonal quadratic (generate_quadratic_*) n=1e8, m=20, Wolfe: time to solution
   configs[4]  Rosenbrock n=1e9, m=10: the 8-GPU problem size, here on ONE GPU (240 GB resident;
@@ -26,10 +28,10 @@ L.lib()
 import numpy as np  # noqa: E402
 
 
-def timed_steps(n, m, obj, ls, warm, steps, tol=1e-5):
+def timed_steps(n, m, obj, ls, warm, steps, tol=1e-5, unfused=False):
     x0 = L.x0_uniform(n, 42, -2.0, 2.0)
     with L.Context(n, m) as c:
-        c.init(obj, x0, ls, tolerance=tol)
+        c.init(obj, x0, ls, tolerance=tol, unfused=unfused)
         del x0
         c.step(warm)
         c.sync()
@@ -38,7 +40,8 @@ def timed_steps(n, m, obj, ls, warm, steps, tol=1e-5):
         c.sync()
         dt = time.perf_counter() - t0
     done = steps if r["status"] == "running" else max(r["iterations"] - warm, 1)
-    return dict(n=n, m=m, objective=obj, line_search=ls, warmup=warm, steps=done, seconds=dt,
+    return dict(n=n, m=m, objective=obj, line_search=ls, kernels="unfused" if unfused else "fused",
+                warmup=warm, steps=done, seconds=dt,
                 iters_per_s=done / dt, ms_per_iter=1e3 * dt / done, gbps=r["bytes"] / dt / 1e9,
                 status=r["status"], f=r["f"], gnorm=r["gnorm"])
 
@@ -75,8 +78,14 @@ def main():
     res["config0_rosen_1e4_m5_bt"] = dict(gpu=timed_steps(10**4, 5, "rosenbrock", "backtracking", 0, 1000),
                                           cpu=cpu_reference(10**4, 5, 1000))
     print(json.dumps(res["config0_rosen_1e4_m5_bt"]), flush=True)
-    res["config1_rosen_1e7_m10"] = timed_steps(10**7, 10, "rosenbrock", "backtracking", 20, 200)
-    print(json.dumps(res["config1_rosen_1e7_m10"]), flush=True)
+    res["config1_rosen_1e7_m10_unfused"] = timed_steps(10**7, 10, "rosenbrock", "backtracking", 20, 200,
+                                                       unfused=True)
+    print(json.dumps(res["config1_rosen_1e7_m10_unfused"]), flush=True)
+    res["config1_rosen_1e7_m10_fused"] = timed_steps(10**7, 10, "rosenbrock", "backtracking", 20, 200)
+    print(json.dumps(res["config1_rosen_1e7_m10_fused"]), flush=True)
+    res["config2_rosen_1e8_m10_unfused"] = timed_steps(10**8, 10, "rosenbrock", "backtracking", 20, 100,
+                                                       unfused=True)
+    print(json.dumps(res["config2_rosen_1e8_m10_unfused"]), flush=True)
     res["config2_rosen_1e8_m10"] = timed_steps(10**8, 10, "rosenbrock", "backtracking", 20, 100)
     print(json.dumps(res["config2_rosen_1e8_m10"]), flush=True)
     res["config3_qtri_1e8_m20_wolfe"] = to_solution(10**8, 20, "quad_tridiag", "wolfe", 1000)
