@@ -58,7 +58,9 @@ def test_unfused_bit_exact_vs_fused_and_oracle(name):
     assert np.array_equal(bits(ru["tr_f"]), bits(o["f"]))
     assert np.array_equal(bits(ru["x"]), bits(o["x"]))
     # more launches, more bytes: every dot and update is its own pass
-    assert ru["passes"] > rf["passes"]
+    assert ru["passes"] >= rf["passes"]
+    if ru["iterations"] > 0:
+        assert ru["passes"] > rf["passes"]
 
 
 def test_unfused_nontemporal_path_bit_exact(monkeypatch):
