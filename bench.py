@@ -51,6 +51,8 @@ def parse():
     p.add_argument("--no-prof", action="store_true", help="no per-kernel HIP events")
     p.add_argument("--unfused", action="store_true",
                    help="one launch per BLAS-1 op (BASELINE configs[1] shape), same iterates")
+    p.add_argument("--vector-free", action="store_true",
+                   help="Gram-matrix two-loop, one fused pass per iteration (opt-in mode)")
     return p.parse_args()
 
 
@@ -165,7 +167,7 @@ def main():
     # BENCH_DEVICE_MOD=k maps rank -> device local_rank % k (rehearsing several ranks on fewer GPUs)
     dev = D.local_rank % int(os.environ["BENCH_DEVICE_MOD"]) if "BENCH_DEVICE_MOD" in os.environ else D.local_rank
     ctx = L.Context(n, a.history, device=dev, rank=rank, world=world, uid=uid)
-    ctx.init(a.objective, x0, a.line_search, tolerance=1e-5, unfused=a.unfused)
+    ctx.init(a.objective, x0, a.line_search, tolerance=1e-5, unfused=a.unfused, vector_free=a.vector_free)
     del x0
     ctx.step(a.warmup)
     ctx.sync()
@@ -246,9 +248,10 @@ def main():
             "data": "synthetic: x0 ~ U(-2,2) from std::mt19937(42), as the reference's main.cpp",
             "config": {"workload": (f"{a.objective} n={n:.0e} m={a.history} {a.line_search}, "
                                     f"{'sharded over ' + str(world) + ' GPUs' if world > 1 else 'one GPU'}"
-                                    + (", unfused per-vector kernels" if a.unfused else ", fused passes")
+                                    + (", unfused per-vector kernels" if a.unfused else
+                                       ", vector-free (Gram-matrix) mode" if a.vector_free else ", fused passes")
                                     + (" (BASELINE configs[2])" if n == 10 ** 8 else "")),
-                       "kernels": "unfused" if a.unfused else "fused",
+                       "kernels": "unfused" if a.unfused else "vector_free" if a.vector_free else "fused",
                        "n": n, "m": a.history, "line_search": a.line_search,
                        "parallelism": f"shard{world}" if world > 1 else "single"},
             "achieved_hbm_gbps": round(bytes_all / T / 1e9, 1),

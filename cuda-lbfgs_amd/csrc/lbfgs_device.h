@@ -22,6 +22,22 @@ extern "C" {
 #define LBK_SEGS 8192
 #define LBK_SEG_PER_GROUP 1024
 
+/* wide result slots (vector-free mode: 4h + 6 components): ids LBK_WSLOT0 + w */
+#define LBK_VF_HMAX 20
+#define LBK_KW (4 * LBK_VF_HMAX + 8)
+#define LBK_WSLOT (LBK_GROUPS * LBK_KW)
+#define LBK_NWSLOTS 4
+#define LBK_WSLOT0 LBK_NSLOTS
+
+/* vector-free commit components (basis b_l = s_0..s_{h-1}, y_0..y_{h-1}; HB = bucket of h) */
+#define LBK_VF_F 0   /* f(x_new)             */
+#define LBK_VF_SY 1  /* s_new . y_new        */
+#define LBK_VF_YY 2  /* y_new . y_new        */
+#define LBK_VF_GG 3  /* g_new . g_new        */
+#define LBK_VF_YG 4  /* y_new . g_new        */
+#define LBK_VF_GGO 5 /* g_new . g_old        */
+#define LBK_VF_YB 6  /* + l: y_new . b_l (l < 2h); g_new . b_l at LBK_VF_YB + 2 HB + l */
+
 /* objective ids (match include/lbfgs_hip.h) */
 #define LBK_OBJ_ROSENBROCK 0
 #define LBK_OBJ_QUAD_TRIDIAG 1
@@ -46,7 +62,7 @@ extern "C" {
 enum {
     LBK_K_DOT = 0, LBK_K_AXPY_DOT, LBK_K_MID, LBK_K_AXPY2_DOT, LBK_K_LAST, LBK_K_NEGDOT,
     LBK_K_EVAL, LBK_K_TRIAL_F, LBK_K_TRIAL_FG, LBK_K_COMMIT, LBK_K_POINT, LBK_K_CHECKSUM,
-    LBK_K_UPDATE, LBK_K_COUNT
+    LBK_K_UPDATE, LBK_K_VF_COMMIT, LBK_K_VF_DIR, LBK_K_COUNT
 };
 
 typedef struct {
@@ -110,6 +126,16 @@ int lbk_commit(lbk_ctx* c, int obj, int dmode, const double* x, const double* ds
 /* z = x + alpha * d (host-callback objectives) */
 int lbk_point(lbk_ctx* c, double* z, const double* x, const double* d, double alpha);
 /* elementwise primitives (op: 0 alpha*a, 1 a+b, 2 -a, 3 a+alpha*b) over the local range */
+/* vector-free mode: d = sum_l c_l b_l + cg g (l ascending, then g) formed on the fly; commit at
+ * x + alpha d with the wide reductions above into wide slot `wslot`. *hb_out = the bucket HB
+ * that fixes the component layout. lbk_vf_dir materialises d. */
+int lbk_vf_commit(lbk_ctx* c, int obj, int h, const double* x, const double* g, const double* const* S,
+                  const double* const* Y, const double* cs, const double* cy, double cg, double alpha,
+                  double* xn, double* gn, double* so, double* yo, int wslot, int* hb_out);
+int lbk_vf_dir(lbk_ctx* c, int h, double* d, const double* g, const double* const* S, const double* const* Y,
+               const double* cs, const double* cy, double cg);
+int lbk_vf_bucket(int h);
+
 /* unfused mode: out = op(a, b) with device-side coefficients (see k_update) */
 enum { LBK_U_AXPY_Q = 0, LBK_U_AXPY_R, LBK_U_SCALE, LBK_U_NEG, LBK_U_SUB, LBK_U_POINT };
 int lbk_update(lbk_ctx* c, int op, double* out, const double* a, const double* b, double rho, int slot_a,

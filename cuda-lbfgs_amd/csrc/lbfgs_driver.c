@@ -43,6 +43,7 @@
 #define SLOT_TRIAL(m) (5 + 2 * (m))
 #define SLOT_MISC(m) (6 + 2 * (m))
 #define REF(slot, comp) ((slot) * LBK_KMAX + (comp))
+#define D_VF 3 /* direction as a combination of the basis (vector-free mode) */
 
 struct lbfgs_ctx {
     lbk_ctx* dev;
@@ -74,6 +75,17 @@ struct lbfgs_ctx {
     int gt_valid;
     double gt_alpha;
     int unfused; /* LBFGS_FLAG_UNFUSED */
+    /* vector-free mode (LBFGS_FLAG_VECTOR_FREE): Gram matrix over the pair pool, indexed by
+     * pool slot (P = m + 1): Gss[p][q] = s_p.s_q, Gsy[p][q] = s_p.y_q, Gyy[p][q] = y_p.y_q,
+     * Gsg[p] = s_p.g, Gyg[p] = y_p.g (g = current gradient; |g|^2 is gg) */
+    int vf;
+    double *Gss, *Gsy, *Gyy, *Gsg, *Gyg;
+    int vf_h;                            /* basis size of this iteration's direction */
+    const double* vf_S[MMAX];            /* basis, ring order */
+    const double* vf_Y[MMAX];
+    double vf_cs[MMAX], vf_cy[MMAX], vf_cg; /* d = sum cs s + sum cy y + cg g */
+    double vf_tot[LBK_KW], vf_spec[LBK_KW];
+    int vf_hb;
     /* counters */
     int64_t trials_f, trials_fg, commits, passes;
     /* messages / trace */
@@ -282,6 +294,11 @@ void lbfgs_ctx_destroy(lbfgs_ctx* c) {
     free(c->tr_a);
     free(c->tr_c1);
     free(c->tr_c2);
+    free(c->Gss);
+    free(c->Gsy);
+    free(c->Gyy);
+    free(c->Gsg);
+    free(c->Gyg);
     free(c);
 }
 
@@ -335,6 +352,8 @@ static int materialize_d(lbfgs_ctx* c) {
     if (c->dmode == LBK_D_TWOLOOP) {
         DEV(lbk_last(c->dev, c->d, c->r, c->S[c->s_last_pair], c->g, c->rho_last, c->ref_b_last,
                      c->ref_a_last, SLOT_LAST(m)));
+    } else if (c->dmode == D_VF) {
+        DEV(lbk_vf_dir(c->dev, c->vf_h, c->d, c->g, c->vf_S, c->vf_Y, c->vf_cs, c->vf_cy, c->vf_cg));
     } else if (c->dmode == LBK_D_NEG_G && c->unfused) {
         DEV(lbk_update(c->dev, LBK_U_NEG, c->d, c->g, NULL, 0.0, -1, -1, 0.0));
         DEV(lbk_dot(c->dev, c->g, c->d, SLOT_LAST(m)));
@@ -781,6 +800,226 @@ static int iterate(lbfgs_ctx* c) {
     return 0;
 }
 
+
+/* ------------------------------------------------------------------------------------------
+ * Vector-free mode (LBFGS_FLAG_VECTOR_FREE; outside the bit-parity contract with the
+ * reference's operation order). lbfgs.cpp:87-143's two-loop recursion runs
+ * on the host over the Gram matrix of the basis [s_0..s_{h-1}, y_0..y_{h-1}, g] (q and r are
+ * coefficient vectors); one device pass forms d from the basis, takes the first trial and the
+ * commit, and reduces g_new and y_new against the basis. The s_new row is derived,
+ * s_new . v = alpha (d . v). Every sum below runs over s terms (ring order), then y terms, then
+ * the g term, starting from 0.0 (oracle/lbfgs_oracle.c restates it in the same order).
+ * ---------------------------------------------------------------------------------------- */
+#define GI(c, p, q) ((p) * ((c)->m + 1) + (q))
+
+/* coefficient vector (ds, dy, dg) dotted with basis vector s_{ring i} or y_{ring i} */
+static double vf_dot_s(const lbfgs_ctx* c, int i, const double* ds, const double* dy, double dg) {
+    const int ri = c->ring[i];
+    double a = 0.0;
+    for (int j = 0; j < c->h; ++j) a = a + ds[j] * c->Gss[GI(c, ri, c->ring[j])];
+    for (int j = 0; j < c->h; ++j) a = a + dy[j] * c->Gsy[GI(c, ri, c->ring[j])];
+    return a + dg * c->Gsg[ri];
+}
+static double vf_dot_y(const lbfgs_ctx* c, int i, const double* ds, const double* dy, double dg) {
+    const int ri = c->ring[i];
+    double a = 0.0;
+    for (int j = 0; j < c->h; ++j) a = a + ds[j] * c->Gsy[GI(c, c->ring[j], ri)];
+    for (int j = 0; j < c->h; ++j) a = a + dy[j] * c->Gyy[GI(c, ri, c->ring[j])];
+    return a + dg * c->Gyg[ri];
+}
+
+static int vf_commit(lbfgs_ctx* c, double alpha, double* tot) {
+    int hb = 0;
+    DEV(lbk_vf_commit(c->dev, c->obj, c->vf_h, c->x, c->g, c->vf_S, c->vf_Y, c->vf_cs, c->vf_cy, c->vf_cg, alpha,
+                      c->xn, c->gn, c->S[c->free_pair], c->Y[c->free_pair], LBK_WSLOT0, &hb));
+    DEVNC(lbk_fetch(c->dev, LBK_WSLOT0, LBK_VF_YB + 4 * hb, tot));
+    c->vf_hb = hb;
+    c->commits++;
+    return 0;
+}
+
+static int iterate_vf(lbfgs_ctx* c) {
+    const int k = c->k, m = c->m, h = c->h;
+    const double gnorm = sqrt(c->gg);
+    int rc = trace_push(c, c->f_cur, gnorm, 1);
+    if (rc) return rc;
+    if (c->flags & LBFGS_FLAG_VERBOSE) {
+        printf("Iteration %d, f = %g, |grad| = %g\n", k, c->f_cur, gnorm);
+        fflush(stdout);
+    }
+    if (gnorm < c->tol) {
+        say(c, "Converged!\n");
+        c->status = LBFGS_STATUS_CONVERGED;
+        return 1;
+    }
+
+    /* ---- direction in coefficient space (:87-143): d = -(r) with r over the basis ---- */
+    c->vf_h = h;
+    for (int j = 0; j < h; ++j) {
+        c->vf_S[j] = c->S[c->ring[j]];
+        c->vf_Y[j] = c->Y[c->ring[j]];
+        c->vf_cs[j] = c->vf_cy[j] = 0.0;
+    }
+    c->vf_cg = -1.0;
+    if (!(k == 0 || h == 0)) {
+        int bad_rho = 0;
+        for (int i = h - 1; i >= 0; --i)
+            if (!isfinite(1.0 / c->Gsy[GI(c, c->ring[i], c->ring[i])])) bad_rho = 1;
+        const int top = c->ring[h - 1];
+        if (bad_rho) {
+            say(c, "Warning: Invalid rho at iteration %d\n", k);
+        } else {
+            const double gamma = c->Gsy[GI(c, top, top)] / c->Gyy[GI(c, top, top)];
+            if (gamma <= 0 || !isfinite(gamma)) {
+                say(c, "Warning: Invalid gamma at iteration %d\n", k);
+            } else {
+                double ds[MMAX], dy[MMAX], a[MMAX], dg = 1.0;
+                for (int j = 0; j < h; ++j) ds[j] = dy[j] = 0.0;
+                for (int i = h - 1; i >= 0; --i) {
+                    const double rho = 1.0 / c->Gsy[GI(c, c->ring[i], c->ring[i])];
+                    a[i] = rho * vf_dot_s(c, i, ds, dy, dg);
+                    dy[i] = dy[i] - a[i];
+                }
+                for (int j = 0; j < h; ++j) {
+                    ds[j] = ds[j] * gamma;
+                    dy[j] = dy[j] * gamma;
+                }
+                dg = dg * gamma;
+                for (int i = 0; i < h; ++i) {
+                    const double rho = 1.0 / c->Gsy[GI(c, c->ring[i], c->ring[i])];
+                    const double beta = rho * vf_dot_y(c, i, ds, dy, dg);
+                    ds[i] = ds[i] + (a[i] - beta);
+                }
+                for (int j = 0; j < h; ++j) {
+                    c->vf_cs[j] = -ds[j];
+                    c->vf_cy[j] = -dy[j];
+                }
+                c->vf_cg = -dg;
+            }
+        }
+    }
+    /* g . d from the Gram row of g */
+    double gd = 0.0;
+    for (int j = 0; j < h; ++j) gd = gd + c->vf_cs[j] * c->Gsg[c->ring[j]];
+    for (int j = 0; j < h; ++j) gd = gd + c->vf_cy[j] * c->Gyg[c->ring[j]];
+    gd = gd + c->vf_cg * c->gg;
+    if (gd >= 0) { /* :146-153 */
+        say(c, "Warning: Not a descent direction, using gradient\n");
+        for (int j = 0; j < h; ++j) c->vf_cs[j] = c->vf_cy[j] = 0.0;
+        c->vf_cg = -1.0;
+        gd = 0.0;
+        for (int j = 0; j < h; ++j) gd = gd + c->vf_cs[j] * c->Gsg[c->ring[j]];
+        for (int j = 0; j < h; ++j) gd = gd + c->vf_cy[j] * c->Gyg[c->ring[j]];
+        gd = gd + c->vf_cg * c->gg;
+    }
+    c->dmode = D_VF;
+    c->d_ready = 0;
+    c->gt_valid = 0;
+
+    /* ---- fused first trial + commit at a0, then the line search (:156) ---- */
+    c->a0 = c->K.initial_step;
+    rc = vf_commit(c, c->a0, c->vf_spec);
+    if (rc) return rc;
+    const double* T = c->vf_spec;
+    const int gb = LBK_VF_YB + 2 * c->vf_hb; /* g_new . b_l components */
+    double dgn = 0.0;                        /* g_new . d */
+    for (int j = 0; j < h; ++j) dgn = dgn + c->vf_cs[j] * T[gb + j];
+    for (int j = 0; j < h; ++j) dgn = dgn + c->vf_cy[j] * T[gb + h + j];
+    dgn = dgn + c->vf_cg * T[LBK_VF_GGO];
+    c->spec_valid = 1;
+    c->spec_f = T[LBK_VF_F];
+    c->spec_dphi = dgn;
+
+    double alpha = 0.0;
+    switch (c->ls) {
+        case LBFGS_LS_BACKTRACKING: rc = ls_backtracking(c, gd, &alpha); break;
+        case LBFGS_LS_INTERPOLATION: rc = ls_interpolation(c, gd, &alpha); break;
+        case LBFGS_LS_WOLFE: rc = ls_wolfe(c, gd, &alpha); break;
+        default: rc = ls_backtracking_wolfe(c, gd, &alpha); break;
+    }
+    if (rc) return rc;
+    if (c->flags & LBFGS_FLAG_TRACE) c->tr_a[c->tr_len - 1] = alpha;
+
+    /* ---- commit (:159-198) ---- */
+    if (alpha == c->a0) {
+        memcpy(c->vf_tot, c->vf_spec, sizeof c->vf_tot);
+    } else {
+        rc = vf_commit(c, alpha, c->vf_tot);
+        if (rc) return rc;
+        T = c->vf_tot;
+        dgn = 0.0;
+        for (int j = 0; j < h; ++j) dgn = dgn + c->vf_cs[j] * T[gb + j];
+        for (int j = 0; j < h; ++j) dgn = dgn + c->vf_cy[j] * T[gb + h + j];
+        dgn = dgn + c->vf_cg * T[LBK_VF_GGO];
+    }
+    T = c->vf_tot;
+    c->f_cur = T[LBK_VF_F];
+    if (alpha < 1e-10) { /* :164-168 */
+        say(c, "Warning: Line search failed at iteration %d\n", k);
+        c->status = LBFGS_STATUS_LS_FAILED;
+        return 1;
+    }
+    const double sy = T[LBK_VF_SY];
+    const int yb = LBK_VF_YB;
+    if (sy > 0) { /* :182-191 */
+        const int p = c->free_pair;
+        /* derived row of s_new = alpha d against the old basis (old g row) */
+        double dS[MMAX], dY[MMAX];
+        for (int q = 0; q < h; ++q) {
+            const int rq = c->ring[q];
+            double a = 0.0, b = 0.0;
+            for (int j = 0; j < h; ++j) a = a + c->vf_cs[j] * c->Gss[GI(c, c->ring[j], rq)];
+            for (int j = 0; j < h; ++j) a = a + c->vf_cy[j] * c->Gsy[GI(c, rq, c->ring[j])];
+            dS[q] = a + c->vf_cg * c->Gsg[rq];
+            for (int j = 0; j < h; ++j) b = b + c->vf_cs[j] * c->Gsy[GI(c, c->ring[j], rq)];
+            for (int j = 0; j < h; ++j) b = b + c->vf_cy[j] * c->Gyy[GI(c, c->ring[j], rq)];
+            dY[q] = b + c->vf_cg * c->Gyg[rq];
+        }
+        double dd = 0.0;
+        for (int j = 0; j < h; ++j) dd = dd + c->vf_cs[j] * dS[j];
+        for (int j = 0; j < h; ++j) dd = dd + c->vf_cy[j] * dY[j];
+        dd = dd + c->vf_cg * gd;
+        for (int q = 0; q < h; ++q) {
+            const int rq = c->ring[q];
+            c->Gss[GI(c, p, rq)] = c->Gss[GI(c, rq, p)] = alpha * dS[q];
+            c->Gsy[GI(c, p, rq)] = alpha * dY[q];
+            c->Gsy[GI(c, rq, p)] = T[yb + q];
+            c->Gyy[GI(c, p, rq)] = c->Gyy[GI(c, rq, p)] = T[yb + h + q];
+            c->Gsg[rq] = T[gb + q];
+            c->Gyg[rq] = T[gb + h + q];
+        }
+        c->Gss[GI(c, p, p)] = (alpha * alpha) * dd;
+        c->Gsy[GI(c, p, p)] = sy;
+        c->Gyy[GI(c, p, p)] = T[LBK_VF_YY];
+        c->Gsg[p] = alpha * dgn;
+        c->Gyg[p] = T[LBK_VF_YG];
+        if (c->h >= m) {
+            const int oldest = c->ring[0];
+            for (int i = 0; i + 1 < m; ++i) c->ring[i] = c->ring[i + 1];
+            c->ring[m - 1] = p;
+            c->free_pair = oldest;
+        } else {
+            c->ring[c->h++] = p;
+            c->free_pair = c->h;
+        }
+    } else {
+        say(c, "Warning: Skipping update, sy = %g\n", sy); /* :192-195 */
+        for (int q = 0; q < h; ++q) {
+            c->Gsg[c->ring[q]] = T[gb + q];
+            c->Gyg[c->ring[q]] = T[gb + h + q];
+        }
+    }
+    double* t = c->x;
+    c->x = c->xn;
+    c->xn = t;
+    t = c->g;
+    c->g = c->gn;
+    c->gn = t;
+    c->gg = T[LBK_VF_GG];
+    c->k++;
+    return 0;
+}
+
 /* ------------------------------------------------------------------------------------------ */
 int lbfgs_solver_init(lbfgs_ctx* c, int objective, const lbfgs_host_fn* cb, int line_search,
                       const lbfgs_constants* k, const double* x0_host, double tolerance,
@@ -795,6 +1034,20 @@ int lbfgs_solver_init(lbfgs_ctx* c, int objective, const lbfgs_host_fn* cb, int 
     }
     c->unfused = (flags & LBFGS_FLAG_UNFUSED) != 0;
     if (c->unfused && (objective == LBFGS_OBJ_HOST || c->geo->world != 1)) return LBFGS_ERR_BAD_ARG;
+    c->vf = (flags & LBFGS_FLAG_VECTOR_FREE) != 0;
+    if (c->vf) {
+        if (c->unfused || objective == LBFGS_OBJ_HOST || c->geo->world != 1 || c->m > LBK_VF_HMAX)
+            return LBFGS_ERR_BAD_ARG;
+        const size_t P = (size_t)c->m + 1;
+        if (!c->Gss) {
+            c->Gss = (double*)calloc(P * P, sizeof(double));
+            c->Gsy = (double*)calloc(P * P, sizeof(double));
+            c->Gyy = (double*)calloc(P * P, sizeof(double));
+            c->Gsg = (double*)calloc(P, sizeof(double));
+            c->Gyg = (double*)calloc(P, sizeof(double));
+            if (!c->Gss || !c->Gsy || !c->Gyy || !c->Gsg || !c->Gyg) return LBFGS_ERR_NOMEM;
+        }
+    }
     c->obj = objective;
     c->ls = line_search;
     if (k)
@@ -851,7 +1104,7 @@ int lbfgs_solver_step(lbfgs_ctx* c, int max_steps, lbfgs_result* out) {
     const double t0 = now_s(), b0 = lbk_bytes_moved(c->dev);
     if (!c->finished) {
         for (int s = 0; s < max_steps; ++s) {
-            int rc = iterate(c);
+            int rc = c->vf ? iterate_vf(c) : iterate(c);
             if (rc < 0) return rc;
             if (rc == 1) {
                 c->finished = 1;

@@ -53,10 +53,11 @@ struct Geo {
 };
 
 struct Red {
-    double* partials;  // [LBK_KMAX][LBK_SEGS], local segment index
+    double* partials;  // [LBK_KW][LBK_SEGS], local segment index
     unsigned* cnt;     // [LBK_GROUPS] tickets
-    double* slot;      // this launch's result slot [LBK_GROUPS][LBK_KMAX]
+    double* slot;      // this launch's result slot [LBK_GROUPS][kstride]
     int ticket;        // 1: in-launch last-arriver stage 2; 0: k_group_reduce after the launch
+    int kstride;       // LBK_KMAX (regular slots) or LBK_KW (wide slots)
 };
 
 // Streaming loads/stores; NT = non-temporal (the vectors are touched once per pass and, at
@@ -225,18 +226,41 @@ __device__ __forceinline__ void reduce_publish(double (&acc)[K], const Geo& geo,
     if (!last_flag) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const int64_t gseg0 = (int64_t)g * LBK_SEG_PER_GROUP;
-    group_tree<K, true>(red.partials, gseg0 - geo.seg_lo, gseg0, geo.nseg, red.slot + g * LBK_KMAX, lds);
+    group_tree<K, true>(red.partials, gseg0 - geo.seg_lo, gseg0, geo.nseg, red.slot + g * red.kstride, lds);
     if (t == 0) __hip_atomic_store(red.cnt + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Reduce-kernel mode: one workgroup per group of this rank (stage 2 after the boundary).
 template <int K>
 __global__ __launch_bounds__(LB_BLOCK) void k_group_reduce(const double* __restrict__ partials, Geo geo,
-                                                           double* __restrict__ slot) {
+                                                           double* __restrict__ slot, int kstride) {
     __shared__ double lds[4][K];
     const int g = geo.g_lo + (int)blockIdx.x;
     const int64_t gseg0 = (int64_t)g * LBK_SEG_PER_GROUP;
-    group_tree<K, false>(partials, gseg0 - geo.seg_lo, gseg0, geo.nseg, slot + g * LBK_KMAX, lds);
+    group_tree<K, false>(partials, gseg0 - geo.seg_lo, gseg0, geo.nseg, slot + g * kstride, lds);
+}
+
+// The same stage 2 for a runtime number of components (wide slots): identical arithmetic per
+// component as group_tree.
+__global__ __launch_bounds__(LB_BLOCK) void k_group_reduce_wide(const double* __restrict__ partials, Geo geo,
+                                                                double* __restrict__ slot, int K, int kstride) {
+    __shared__ double lds[4][LBK_KW];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int g = geo.g_lo + (int)blockIdx.x;
+    const int64_t gseg0 = (int64_t)g * LBK_SEG_PER_GROUP;
+    const int64_t lbase = gseg0 - geo.seg_lo;
+    for (int k = 0; k < K; ++k) {
+        double p[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int64_t j = 4 * t + i;
+            p[i] = (gseg0 + j < geo.nseg) ? partials[(int64_t)k * LBK_SEGS + lbase + j] : 0.0;
+        }
+        const double q = wave_sum((p[0] + p[1]) + (p[2] + p[3]));
+        if (lane == 0) lds[w][k] = q;
+    }
+    __syncthreads();
+    for (int k = t; k < K; k += LB_BLOCK) slot[g * kstride + k] = (lds[0][k] + lds[1][k]) + (lds[2][k] + lds[3][k]);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -821,6 +845,170 @@ __global__ __launch_bounds__(LB_BLOCK) void k_commit(const double* __restrict__ 
     run_pass<OpCommit<OBJ, DMODE, NT>, 7>(OpCommit<OBJ, DMODE, NT>{x, da, alpha, xn, gn, so, yo, geo.n, geo.n_loc}, geo, red);
 }
 
+// ---------------------------------------------------------------------------------------
+// Vector-free mode (LBFGS_FLAG_VECTOR_FREE). The two-loop runs on the host in coefficient
+// space over the Gram matrix of the basis b = [s_0..s_{h-1}, y_0..y_{h-1}, g]; the device
+// pass forms d = sum_l c_l b_l + cg g on the fly (l ascending, then g; each product rounded,
+// -ffp-contract=off), evaluates the first trial and commits in one sweep, and reduces the new
+// Gram rows. HB is the compile-time capacity (bucket) of h, with uniform runtime guards l < 2h,
+// so the basis registers and accumulators have static indices.
+// ---------------------------------------------------------------------------------------
+template <int HB>
+struct VfBasis {
+    const double* b[2 * HB > 0 ? 2 * HB : 1];
+    double c[2 * HB > 0 ? 2 * HB : 1];
+    double cg;
+    int h;
+};
+
+template <int HB>
+__device__ __forceinline__ double vf_dir1(const VfBasis<HB>& B, const double* __restrict__ g, int64_t i) {
+    double d = 0.0;
+#pragma unroll
+    for (int l = 0; l < 2 * HB; ++l)
+        if (l < 2 * B.h) d = (l == 0) ? B.c[0] * B.b[0][i] : d + B.c[l] * B.b[l][i];
+    return B.h == 0 ? B.cg * g[i] : d + B.cg * g[i];
+}
+
+// f terms, gradient, x_new, s, y, and the dots (components LBK_VF_*)
+template <int OBJ, int HB, bool NT>
+struct OpVfCommit {
+    static constexpr int K = LBK_VF_YB + 4 * HB;
+    const double* __restrict__ x;
+    const double* __restrict__ g;
+    VfBasis<HB> B;
+    double alpha;
+    double* __restrict__ xn;
+    double* __restrict__ gn;
+    double* __restrict__ so;
+    double* __restrict__ yo;
+    int64_t n, n_loc;
+    struct Row {
+        double2 x, g, d, z;
+        double2 b[2 * HB > 0 ? 2 * HB : 1];
+        double zh;
+    };
+    __device__ void load(Row& r, int64_t i) const {
+        r.x = ldv<NT>(x + i);
+        r.g = ldv<NT>(g + i);
+#pragma unroll
+        for (int l = 0; l < 2 * HB; ++l)
+            if (l < 2 * B.h) r.b[l] = ldv<NT>(B.b[l] + i);
+        double2 d = make_double2(0.0, 0.0);
+#pragma unroll
+        for (int l = 0; l < 2 * HB; ++l) {
+            if (l < 2 * B.h) {
+                if (l == 0) {
+                    d.x = B.c[0] * r.b[0].x;
+                    d.y = B.c[0] * r.b[0].y;
+                } else {
+                    d.x = d.x + B.c[l] * r.b[l].x;
+                    d.y = d.y + B.c[l] * r.b[l].y;
+                }
+            }
+        }
+        if (B.h == 0) {
+            d.x = B.cg * r.g.x;
+            d.y = B.cg * r.g.y;
+        } else {
+            d.x = d.x + B.cg * r.g.x;
+            d.y = d.y + B.cg * r.g.y;
+        }
+        r.d = d;
+        r.z.x = r.x.x + alpha * d.x;
+        r.z.y = r.x.y + alpha * d.y;
+        r.zh = 0.0;
+        if (needs_halo<OBJ>()) {
+            const int lane = threadIdx.x & 63;
+            if (lane == 0 || lane == 63) {
+                const int64_t hi = (lane == 0) ? i - 1 : i + 2;
+                if (hi >= -1 && hi <= n_loc) r.zh = x[hi] + alpha * vf_dir1<HB>(B, g, hi);
+            }
+        }
+    }
+    template <bool MASK>
+    __device__ void apply(Row& r, int64_t i, int64_t e0, bool v0, bool v1, double (&acc)[K]) const {
+        const double2 g2 = objective_pair<OBJ, MASK>(r.z, r.zh, e0, n, v0, v1, acc[LBK_VF_F], true);
+        st2<MASK, NT>(gn + i, g2, v0, v1);
+        st2<MASK, NT>(xn + i, r.z, v0, v1);
+        double2 sv, yv;
+        sv.x = r.z.x - r.x.x;
+        sv.y = r.z.y - r.x.y;
+        yv.x = g2.x - r.g.x;
+        yv.y = g2.y - r.g.y;
+        st2<MASK, NT>(so + i, sv, v0, v1);
+        st2<MASK, NT>(yo + i, yv, v0, v1);
+        acc[LBK_VF_SY] = fma2<MASK>(sv, yv, acc[LBK_VF_SY], v0, v1);
+        acc[LBK_VF_YY] = fma2<MASK>(yv, yv, acc[LBK_VF_YY], v0, v1);
+        acc[LBK_VF_GG] = fma2<MASK>(g2, g2, acc[LBK_VF_GG], v0, v1);
+        acc[LBK_VF_YG] = fma2<MASK>(yv, g2, acc[LBK_VF_YG], v0, v1);
+        acc[LBK_VF_GGO] = fma2<MASK>(g2, r.g, acc[LBK_VF_GGO], v0, v1);
+#pragma unroll
+        for (int l = 0; l < 2 * HB; ++l) {
+            if (l < 2 * B.h) {
+                acc[LBK_VF_YB + l] = fma2<MASK>(yv, r.b[l], acc[LBK_VF_YB + l], v0, v1);
+                acc[LBK_VF_YB + 2 * HB + l] = fma2<MASK>(g2, r.b[l], acc[LBK_VF_YB + 2 * HB + l], v0, v1);
+            }
+        }
+    }
+};
+
+// one row per step: a row already has 2h + 2 independent 16-B loads in flight per lane
+template <int K, class Op>
+__device__ __forceinline__ void stream1(const Op& op, const Seg& s, const Geo& geo, double (&acc)[K]) {
+    if (s.len == geo.L) {
+        for (int u = 0; u < s.nrows; ++u) rows<false, 1>(op, s, u, acc);
+    } else {
+        for (int u = 0; u < s.nrows; ++u) rows<true, 1>(op, s, u, acc);
+    }
+}
+
+template <int OBJ, int HB, bool NT>
+__global__ __launch_bounds__(LB_BLOCK) void k_vf_commit(OpVfCommit<OBJ, HB, NT> op, Geo geo, Red red) {
+    constexpr int K = OpVfCommit<OBJ, HB, NT>::K;
+    const Seg s = seg_setup(geo);
+    double acc[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) acc[k] = 0.0;
+    stream1(op, s, geo, acc);
+    reduce_publish<K>(acc, geo, red);
+}
+
+// materialised d over [0, n_loc) (the rejected-first-trial path; same formula as the commit)
+template <int HB, bool NT>
+__global__ __launch_bounds__(256) void k_vf_dir(double* __restrict__ d, const double* __restrict__ g, VfBasis<HB> B,
+                                                int64_t n_loc) {
+    const int64_t npair = n_loc >> 1;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < npair; p += stride) {
+        const int64_t i = 2 * p;
+        double2 v = make_double2(0.0, 0.0);
+#pragma unroll
+        for (int l = 0; l < 2 * HB; ++l) {
+            if (l < 2 * B.h) {
+                const double2 b = ldv<NT>(B.b[l] + i);
+                if (l == 0) {
+                    v.x = B.c[0] * b.x;
+                    v.y = B.c[0] * b.y;
+                } else {
+                    v.x = v.x + B.c[l] * b.x;
+                    v.y = v.y + B.c[l] * b.y;
+                }
+            }
+        }
+        const double2 gv = ldv<NT>(g + i);
+        if (B.h == 0) {
+            v.x = B.cg * gv.x;
+            v.y = B.cg * gv.y;
+        } else {
+            v.x = v.x + B.cg * gv.x;
+            v.y = v.y + B.cg * gv.y;
+        }
+        stv<NT>(d + i, v);
+    }
+    if ((n_loc & 1) && blockIdx.x == 0 && threadIdx.x == 0) d[n_loc - 1] = vf_dir1<HB>(B, g, n_loc - 1);
+}
+
 // z = x + alpha d over the whole local range incl. ghosts (host-callback objectives)
 __global__ void k_point(double* __restrict__ z, const double* __restrict__ x, const double* __restrict__ d,
                         double alpha, int64_t lo, int64_t hi) {
@@ -930,7 +1118,7 @@ __global__ void k_checksum(const double* __restrict__ x, int64_t n_loc, int64_t 
 struct lbk_group {
     int world;
     pthread_barrier_t bar;
-    double table[LBK_SLOT];
+    double table[LBK_WSLOT];
     unsigned long long ck[LBK_GROUPS][2];
 };
 
@@ -942,6 +1130,8 @@ struct lbk_ctx {
     unsigned* cnt;      // LBK_GROUPS
     double* slots;      // LBK_NSLOTS * LBK_SLOT
     double* h_slots;    // pinned mirror
+    double* wslots;     // LBK_NWSLOTS * LBK_WSLOT (wide slots)
+    double* h_wslots;   // pinned mirror
     unsigned long long* d_ck;
     unsigned long long* h_ck;
     int64_t vec_doubles;  // allocation per vector
@@ -992,11 +1182,23 @@ Geo kgeo(const lbk_ctx* c) {
     return g;
 }
 
+// regular slots 0..LBK_NSLOTS-1 (LBK_KMAX components), wide slots LBK_WSLOT0 + w (LBK_KW)
+double* slot_base(const lbk_ctx* c, int slot) {
+    return slot < LBK_NSLOTS ? c->slots + (int64_t)slot * LBK_SLOT
+                             : c->wslots + (int64_t)(slot - LBK_WSLOT0) * LBK_WSLOT;
+}
+double* slot_host(const lbk_ctx* c, int slot) {
+    return slot < LBK_NSLOTS ? c->h_slots + (int64_t)slot * LBK_SLOT
+                             : c->h_wslots + (int64_t)(slot - LBK_WSLOT0) * LBK_WSLOT;
+}
+int slot_stride(int slot) { return slot < LBK_NSLOTS ? LBK_KMAX : LBK_KW; }
+
 Red kred(const lbk_ctx* c, int slot) {
     Red r;
     r.partials = c->partials;
     r.cnt = c->cnt;
-    r.slot = c->slots + (int64_t)slot * LBK_SLOT;
+    r.slot = slot_base(c, slot);
+    r.kstride = slot_stride(slot);
     r.ticket = c->ticket;
     return r;
 }
@@ -1042,19 +1244,20 @@ int prof_flush(lbk_ctx* c) {
 // every rank holds all 8 (one RCCL all-gather of (8/world) x KMAX doubles per reduction, in
 // place, on the solver stream), or through the host group for emulated ranks.
 int exchange_slot(lbk_ctx* c, int slot) {
-    const int per = (c->geo.g_hi - c->geo.g_lo) * LBK_KMAX;
-    double* base = c->slots + (int64_t)slot * LBK_SLOT;
+    const int ks = slot_stride(slot);
+    const int per = (c->geo.g_hi - c->geo.g_lo) * ks;
+    double* base = slot_base(c, slot);
     if (c->grp) {
         lbk_group* G = c->grp;
         HIPCHK(c, hipStreamSynchronize(c->stream));
-        HIPCHK(c, hipMemcpy(G->table + c->geo.g_lo * LBK_KMAX, base + c->geo.g_lo * LBK_KMAX,
+        HIPCHK(c, hipMemcpy(G->table + c->geo.g_lo * ks, base + c->geo.g_lo * ks,
                             sizeof(double) * per, hipMemcpyDeviceToHost));
         pthread_barrier_wait(&G->bar);
-        HIPCHK(c, hipMemcpy(base, G->table, sizeof(double) * LBK_SLOT, hipMemcpyHostToDevice));
+        HIPCHK(c, hipMemcpy(base, G->table, sizeof(double) * LBK_GROUPS * ks, hipMemcpyHostToDevice));
         pthread_barrier_wait(&G->bar);
         return 0;
     }
-    ncclResult_t r = ncclAllGather(base + c->geo.g_lo * LBK_KMAX, base, (size_t)per, ncclDouble, c->comm, c->stream);
+    ncclResult_t r = ncclAllGather(base + c->geo.g_lo * ks, base, (size_t)per, ncclDouble, c->comm, c->stream);
     if (r != ncclSuccess) {
         snprintf(c->err, sizeof c->err, "ncclAllGather: %s", ncclGetErrorString(r));
         return -3;
@@ -1080,12 +1283,16 @@ int launch(lbk_ctx* c, int kind, double vec_passes, int slot, F&& fn, int K = 1)
     }
     if (slot >= 0 && !c->ticket) {
         const Geo g = kgeo(c);
-        double* sl = c->slots + (int64_t)slot * LBK_SLOT;
+        double* sl = slot_base(c, slot);
+        const int ks = slot_stride(slot);
         const dim3 grid(c->geo.g_hi - c->geo.g_lo), blk(LB_BLOCK);
         switch (K) {
-            case 1: hipLaunchKernelGGL(k_group_reduce<1>, grid, blk, 0, c->stream, c->partials, g, sl); break;
-            case 2: hipLaunchKernelGGL(k_group_reduce<2>, grid, blk, 0, c->stream, c->partials, g, sl); break;
-            default: hipLaunchKernelGGL(k_group_reduce<7>, grid, blk, 0, c->stream, c->partials, g, sl); break;
+            case 1: hipLaunchKernelGGL(k_group_reduce<1>, grid, blk, 0, c->stream, c->partials, g, sl, ks); break;
+            case 2: hipLaunchKernelGGL(k_group_reduce<2>, grid, blk, 0, c->stream, c->partials, g, sl, ks); break;
+            case 7: hipLaunchKernelGGL(k_group_reduce<7>, grid, blk, 0, c->stream, c->partials, g, sl, ks); break;
+            default:
+                hipLaunchKernelGGL(k_group_reduce_wide, grid, blk, 0, c->stream, c->partials, g, sl, K, ks);
+                break;
         }
         HIPCHK(c, hipGetLastError());
     }
@@ -1168,13 +1375,16 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
     } while (0)
     CK(hipSetDevice(device));
     CK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-    CK(hipMalloc(&c->partials, sizeof(double) * LBK_KMAX * LBK_SEGS));
+    CK(hipMalloc(&c->partials, sizeof(double) * LBK_KW * LBK_SEGS));
     CK(hipMalloc(&c->cnt, sizeof(unsigned) * 16));
     CK(hipMalloc(&c->slots, sizeof(double) * LBK_NSLOTS * LBK_SLOT));
     CK(hipHostMalloc(&c->h_slots, sizeof(double) * LBK_NSLOTS * LBK_SLOT, hipHostMallocDefault));
     CK(hipMalloc(&c->d_ck, 2 * sizeof(unsigned long long)));
     CK(hipHostMalloc(&c->h_ck, 2 * sizeof(unsigned long long), hipHostMallocDefault));
-    CK(hipMemset(c->partials, 0, sizeof(double) * LBK_KMAX * LBK_SEGS));
+    CK(hipMemset(c->partials, 0, sizeof(double) * LBK_KW * LBK_SEGS));
+    CK(hipMalloc(&c->wslots, sizeof(double) * LBK_NWSLOTS * LBK_WSLOT));
+    CK(hipHostMalloc(&c->h_wslots, sizeof(double) * LBK_NWSLOTS * LBK_WSLOT, hipHostMallocDefault));
+    CK(hipMemset(c->wslots, 0, sizeof(double) * LBK_NWSLOTS * LBK_WSLOT));
     CK(hipMemset(c->cnt, 0, sizeof(unsigned) * 16));
     CK(hipMemset(c->slots, 0, sizeof(double) * LBK_NSLOTS * LBK_SLOT));
     CK(hipDeviceSynchronize());
@@ -1202,6 +1412,8 @@ void lbk_destroy(lbk_ctx* c) {
     (void)hipFree(c->cnt);
     (void)hipFree(c->slots);
     (void)hipHostFree(c->h_slots);
+    (void)hipFree(c->wslots);
+    (void)hipHostFree(c->h_wslots);
     (void)hipFree(c->d_ck);
     (void)hipHostFree(c->h_ck);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -1431,6 +1643,98 @@ int lbk_elementwise(lbk_ctx* c, int op, double* out, const double* a, const doub
     });
 }
 
+// ---- vector-free mode -------------------------------------------------------------------
+}  // extern "C"
+namespace {
+template <int HB>
+VfBasis<HB> vf_basis(int h, const double* const* S, const double* const* Y, const double* cs, const double* cy,
+                     double cg) {
+    VfBasis<HB> B;
+    memset(&B, 0, sizeof B);
+    B.h = h;
+    B.cg = cg;
+    for (int l = 0; l < h; ++l) {
+        B.b[l] = S[l];
+        B.c[l] = cs[l];
+        B.b[h + l] = Y[l];
+        B.c[h + l] = cy[l];
+    }
+    return B;
+}
+
+template <int HB>
+int vf_commit_hb(lbk_ctx* c, int obj, int h, const double* x, const double* g, const double* const* S,
+                 const double* const* Y, const double* cs, const double* cy, double cg, double alpha, double* xn,
+                 double* gn, double* so, double* yo, int wslot) {
+    Geo geo = kgeo(c);
+    Red r = kred(c, wslot);
+    const VfBasis<HB> B = vf_basis<HB>(h, S, Y, cs, cy, cg);
+    constexpr int K = LBK_VF_YB + 4 * HB;
+    return launch(c, LBK_K_VF_COMMIT, 2.0 * h + 6.0, wslot, [&] {
+        OBJ_DISPATCH(obj, {
+            OpVfCommit<O_, HB, NT_> op{x, g, B, alpha, xn, gn, so, yo, geo.n, geo.n_loc};
+            hipLaunchKernelGGL((k_vf_commit<O_, HB, NT_>), dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, op, geo, r);
+        });
+        return 0;
+    }, K);
+}
+
+template <int HB>
+int vf_dir_hb(lbk_ctx* c, int h, double* d, const double* g, const double* const* S, const double* const* Y,
+              const double* cs, const double* cy, double cg) {
+    const VfBasis<HB> B = vf_basis<HB>(h, S, Y, cs, cy, cg);
+    const int64_t npair = c->geo.n_loc / 2;
+    const int nb = (int)std::max<int64_t>(1, std::min<int64_t>((npair + 255) / 256, 16384));
+    return launch(c, LBK_K_VF_DIR, 2.0 * h + 2.0, -1, [&] {
+        if (c->geo.n_loc <= 0) return;
+        NT_DISPATCH(c, hipLaunchKernelGGL((k_vf_dir<HB, NT_>), dim3(nb), dim3(256), 0, c->stream, d, g, B,
+                                          c->geo.n_loc));
+    });
+}
+}  // namespace
+extern "C" {
+
+#define VF_BUCKETS(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(8) X(10) X(12) X(16) X(20)
+
+int lbk_vf_bucket(int h) {
+    static const int hb[] = {0, 1, 2, 3, 4, 5, 6, 8, 10, 12, 16, 20};
+    for (int v : hb)
+        if (h <= v) return v;
+    return -1;
+}
+
+int lbk_vf_commit(lbk_ctx* c, int obj, int h, const double* x, const double* g, const double* const* S,
+                  const double* const* Y, const double* cs, const double* cy, double cg, double alpha,
+                  double* xn, double* gn, double* so, double* yo, int wslot, int* hb_out) {
+    const int hb = lbk_vf_bucket(h);
+    if (hb < 0 || wslot < LBK_WSLOT0 || wslot >= LBK_WSLOT0 + LBK_NWSLOTS || c->geo.world != 1) {
+        snprintf(c->err, sizeof c->err, "lbk_vf_commit: h=%d (max %d), slot %d, world %d", h, LBK_VF_HMAX, wslot,
+                 c->geo.world);
+        return -1;
+    }
+    *hb_out = hb;
+    switch (hb) {
+#define VF_CASE(HB) \
+    case HB: return vf_commit_hb<HB>(c, obj, h, x, g, S, Y, cs, cy, cg, alpha, xn, gn, so, yo, wslot);
+        VF_BUCKETS(VF_CASE)
+#undef VF_CASE
+    }
+    return -1;
+}
+
+int lbk_vf_dir(lbk_ctx* c, int h, double* d, const double* g, const double* const* S, const double* const* Y,
+               const double* cs, const double* cy, double cg) {
+    const int hb = lbk_vf_bucket(h);
+    if (hb < 0 || c->geo.world != 1) return -1;
+    switch (hb) {
+#define VF_CASE(HB) \
+    case HB: return vf_dir_hb<HB>(c, h, d, g, S, Y, cs, cy, cg);
+        VF_BUCKETS(VF_CASE)
+#undef VF_CASE
+    }
+    return -1;
+}
+
 int lbk_update(lbk_ctx* c, int op, double* out, const double* a, const double* b, double rho, int slot_a,
                int slot_b, double scal) {
     const int64_t npair = c->geo.n_loc / 2;
@@ -1505,19 +1809,25 @@ double lbk_total(const double* groups64, int comp) {
 }
 
 int lbk_fetch_groups(lbk_ctx* c, int slot, double* groups64) {
-    double* h = c->h_slots + (int64_t)slot * LBK_SLOT;
-    HIPCHK(c, hipMemcpyAsync(h, c->slots + (int64_t)slot * LBK_SLOT, sizeof(double) * LBK_SLOT,
-                             hipMemcpyDeviceToHost, c->stream));
+    double* h = slot_host(c, slot);
+    const size_t bytes = sizeof(double) * LBK_GROUPS * slot_stride(slot);
+    HIPCHK(c, hipMemcpyAsync(h, slot_base(c, slot), bytes, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    memcpy(groups64, h, sizeof(double) * LBK_SLOT);
+    memcpy(groups64, h, bytes);
     return 0;
 }
 
+// fixed-order total Q0 + Q1 + ... + Q7 of each component (regular or wide slot)
 int lbk_fetch(lbk_ctx* c, int slot, int ncomp, double* totals) {
-    double g64[LBK_SLOT];
-    int rc = lbk_fetch_groups(c, slot, g64);
+    double gw[LBK_WSLOT];
+    int rc = lbk_fetch_groups(c, slot, gw);
     if (rc) return rc;
-    for (int k = 0; k < ncomp; ++k) totals[k] = lbk_total(g64, k);
+    const int ks = slot_stride(slot);
+    for (int k = 0; k < ncomp; ++k) {
+        double t = gw[k];
+        for (int g = 1; g < LBK_GROUPS; ++g) t = t + gw[g * ks + k];
+        totals[k] = t;
+    }
     return 0;
 }
 

@@ -19,9 +19,9 @@ LIB_PATH = os.environ.get("LBFGS_LIB") or os.path.join(HERE, "liblbfgs_hip.so") 
 OBJECTIVES = {"rosenbrock": 0, "quad_tridiag": 1, "quad_sep": 2, "host": 3}
 LINE_SEARCHES = {"backtracking": 0, "interpolation": 1, "wolfe": 2, "backtracking_wolfe": 3}
 STATUS = {0: "converged", 1: "max_iter", 2: "ls_failed", 3: "running"}
-FLAG_VERBOSE, FLAG_QUIET, FLAG_TRACE, FLAG_UNFUSED = 1, 2, 4, 8
+FLAG_VERBOSE, FLAG_QUIET, FLAG_TRACE, FLAG_UNFUSED, FLAG_VECTOR_FREE = 1, 2, 4, 8, 16
 KERNELS = ["dot", "axpy_dot", "mid", "axpy2_dot", "last", "negdot", "eval", "trial_f",
-           "trial_fg", "commit", "point", "checksum", "update"]
+           "trial_fg", "commit", "point", "checksum", "update", "vf_commit", "vf_dir"]
 
 
 class LbfgsError(RuntimeError):
@@ -242,14 +242,15 @@ class Context:
 
     def minimize(self, objective, x0, line_search="backtracking", max_iterations=1000, m=None,
                  tolerance=1e-5, verbose=False, quiet=True, trace=False, consts=None,
-                 f=None, grad=None, unfused=False):
+                 f=None, grad=None, unfused=False, vector_free=False):
         assert m is None or m == self.m
         x0 = np.ascontiguousarray(x0, dtype=np.float64)
         assert x0.shape == (self.n,)
         x = np.zeros(self.n)
         res = Result()
         flags = (FLAG_VERBOSE if verbose else 0) | (FLAG_QUIET if quiet else 0) | \
-                (FLAG_TRACE if trace else 0) | (FLAG_UNFUSED if unfused else 0)
+                (FLAG_TRACE if trace else 0) | (FLAG_UNFUSED if unfused else 0) | \
+                (FLAG_VECTOR_FREE if vector_free else 0)
         cb = self._host_fn(f, grad) if objective == "host" else None
         k = consts if consts is not None else constants()
         rc = lib().lbfgs_minimize(self.h, OBJECTIVES[objective], C.byref(cb) if cb else None,
@@ -265,9 +266,10 @@ class Context:
         return out
 
     def init(self, objective, x0, line_search="backtracking", tolerance=1e-5, quiet=True,
-             trace=False, consts=None, unfused=False):
+             trace=False, consts=None, unfused=False, vector_free=False):
         x0 = np.ascontiguousarray(x0, dtype=np.float64)
-        flags = (FLAG_QUIET if quiet else 0) | (FLAG_TRACE if trace else 0) | (FLAG_UNFUSED if unfused else 0)
+        flags = (FLAG_QUIET if quiet else 0) | (FLAG_TRACE if trace else 0) | \
+            (FLAG_UNFUSED if unfused else 0) | (FLAG_VECTOR_FREE if vector_free else 0)
         k = consts if consts is not None else constants()
         rc = lib().lbfgs_solver_init(self.h, OBJECTIVES[objective], None,
                                      LINE_SEARCHES[line_search], C.byref(k), x0, float(tolerance),

@@ -80,6 +80,13 @@ enum {
  * the commit). Same iterates, bit for bit, as the fused default; single rank, device
  * objectives only. BASELINE configs[1] ("unfused per-vector kernels"). */
 #define LBFGS_FLAG_UNFUSED 8u
+/* vector-free (Gram-matrix) L-BFGS: the two-loop recursion on the host over the Gram matrix of
+ * the basis {s_i, y_i, g}; one fused device pass per iteration forms d, takes the first trial,
+ * commits and reduces the new Gram rows (~2m+6 vector passes instead of 8m+3). The same
+ * algorithm in exact arithmetic; rounding differs from the reference's operation order
+ * (f within 1e-10 over horizons comparable to the canonical order's). Single rank,
+ * device objectives, m <= 20. */
+#define LBFGS_FLAG_VECTOR_FREE 16u
 
 typedef struct {
     double c1;                 /* C1 = 1e-4                  config.h:5 */
@@ -193,7 +200,8 @@ enum {
     LBFGS_KERNEL_DOT = 0, LBFGS_KERNEL_AXPY_DOT, LBFGS_KERNEL_MID, LBFGS_KERNEL_AXPY2_DOT,
     LBFGS_KERNEL_LAST, LBFGS_KERNEL_NEGDOT, LBFGS_KERNEL_EVAL, LBFGS_KERNEL_TRIAL_F,
     LBFGS_KERNEL_TRIAL_FG, LBFGS_KERNEL_COMMIT, LBFGS_KERNEL_POINT, LBFGS_KERNEL_CHECKSUM,
-    LBFGS_KERNEL_UPDATE, LBFGS_KERNEL_COUNT
+    LBFGS_KERNEL_UPDATE, LBFGS_KERNEL_VF_COMMIT, LBFGS_KERNEL_VF_DIR,
+    LBFGS_KERNEL_COUNT
 };
 void lbfgs_prof_enable(lbfgs_ctx* ctx, int on);
 void lbfgs_prof_reset(lbfgs_ctx* ctx);

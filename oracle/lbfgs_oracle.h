@@ -38,6 +38,9 @@ typedef struct {
     double (*host_f)(const double* x, int64_t n, void* user);
     void (*host_g)(const double* x, int64_t n, double* g, void* user);
     void* host_user;
+    /* 1: vector-free (Gram-matrix) variant of the product's LBFGS_FLAG_VECTOR_FREE mode,
+     * restated in ORC_CANON order (not a reference algorithm; its own parity contract) */
+    int vf;
 } orc_opts;
 
 typedef struct {

@@ -31,7 +31,8 @@ class Opts(C.Structure):
                 ("c1", C.c_double), ("c2", C.c_double), ("initial_step", C.c_double),
                 ("backtracking_alpha", C.c_double), ("backtracking_tol", C.c_double),
                 ("wolfe_interp_min", C.c_double),
-                ("host_f", C.c_void_p), ("host_g", C.c_void_p), ("host_user", C.c_void_p)]
+                ("host_f", C.c_void_p), ("host_g", C.c_void_p), ("host_user", C.c_void_p),
+                ("vf", C.c_int)]
 
 
 HOST_F = C.CFUNCTYPE(C.c_double, C.POINTER(C.c_double), C.c_int64, C.c_void_p)
@@ -136,7 +137,7 @@ def np_checksum(x):
 
 
 def lbfgs(obj, x0, ls, m, maxit, tol, mode=CANON, consts=None, log_calls=False, verbose=False,
-          f=None, grad=None):
+          f=None, grad=None, vector_free=False):
     """Run the oracle; returns a dict with x, trace arrays, call logs and messages.
     obj="host" takes the objective from the Python callables f(x) and grad(x)."""
     x0 = np.ascontiguousarray(x0, np.float64)
@@ -145,7 +146,7 @@ def lbfgs(obj, x0, ls, m, maxit, tol, mode=CANON, consts=None, log_calls=False, 
     if consts:
         k.update(consts)
     o = Opts(obj=OBJ[obj], ls=LS[ls], mode=mode, verbose=int(verbose), n=n, m=m, maxit=maxit,
-             tol=tol, **k)
+             tol=tol, vf=int(vector_free), **k)
     cbs = None
     if obj == "host":
         cbs = host_callbacks(f, grad)
