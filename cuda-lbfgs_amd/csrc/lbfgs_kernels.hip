@@ -411,10 +411,10 @@ __device__ __forceinline__ void stream(const Op& op, const Seg& s, const Geo& ge
 
 template <bool MASK, bool NT>
 __device__ __forceinline__ void st2(double* p, double2 v, bool v0, bool v1) {
-    if (MASK)
-        st2m(p, v, v0, v1);
-    else
+    if (!MASK || (v0 && v1))
         stv<NT>(p, v);
+    else
+        st2m(p, v, v0, v1);
 }
 
 // acc = fma(a, b, acc) for the valid elements of a lane pair
@@ -874,6 +874,7 @@ __device__ __forceinline__ double vf_dir1(const VfBasis<HB>& B, const double* __
 template <int OBJ, int HB, bool NT>
 struct OpVfCommit {
     static constexpr int K = LBK_VF_YB + 4 * HB;
+    static constexpr int NB = 2 * HB;
     const double* __restrict__ x;
     const double* __restrict__ g;
     VfBasis<HB> B;
@@ -884,10 +885,11 @@ struct OpVfCommit {
     double* __restrict__ yo;
     int64_t n, n_loc;
     struct Row {
-        double2 x, g, d, z;
+        double2 x, g, z;
         double2 b[2 * HB > 0 ? 2 * HB : 1];
         double zh;
     };
+    // x, g, the basis and z = x + alpha d of local elements i, i+1
     __device__ void load(Row& r, int64_t i) const {
         r.x = ldv<NT>(x + i);
         r.g = ldv<NT>(g + i);
@@ -914,17 +916,45 @@ struct OpVfCommit {
             d.x = d.x + B.cg * r.g.x;
             d.y = d.y + B.cg * r.g.y;
         }
-        r.d = d;
         r.z.x = r.x.x + alpha * d.x;
         r.z.y = r.x.y + alpha * d.y;
         r.zh = 0.0;
-        if (needs_halo<OBJ>()) {
-            const int lane = threadIdx.x & 63;
-            if (lane == 0 || lane == 63) {
-                const int64_t hi = (lane == 0) ? i - 1 : i + 2;
-                if (hi >= -1 && hi <= n_loc) r.zh = x[hi] + alpha * vf_dir1<HB>(B, g, hi);
+    }
+    // lane 63: keep the basis values of its last element for finish()
+    __device__ void park(const Row& r, double* pk) const {
+#pragma unroll
+        for (int l = 0; l < 2 * HB; ++l)
+            if (l < 2 * B.h) pk[l] = r.b[l].y;
+    }
+    // the deferred last element of a row (local i, global e) once its right neighbour zp is
+    // known: the second element of apply() for lane 63, in the same operation order
+    __device__ void finish(double zm, double zc, double zp, double xv, double gv, const double* pk, int64_t i,
+                           int64_t e, double (&acc)[K]) const {
+        const bool p1 = e + 1 < n;
+        if (obj_has_term<OBJ>(p1)) acc[LBK_VF_F] = acc[LBK_VF_F] + obj_term<OBJ>(zc, zp, p1);
+        const double g2 = obj_grad<OBJ>(zm, zc, zp, true, p1);
+        gn[i] = g2;
+        xn[i] = zc;
+        const double sv = zc - xv, yv = g2 - gv;
+        so[i] = sv;
+        yo[i] = yv;
+        acc[LBK_VF_SY] = fma(sv, yv, acc[LBK_VF_SY]);
+        acc[LBK_VF_YY] = fma(yv, yv, acc[LBK_VF_YY]);
+        acc[LBK_VF_GG] = fma(g2, g2, acc[LBK_VF_GG]);
+        acc[LBK_VF_YG] = fma(yv, g2, acc[LBK_VF_YG]);
+        acc[LBK_VF_GGO] = fma(g2, gv, acc[LBK_VF_GGO]);
+#pragma unroll
+        for (int l = 0; l < 2 * HB; ++l) {
+            if (l < 2 * B.h) {
+                acc[LBK_VF_YB + l] = fma(yv, pk[l], acc[LBK_VF_YB + l]);
+                acc[LBK_VF_YB + 2 * HB + l] = fma(g2, pk[l], acc[LBK_VF_YB + 2 * HB + l]);
             }
         }
+    }
+    // z at one local element (-1 <= hi <= n_loc) formed from memory (segment edges only)
+    __device__ double z_at(int64_t hi) const {
+        if (!needs_halo<OBJ>()) return 0.0;
+        return (hi >= -1 && hi <= n_loc) ? x[hi] + alpha * vf_dir1<HB>(B, g, hi) : 0.0;
     }
     template <bool MASK>
     __device__ void apply(Row& r, int64_t i, int64_t e0, bool v0, bool v1, double (&acc)[K]) const {
@@ -943,6 +973,9 @@ struct OpVfCommit {
         acc[LBK_VF_GG] = fma2<MASK>(g2, g2, acc[LBK_VF_GG], v0, v1);
         acc[LBK_VF_YG] = fma2<MASK>(yv, g2, acc[LBK_VF_YG], v0, v1);
         acc[LBK_VF_GGO] = fma2<MASK>(g2, r.g, acc[LBK_VF_GGO], v0, v1);
+#if LBK_VF_EXP == 2
+        if (B.h < 0)
+#endif
 #pragma unroll
         for (int l = 0; l < 2 * HB; ++l) {
             if (l < 2 * B.h) {
@@ -953,13 +986,57 @@ struct OpVfCommit {
     }
 };
 
-// one row per step: a row already has 2h + 2 independent 16-B loads in flight per lane
+#ifndef LBK_VF_EXP
+#define LBK_VF_EXP 0
+#endif
+
+// The segment walk of the vector-free commit. Wave w takes a contiguous run of rows
+// [wR, min((w+1)R, nrow)), R = ceil(nrow / 4) (the ORC_CANON_VF order), so a row's left stencil
+// neighbour is the previous row's last z, carried in a register, and its right neighbour is the
+// next row's first z: lane 63's last element is finished one step later, after the next row is
+// loaded (its basis values parked in wave-private LDS). Each lane still accumulates its
+// elements in ascending order. Only the ends of a wave's run form z from memory (Op::z_at):
+// 2 per wave per segment instead of 2 per row. No barriers: the waves stream independently.
 template <int K, class Op>
-__device__ __forceinline__ void stream1(const Op& op, const Seg& s, const Geo& geo, double (&acc)[K]) {
-    if (s.len == geo.L) {
-        for (int u = 0; u < s.nrows; ++u) rows<false, 1>(op, s, u, acc);
-    } else {
-        for (int u = 0; u < s.nrows; ++u) rows<true, 1>(op, s, u, acc);
+__device__ __forceinline__ void stream_vf(const Op& op, const Seg& s, const Geo& geo, double (&acc)[K]) {
+    constexpr int NB = Op::NB > 0 ? Op::NB : 1;
+    __shared__ double park[4][NB];
+    const int nrow = (int)((s.len + 127) / 128);
+    const int R = (nrow + 3) / 4;
+    const int r0 = s.w * R;
+    const int r1 = min(r0 + R, nrow);
+    if (r0 >= r1) return;
+    const bool full = s.len == geo.L;
+    const bool last_lane = s.lane == 63;
+    double zl = (s.lane == 0) ? op.z_at(s.lb + (int64_t)r0 * 128 - 1) : 0.0;
+    double pz_m = 0.0, pz_c = 0.0, px = 0.0, pg = 0.0;  // lane 63: deferred element of the previous row
+    int64_t pi = 0, pe = 0;
+    bool pvalid = false;
+    for (int row = r0; row < r1; ++row) {
+        const int64_t o = (int64_t)row * 128 + 2 * s.lane;
+        typename Op::Row r;
+        op.load(r, s.lb + o);
+        const double zfirst = __shfl(r.z.x, 0, 64);
+        if (last_lane && row > r0 && pvalid) op.finish(pz_m, pz_c, zfirst, px, pg, park[s.w], pi, pe, acc);
+        r.zh = zl;  // lane 0's left neighbour; lane 63's right neighbour is deferred
+        const bool v0 = full || o < s.len;
+        const bool v1 = !last_lane && (full || o + 1 < s.len);
+        op.template apply<true>(r, s.lb + o, s.sbeg + o, v0, v1, acc);
+        if (last_lane) {
+            pz_m = r.z.x;
+            pz_c = r.z.y;
+            px = r.x.y;
+            pg = r.g.y;
+            op.park(r, park[s.w]);
+            pi = s.lb + o + 1;
+            pe = s.sbeg + o + 1;
+            pvalid = full || o + 1 < s.len;
+        }
+        zl = __shfl(r.z.y, 63, 64);
+    }
+    if (last_lane && pvalid) {
+        const double zp = op.z_at(s.lb + (int64_t)r1 * 128);
+        op.finish(pz_m, pz_c, zp, px, pg, park[s.w], pi, pe, acc);
     }
 }
 
@@ -970,7 +1047,7 @@ __global__ __launch_bounds__(LB_BLOCK) void k_vf_commit(OpVfCommit<OBJ, HB, NT> 
     double acc[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) acc[k] = 0.0;
-    stream1(op, s, geo, acc);
+    stream_vf(op, s, geo, acc);
     reduce_publish<K>(acc, geo, red);
 }
 

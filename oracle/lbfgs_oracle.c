@@ -105,9 +105,13 @@ static double tree_sum(double* a, int count) { /* balanced, natural order, in pl
     return a[0];
 }
 
-/* kind 0: dot of (a,b) with fma; kind 1: sum of a[] */
-static void canon_groups(const double* a, const double* b, int64_t n, int64_t limit, int kind,
-                         double* q8) {
+/* kind 0: dot of (a,b) with fma; kind 1: sum of a[].
+ * Row-to-wave assignment within a segment: rows r = 4u + w (the default order), or, for
+ * ORC_CANON_VF (the vector-free commit, lbfgs_kernels.hip stream_vf), contiguous runs: wave w
+ * takes rows [wR, min((w+1)R, nrow)), R = ceil(nrow / 4), nrow = rows of the segment's
+ * elements. Each lane accumulates its rows in ascending order either way. */
+static void canon_groups_mode(const double* a, const double* b, int64_t n, int64_t limit, int kind, int contig,
+                              double* q8) {
     int64_t L, nseg;
     orc_canon_geometry(n, &L, &nseg);
     double* segp = (double*)calloc(CANON_SEGS, sizeof(double));
@@ -115,12 +119,21 @@ static void canon_groups(const double* a, const double* b, int64_t n, int64_t li
     for (int64_t s = 0; s < nseg; ++s) {
         int64_t sbeg = s * L;
         int64_t send = sbeg + L < n ? sbeg + L : n;
+        const int64_t nrow = (send - sbeg + 127) / 128, R = (nrow + 3) / 4;
         if (send > limit) send = limit > sbeg ? limit : sbeg;
         for (int t = 0; t < 256; ++t) {
             int w = t >> 6, lane = t & 63;
             double v = 0.0;
-            for (int64_t u = 0; 128 * (4 * u + w) < L; ++u) { /* rows r = 4u + w of the segment */
-                int64_t base = sbeg + 128 * (4 * u + w) + 2 * lane;
+            for (int64_t u = 0;; ++u) {
+                int64_t row;
+                if (contig) {
+                    row = w * R + u;
+                    if (u >= R || row >= nrow) break;
+                } else {
+                    row = 4 * u + w; /* rows r = 4u + w of the segment */
+                    if (128 * row >= L) break;
+                }
+                int64_t base = sbeg + 128 * row + 2 * lane;
                 for (int k = 0; k < 2; ++k) {
                     int64_t e = base + k;
                     if (e < send) v = kind == 0 ? fma(a[e], b[e], v) : v + a[e];
@@ -134,6 +147,10 @@ static void canon_groups(const double* a, const double* b, int64_t n, int64_t li
     free(segp);
 }
 
+static void canon_groups(const double* a, const double* b, int64_t n, int64_t limit, int kind, double* q8) {
+    canon_groups_mode(a, b, n, limit, kind, 0, q8);
+}
+
 static double canon_total(const double* q8) {
     double t = q8[0];
     for (int g = 1; g < CANON_GROUPS; ++g) t = t + q8[g];
@@ -145,9 +162,9 @@ void orc_canon_dot_groups(const double* a, const double* b, int64_t n, double* q
 }
 
 double orc_dot(const double* a, const double* b, int64_t n, int mode) {
-    if (mode == ORC_CANON) {
+    if (mode == ORC_CANON || mode == ORC_CANON_VF) {
         double q8[CANON_GROUPS];
-        canon_groups(a, b, n, n, 0, q8);
+        canon_groups_mode(a, b, n, n, 0, mode == ORC_CANON_VF, q8);
         return canon_total(q8);
     }
     double sum = 0.; /* vector_utils.cpp:36-38 */
@@ -156,9 +173,9 @@ double orc_dot(const double* a, const double* b, int64_t n, int mode) {
 }
 
 double orc_sum(const double* t, int64_t n, int64_t limit, int mode) {
-    if (mode == ORC_CANON) {
+    if (mode == ORC_CANON || mode == ORC_CANON_VF) {
         double q8[CANON_GROUPS];
-        canon_groups(t, NULL, n, limit, 1, q8);
+        canon_groups_mode(t, NULL, n, limit, 1, mode == ORC_CANON_VF, q8);
         return canon_total(q8);
     }
     double sum = 0.0;
@@ -223,7 +240,7 @@ double orc_f(int obj, const double* x, int64_t n, int mode) {
     } else {
         for (int64_t i = 0; i < n; i++) t[i] = (x[i] - 1) * (x[i] - 1);
     }
-    return orc_sum(t, n, limit, ORC_CANON);
+    return orc_sum(t, n, limit, mode);
 }
 
 void orc_grad(int obj, const double* x, int64_t n, double* g) {
@@ -667,7 +684,8 @@ static int orc_lbfgs_vf(const orc_opts* o, const double* x0, double* x_out, doub
             const double at = pass == 0 ? o->initial_step : alpha;
             if (pass == 1 && at == o->initial_step) break;
             trial_point(x, d, at, n, xn);
-            fN = F(C, xn);
+            fN = orc_f(o->obj, xn, n, ORC_CANON_VF);
+            C->nf++;
             G(C, xn, gn);
             double* sk = S[free_pair];
             double* yk = Y[free_pair];
@@ -675,14 +693,14 @@ static int orc_lbfgs_vf(const orc_opts* o, const double* x0, double* x_out, doub
                 sk[i] = xn[i] - x[i];
                 yk[i] = gn[i] - g[i];
             }
-            sy = orc_dot(sk, yk, n, ORC_CANON);
-            yy = orc_dot(yk, yk, n, ORC_CANON);
-            ggN = orc_dot(gn, gn, n, ORC_CANON);
-            yg = orc_dot(yk, gn, n, ORC_CANON);
-            ggo = orc_dot(gn, g, n, ORC_CANON);
+            sy = orc_dot(sk, yk, n, ORC_CANON_VF);
+            yy = orc_dot(yk, yk, n, ORC_CANON_VF);
+            ggN = orc_dot(gn, gn, n, ORC_CANON_VF);
+            yg = orc_dot(yk, gn, n, ORC_CANON_VF);
+            ggo = orc_dot(gn, g, n, ORC_CANON_VF);
             for (int l = 0; l < 2 * h; ++l) {
-                YB[l] = orc_dot(yk, B[l], n, ORC_CANON);
-                GB[l] = orc_dot(gn, B[l], n, ORC_CANON);
+                YB[l] = orc_dot(yk, B[l], n, ORC_CANON_VF);
+                GB[l] = orc_dot(gn, B[l], n, ORC_CANON_VF);
             }
             if (pass == 0) {
                 double dgn = 0.0;
