@@ -240,27 +240,33 @@ __global__ __launch_bounds__(LB_BLOCK) void k_group_reduce(const double* __restr
     group_tree<K, false>(partials, gseg0 - geo.seg_lo, gseg0, geo.nseg, slot + g * kstride, lds);
 }
 
-// The same stage 2 for a runtime number of components (wide slots): identical arithmetic per
-// component as group_tree.
+// The same stage 2 for a runtime number of components (wide slots): blockIdx.y takes
+// components [8 y, 8 y + 8), all their partial loads issued before the first butterfly;
+// identical arithmetic per component as group_tree.
 __global__ __launch_bounds__(LB_BLOCK) void k_group_reduce_wide(const double* __restrict__ partials, Geo geo,
                                                                 double* __restrict__ slot, int K, int kstride) {
-    __shared__ double lds[4][LBK_KW];
+    constexpr int KC = 8;
+    __shared__ double lds[4][KC];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int g = geo.g_lo + (int)blockIdx.x;
+    const int k0 = KC * (int)blockIdx.y;
     const int64_t gseg0 = (int64_t)g * LBK_SEG_PER_GROUP;
     const int64_t lbase = gseg0 - geo.seg_lo;
-    for (int k = 0; k < K; ++k) {
-        double p[4];
+    double p[KC][4];
+#pragma unroll
+    for (int c = 0; c < KC; ++c)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int64_t j = 4 * t + i;
-            p[i] = (gseg0 + j < geo.nseg) ? partials[(int64_t)k * LBK_SEGS + lbase + j] : 0.0;
+            p[c][i] = (k0 + c < K && gseg0 + j < geo.nseg) ? partials[(int64_t)(k0 + c) * LBK_SEGS + lbase + j] : 0.0;
         }
-        const double q = wave_sum((p[0] + p[1]) + (p[2] + p[3]));
-        if (lane == 0) lds[w][k] = q;
+#pragma unroll
+    for (int c = 0; c < KC; ++c) {
+        const double q = wave_sum((p[c][0] + p[c][1]) + (p[c][2] + p[c][3]));
+        if (lane == 0) lds[w][c] = q;
     }
     __syncthreads();
-    for (int k = t; k < K; k += LB_BLOCK) slot[g * kstride + k] = (lds[0][k] + lds[1][k]) + (lds[2][k] + lds[3][k]);
+    if (t < KC && k0 + t < K) slot[g * kstride + k0 + t] = (lds[0][t] + lds[1][t]) + (lds[2][t] + lds[3][t]);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1368,7 +1374,8 @@ int launch(lbk_ctx* c, int kind, double vec_passes, int slot, F&& fn, int K = 1)
             case 2: hipLaunchKernelGGL(k_group_reduce<2>, grid, blk, 0, c->stream, c->partials, g, sl, ks); break;
             case 7: hipLaunchKernelGGL(k_group_reduce<7>, grid, blk, 0, c->stream, c->partials, g, sl, ks); break;
             default:
-                hipLaunchKernelGGL(k_group_reduce_wide, grid, blk, 0, c->stream, c->partials, g, sl, K, ks);
+                hipLaunchKernelGGL(k_group_reduce_wide, dim3(c->geo.g_hi - c->geo.g_lo, (K + 7) / 8), blk, 0, c->stream,
+                                   c->partials, g, sl, K, ks);
                 break;
         }
         HIPCHK(c, hipGetLastError());
