@@ -24,7 +24,11 @@ extern "C" {
 
 /* wide result slots (vector-free mode: 4h + 6 components): ids LBK_WSLOT0 + w */
 #define LBK_VF_HMAX 20
-#define LBK_KW (4 * LBK_VF_HMAX + 8)
+#define LBK_KW (4 * LBK_VF_HMAX + 16)
+/* sharded vector-free: the rank's first / last element of x, g, s, y ride the wide slot's
+ * spare components (group g_lo / g_hi - 1) into the neighbours' ghost cells */
+#define LBK_VF_EDGE0 (LBK_KW - 8)
+#define LBK_VF_EDGE1 (LBK_KW - 4)
 #define LBK_WSLOT (LBK_GROUPS * LBK_KW)
 #define LBK_NWSLOTS 4
 #define LBK_WSLOT0 LBK_NSLOTS
@@ -135,6 +139,8 @@ int lbk_vf_commit(lbk_ctx* c, int obj, int h, const double* x, const double* g, 
 int lbk_vf_dir(lbk_ctx* c, int h, double* d, const double* g, const double* const* S, const double* const* Y,
                const double* cs, const double* cy, double cg);
 int lbk_vf_bucket(int h);
+/* sharded vector-free: fill the ghost cells of x and g from the neighbours (solver start) */
+int lbk_vf_ghost_init(lbk_ctx* c, double* x, double* g, int wslot);
 
 /* unfused mode: out = op(a, b) with device-side coefficients (see k_update) */
 enum { LBK_U_AXPY_Q = 0, LBK_U_AXPY_R, LBK_U_SCALE, LBK_U_NEG, LBK_U_SUB, LBK_U_POINT };

@@ -360,7 +360,8 @@ static int materialize_d(lbfgs_ctx* c) {
     } else if (c->dmode == LBK_D_NEG_G) {
         DEV(lbk_negdot(c->dev, c->d, c->g, SLOT_LAST(m)));
     }
-    lbk_set_ghost_slot(c->dev, SLOT_LAST(m)); /* sharded: neighbours' edge d rides this slot */
+    /* sharded: neighbours' edge d rides this slot (vector-free: d's ghost cells hold it) */
+    lbk_set_ghost_slot(c->dev, c->dmode == D_VF ? -1 : SLOT_LAST(m));
     c->dmode = LBK_D_BUF;
     c->d_ready = 1;
     return 0;
@@ -1036,8 +1037,7 @@ int lbfgs_solver_init(lbfgs_ctx* c, int objective, const lbfgs_host_fn* cb, int 
     if (c->unfused && (objective == LBFGS_OBJ_HOST || c->geo->world != 1)) return LBFGS_ERR_BAD_ARG;
     c->vf = (flags & LBFGS_FLAG_VECTOR_FREE) != 0;
     if (c->vf) {
-        if (c->unfused || objective == LBFGS_OBJ_HOST || c->geo->world != 1 || c->m > LBK_VF_HMAX)
-            return LBFGS_ERR_BAD_ARG;
+        if (c->unfused || objective == LBFGS_OBJ_HOST || c->m > LBK_VF_HMAX) return LBFGS_ERR_BAD_ARG;
         const size_t P = (size_t)c->m + 1;
         if (!c->Gss) {
             c->Gss = (double*)calloc(P * P, sizeof(double));
@@ -1080,6 +1080,7 @@ int lbfgs_solver_init(lbfgs_ctx* c, int objective, const lbfgs_host_fn* cb, int 
         DEVNC(lbk_fetch(c->dev, SLOT_INIT, 2, t));
         c->f_cur = t[0];
         c->gg = t[1];
+        if (c->vf) DEVNC(lbk_vf_ghost_init(c->dev, c->x, c->g, LBK_WSLOT0));
     }
     c->inited = 1;
     return 0;

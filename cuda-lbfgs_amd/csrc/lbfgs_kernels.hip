@@ -1090,6 +1090,35 @@ __global__ __launch_bounds__(256) void k_vf_dir(double* __restrict__ d, const do
         stv<NT>(d + i, v);
     }
     if ((n_loc & 1) && blockIdx.x == 0 && threadIdx.x == 0) d[n_loc - 1] = vf_dir1<HB>(B, g, n_loc - 1);
+    if (blockIdx.x == 0 && threadIdx.x == 1) {  // ghost cells (sharded: the neighbours' d, from basis ghosts)
+        d[-1] = vf_dir1<HB>(B, g, -1);
+        d[n_loc] = vf_dir1<HB>(B, g, n_loc);
+    }
+}
+
+// sharded vector-free: publish this rank's edge values of x, g, s, y (s, y may be null) into the
+// wide slot's spare components, to be all-gathered with the reductions
+__global__ void k_vf_edges(double* __restrict__ slot, const double* __restrict__ x, const double* __restrict__ g,
+                           const double* __restrict__ s, const double* __restrict__ y, int64_t n_loc, int g_lo,
+                           int g_hi) {
+    if (threadIdx.x != 0) return;
+    const double* v[4] = {x, g, s, y};
+    for (int k = 0; k < 4; ++k) {
+        slot[g_lo * LBK_KW + LBK_VF_EDGE0 + k] = v[k] ? v[k][0] : 0.0;
+        slot[(g_hi - 1) * LBK_KW + LBK_VF_EDGE1 + k] = v[k] ? v[k][n_loc - 1] : 0.0;
+    }
+}
+
+// ... and after the all-gather, the neighbours' edges into this rank's ghost cells
+__global__ void k_vf_ghosts(const double* __restrict__ slot, double* x, double* g, double* s, double* y, int64_t n_loc,
+                            int g_lo, int g_hi, int has_left, int has_right) {
+    if (threadIdx.x != 0) return;
+    double* v[4] = {x, g, s, y};
+    for (int k = 0; k < 4; ++k) {
+        if (!v[k]) continue;
+        if (has_left) v[k][-1] = slot[(g_lo - 1) * LBK_KW + LBK_VF_EDGE1 + k];
+        if (has_right) v[k][n_loc] = slot[g_hi * LBK_KW + LBK_VF_EDGE0 + k];
+    }
 }
 
 // z = x + alpha d over the whole local range incl. ghosts (host-callback objectives)
@@ -1350,7 +1379,7 @@ int exchange_slot(lbk_ctx* c, int slot) {
 
 // launch wrapper: byte accounting, optional event timing, all-gather of group partials
 template <class F>
-int launch(lbk_ctx* c, int kind, double vec_passes, int slot, F&& fn, int K = 1) {
+int launch(lbk_ctx* c, int kind, double vec_passes, int slot, F&& fn, int K = 1, bool exchange = true) {
     const double bytes = vec_passes * 8.0 * (double)c->geo.n_loc;
     c->bytes_total += bytes;
     hipEvent_t a = nullptr, b = nullptr;
@@ -1384,7 +1413,22 @@ int launch(lbk_ctx* c, int kind, double vec_passes, int slot, F&& fn, int K = 1)
         HIPCHK(c, hipEventRecord(b, c->stream));
         c->pending.push_back({kind, a, b, bytes});
     }
-    if (c->geo.world > 1 && slot >= 0) return exchange_slot(c, slot);
+    if (exchange && c->geo.world > 1 && slot >= 0) return exchange_slot(c, slot);
+    return 0;
+}
+
+// sharded vector-free: edges of (x, g, s, y) into the slot, all-gather, neighbours' edges into
+// the ghost cells
+int vf_exchange_ghosts(lbk_ctx* c, int wslot, double* x, double* g, double* s, double* y) {
+    double* sl = slot_base(c, wslot);
+    const lbk_geo& G = c->geo;
+    hipLaunchKernelGGL(k_vf_edges, dim3(1), dim3(64), 0, c->stream, sl, x, g, s, y, G.n_loc, G.g_lo, G.g_hi);
+    HIPCHK(c, hipGetLastError());
+    const int rc = exchange_slot(c, wslot);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_vf_ghosts, dim3(1), dim3(64), 0, c->stream, sl, x, g, s, y, G.n_loc, G.g_lo, G.g_hi,
+                       G.elem_lo > 0 ? 1 : 0, G.elem_lo + G.n_loc < G.n ? 1 : 0);
+    HIPCHK(c, hipGetLastError());
     return 0;
 }
 
@@ -1754,13 +1798,15 @@ int vf_commit_hb(lbk_ctx* c, int obj, int h, const double* x, const double* g, c
     Red r = kred(c, wslot);
     const VfBasis<HB> B = vf_basis<HB>(h, S, Y, cs, cy, cg);
     constexpr int K = LBK_VF_YB + 4 * HB;
-    return launch(c, LBK_K_VF_COMMIT, 2.0 * h + 6.0, wslot, [&] {
+    const int rc = launch(c, LBK_K_VF_COMMIT, 2.0 * h + 6.0, wslot, [&] {
         OBJ_DISPATCH(obj, {
             OpVfCommit<O_, HB, NT_> op{x, g, B, alpha, xn, gn, so, yo, geo.n, geo.n_loc};
             hipLaunchKernelGGL((k_vf_commit<O_, HB, NT_>), dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, op, geo, r);
         });
         return 0;
-    }, K);
+    }, K, false);
+    if (rc || c->geo.world == 1) return rc;
+    return vf_exchange_ghosts(c, wslot, xn, gn, so, yo);
 }
 
 template <int HB>
@@ -1780,6 +1826,11 @@ extern "C" {
 
 #define VF_BUCKETS(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(8) X(10) X(12) X(16) X(20)
 
+int lbk_vf_ghost_init(lbk_ctx* c, double* x, double* g, int wslot) {
+    if (c->geo.world == 1) return 0;
+    return vf_exchange_ghosts(c, wslot, x, g, nullptr, nullptr);
+}
+
 int lbk_vf_bucket(int h) {
     static const int hb[] = {0, 1, 2, 3, 4, 5, 6, 8, 10, 12, 16, 20};
     for (int v : hb)
@@ -1791,9 +1842,8 @@ int lbk_vf_commit(lbk_ctx* c, int obj, int h, const double* x, const double* g, 
                   const double* const* Y, const double* cs, const double* cy, double cg, double alpha,
                   double* xn, double* gn, double* so, double* yo, int wslot, int* hb_out) {
     const int hb = lbk_vf_bucket(h);
-    if (hb < 0 || wslot < LBK_WSLOT0 || wslot >= LBK_WSLOT0 + LBK_NWSLOTS || c->geo.world != 1) {
-        snprintf(c->err, sizeof c->err, "lbk_vf_commit: h=%d (max %d), slot %d, world %d", h, LBK_VF_HMAX, wslot,
-                 c->geo.world);
+    if (hb < 0 || wslot < LBK_WSLOT0 || wslot >= LBK_WSLOT0 + LBK_NWSLOTS) {
+        snprintf(c->err, sizeof c->err, "lbk_vf_commit: h=%d (max %d), slot %d", h, LBK_VF_HMAX, wslot);
         return -1;
     }
     *hb_out = hb;
@@ -1809,7 +1859,7 @@ int lbk_vf_commit(lbk_ctx* c, int obj, int h, const double* x, const double* g, 
 int lbk_vf_dir(lbk_ctx* c, int h, double* d, const double* g, const double* const* S, const double* const* Y,
                const double* cs, const double* cy, double cg) {
     const int hb = lbk_vf_bucket(h);
-    if (hb < 0 || c->geo.world != 1) return -1;
+    if (hb < 0) return -1;
     switch (hb) {
 #define VF_CASE(HB) \
     case HB: return vf_dir_hb<HB>(c, h, d, g, S, Y, cs, cy, cg);

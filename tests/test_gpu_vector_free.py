@@ -102,7 +102,7 @@ def test_vector_free_nontemporal_bit_exact(monkeypatch):
 
 
 def test_vector_free_rejects_unsupported():
-    with L.Context(100, 3) as c:
+    with L.Context(100, 3) as c:  # host callbacks, unfused + vector-free, m > 20
         with pytest.raises(L.LbfgsError):
             c.minimize("host", np.zeros(100), "backtracking", 5, f=lambda x: 0.0, grad=lambda x: x,
                        vector_free=True)
@@ -111,3 +111,48 @@ def test_vector_free_rejects_unsupported():
     with L.Context(100, 21) as c:
         with pytest.raises(L.LbfgsError):
             c.minimize("rosenbrock", np.zeros(100), "backtracking", 5, vector_free=True)
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+@pytest.mark.parametrize("obj,ls", [("rosenbrock", "backtracking"), ("rosenbrock", "wolfe"),
+                                    ("quad_tridiag", "wolfe")])
+def test_vector_free_sharded_emulated_bit_exact(world, obj, ls):
+    """Sharded vector-free mode (one wide all-gather per commit carrying the reductions and the
+    ranks' edge values of x, g, s, y into the neighbours' ghost cells) with `world` emulated
+    ranks on this GPU gives the single-GPU trajectory bit for bit."""
+    import threading
+
+    n = 4_000_003
+    m, iters = 5, 12
+    x0 = L.x0_uniform(n, 42, -2.0, 2.0)
+    with L.Context(n, m) as c:
+        ref = c.minimize(obj, x0, ls, iters, trace=True, vector_free=True)
+    grp = L.HostGroup(world)
+    ctxs = [L.Context(n, m, rank=r, group=grp) for r in range(world)]
+    out = [None] * world
+    err = [None] * world
+
+    def run(r):
+        try:
+            out[r] = ctxs[r].minimize(obj, x0, ls, iters, trace=True, vector_free=True)
+        except Exception as e:  # pragma: no cover
+            err[r] = e
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=600)
+    assert not any(err), err
+    x = np.zeros(n)
+    for r in range(world):
+        o = out[r]
+        for key in ["tr_f", "tr_gnorm", "tr_alpha"]:
+            assert np.array_equal(bits(o[key]), bits(ref[key])), (r, key)
+        assert np.array_equal(o["tr_c1"], ref["tr_c1"]) and np.array_equal(o["tr_c2"], ref["tr_c2"])
+        lo, nl = ctxs[r].elem_lo, ctxs[r].n_loc
+        x[lo:lo + nl] = o["x"][lo:lo + nl]
+    assert np.array_equal(bits(x), bits(ref["x"]))
+    for c in ctxs:
+        c.close()
+    grp.close()
