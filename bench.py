@@ -221,11 +221,12 @@ def main():
     dev = D.local_rank % int(os.environ["BENCH_DEVICE_MOD"]) if "BENCH_DEVICE_MOD" in os.environ else D.local_rank
     T, res, prof, bytes_all, done_steps = measure(a, D, n, x0, dev, rank, world, uid,
                                                   unfused=a.unfused, vector_free=a.vector_free)
-    # the opt-in vector-free mode alongside the default (one GPU; outside the bit-parity
-    # contract with the reference's operation order)
+    # the opt-in vector-free mode alongside the default (outside the bit-parity contract with
+    # the reference's operation order); sharded runs need a fresh RCCL id
     vf = None
-    if world == 1 and not (a.unfused or a.vector_free or a.no_vector_free) and a.history <= 20:
-        Tv, rv, pv, bv, dv = measure(a, D, n, x0, dev, rank, world, uid, vector_free=True)
+    if not (a.unfused or a.vector_free or a.no_vector_free) and a.history <= 20:
+        uid2 = D.broadcast_bytes(L.unique_id() if rank == 0 else None) if world > 1 else None
+        Tv, rv, pv, bv, dv = measure(a, D, n, x0, dev, rank, world, uid2, vector_free=True)
         vf = dict(value=round(dv / Tv, 4), ms_per_step=round(Tv / dv * 1e3, 4), steps=dv,
                   achieved_hbm_gbps=round(bv / Tv / 1e9, 1), roofline=roofline(pv, n, world),
                   solver={"status": rv["status"], "f": rv["f"], "gnorm": rv["gnorm"],
