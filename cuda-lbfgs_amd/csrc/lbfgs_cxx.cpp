@@ -229,8 +229,16 @@ vector<double> run(const FnF& f, const FnG& grad, const vector<double>& x0, int 
     lbfgs_host_fn cb{host_f, host_g, &hf};
     vector<double> x(n);
     lbfgs_result res;
+    // execution mode (include/lbfgs_hip.h flags): LBFGS_MODE=vector_free | unfused; the
+    // vector-free mode needs a device objective and m <= 20, else the default mode runs
+    unsigned flags = verbose ? LBFGS_FLAG_VERBOSE : 0u;
+    if (const char* mode = std::getenv("LBFGS_MODE")) {
+        const std::string md(mode);
+        if (md == "vector_free" && obj != LBFGS_OBJ_HOST && m <= 20) flags |= LBFGS_FLAG_VECTOR_FREE;
+        else if (md == "unfused" && obj != LBFGS_OBJ_HOST) flags |= LBFGS_FLAG_UNFUSED;
+    }
     int rc = lbfgs_minimize(c, obj, obj == LBFGS_OBJ_HOST ? &cb : nullptr, ls, &k, x0.data(), x.data(),
-                            max_iterations, tolerance, verbose ? LBFGS_FLAG_VERBOSE : 0u, &res);
+                            max_iterations, tolerance, flags, &res);
     if (!hf.error.empty()) throw std::runtime_error("objective callback failed: " + hf.error);
     if (rc < 0) throw std::runtime_error(std::string("LBFGS failed: ") + lbfgs_last_error(c));
     return x;
