@@ -76,3 +76,20 @@ def test_cxx_dropin_on_gpu(tmp_path):
     assert _ck(k["x_cuda_bt"]) == O.checksum(ob["x"])
     assert _fx(k["C2"]) == 0.9
     assert "Maximum iterations reached" in r.stdout and "Converged!" in r.stdout
+
+
+@pytest.mark.gpu
+def test_cxx_dropin_vector_free_mode(tmp_path):
+    """LBFGS_MODE=vector_free: the unchanged reference-style caller runs the vector-free mode for
+    its device objectives (bit-exact with the oracle's restatement) and the default mode for its
+    host-callback objective."""
+    exe = _build(str(tmp_path))
+    env = dict(os.environ, LBFGS_MODE="vector_free")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr
+    k = _parse(r.stdout)
+    x0 = O.x0_uniform(2000, 42, -2.0, 2.0)
+    o = O.lbfgs("rosenbrock", x0, "backtracking", 5, 30, 1e-5, mode=O.CANON, vector_free=True)
+    assert _ck(k["x_device"]) == O.checksum(o["x"])
+    oq = O.lbfgs("quad_tridiag", x0, "wolfe", 20, 1000, 1e-5, mode=O.CANON, vector_free=True)
+    assert _ck(k["x_qtri"]) == O.checksum(oq["x"])
