@@ -107,6 +107,32 @@ def test_twoloop_bit_exact(h, n):
     assert bits([gd])[0] == bits([gdref])[0]
 
 
+@pytest.mark.parametrize("k", [10, 30, 60])
+def test_one_step_from_reference_state(k):
+    """SURVEY 8c parity item 3: one L-BFGS step from the reference's own state. The sequential
+    oracle (bit-exact with the reference, tests/test_oracle_golden.py) gives x_j for
+    j = k-m .. k+1 of Rosenbrock n=1e4, m=5, backtracking, hence g_j, s_j, y_j exactly as the
+    reference holds them; the device two-loop from (g_k, s, y) with the reference's accepted
+    step gives x_{k+1} within 1e-12 relative (norm-wise; elementwise is meaningless for
+    components near 0) of the reference's x_{k+1}, and the step itself within 1e-12. Measured
+    on CPU with the canonical restatement: 6e-16 and 6e-15."""
+    n, m = 10_000, 5
+    x0 = O.x0_uniform(n, 42, -2.0, 2.0)
+    xs = {j: O.lbfgs("rosenbrock", x0, "backtracking", m, j, 1e-5, mode=O.SEQ)["x"]
+          for j in range(k - m, k + 2)}
+    run = O.lbfgs("rosenbrock", x0, "backtracking", m, k + 1, 1e-5, mode=O.SEQ)
+    assert "Skipping" not in run["messages"]  # the ring holds the last m pairs
+    gs = {j: O.grad("rosenbrock", xs[j]) for j in xs}
+    S = [xs[j + 1] - xs[j] for j in range(k - m, k)]
+    Y = [gs[j + 1] - gs[j] for j in range(k - m, k)]
+    d, _ = ctx(n, m).twoloop(gs[k], S, Y)
+    alpha = run["alpha"][k]
+    x1 = xs[k] + alpha * d
+    assert np.linalg.norm(x1 - xs[k + 1]) <= 1e-12 * np.linalg.norm(xs[k + 1])
+    step = xs[k + 1] - xs[k]
+    assert np.linalg.norm(alpha * d - step) <= 1e-12 * np.linalg.norm(step)
+
+
 def _run_gpu(meta):
     n = meta["n"]
     x0 = L.x0_uniform(n, meta["seed"], meta["lo"], meta["hi"])
