@@ -28,10 +28,10 @@ L.lib()
 import numpy as np  # noqa: E402
 
 
-def timed_steps(n, m, obj, ls, warm, steps, tol=1e-5, unfused=False):
+def timed_steps(n, m, obj, ls, warm, steps, tol=1e-5, unfused=False, vector_free=False):
     x0 = L.x0_uniform(n, 42, -2.0, 2.0)
     with L.Context(n, m) as c:
-        c.init(obj, x0, ls, tolerance=tol, unfused=unfused)
+        c.init(obj, x0, ls, tolerance=tol, unfused=unfused, vector_free=vector_free)
         del x0
         c.step(warm)
         c.sync()
@@ -40,19 +40,21 @@ def timed_steps(n, m, obj, ls, warm, steps, tol=1e-5, unfused=False):
         c.sync()
         dt = time.perf_counter() - t0
     done = steps if r["status"] == "running" else max(r["iterations"] - warm, 1)
-    return dict(n=n, m=m, objective=obj, line_search=ls, kernels="unfused" if unfused else "fused",
+    return dict(n=n, m=m, objective=obj, line_search=ls,
+                kernels="unfused" if unfused else "vector_free" if vector_free else "fused",
                 warmup=warm, steps=done, seconds=dt,
                 iters_per_s=done / dt, ms_per_iter=1e3 * dt / done, gbps=r["bytes"] / dt / 1e9,
                 status=r["status"], f=r["f"], gnorm=r["gnorm"])
 
 
-def to_solution(n, m, obj, ls, maxit, tol=1e-5):
+def to_solution(n, m, obj, ls, maxit, tol=1e-5, vector_free=False):
     x0 = L.x0_uniform(n, 42, -2.0, 2.0)
     with L.Context(n, m) as c:
         t0 = time.perf_counter()
-        r = c.minimize(obj, x0, ls, maxit, tolerance=tol)
+        r = c.minimize(obj, x0, ls, maxit, tolerance=tol, vector_free=vector_free)
         dt = time.perf_counter() - t0
-    return dict(n=n, m=m, objective=obj, line_search=ls, seconds=dt, iterations=r["iterations"],
+    return dict(n=n, m=m, objective=obj, line_search=ls, kernels="vector_free" if vector_free else "fused",
+                seconds=dt, iterations=r["iterations"],
                 status=r["status"], f=r["f"], gnorm=r["gnorm"], trials_f=r["trials_f"],
                 trials_fg=r["trials_fg"], gbps=r["bytes"] / dt / 1e9,
                 note="includes x0 upload and result download")
@@ -72,9 +74,25 @@ def cpu_reference(n, m, iters):
                 kind="reference (oracle/_ref, 1 core)")
 
 
+def put(res, key, val):
+    res[key] = val
+    print(key, json.dumps(val), flush=True)
+
+
 def main():
     out = sys.argv[1] if len(sys.argv) > 1 and not sys.argv[1].startswith("--") else None
     res = {}
+    put(res, "config0_rosen_1e4_m5_bt_vector_free", timed_steps(10**4, 5, "rosenbrock", "backtracking", 0, 1000,
+                                                                vector_free=True))
+    put(res, "config1_rosen_1e7_m10_vector_free", timed_steps(10**7, 10, "rosenbrock", "backtracking", 20, 200,
+                                                              vector_free=True))
+    put(res, "config2_rosen_1e8_m10_vector_free", timed_steps(10**8, 10, "rosenbrock", "backtracking", 20, 100,
+                                                              vector_free=True))
+    put(res, "config3_qtri_1e8_m20_wolfe_vector_free", to_solution(10**8, 20, "quad_tridiag", "wolfe", 1000,
+                                                                   vector_free=True))
+    if "--skip-1e9" not in sys.argv:
+        put(res, "config4_rosen_1e9_m10_single_gpu_vector_free",
+            timed_steps(10**9, 10, "rosenbrock", "backtracking", 5, 10, vector_free=True))
     res["config0_rosen_1e4_m5_bt"] = dict(gpu=timed_steps(10**4, 5, "rosenbrock", "backtracking", 0, 1000),
                                           cpu=cpu_reference(10**4, 5, 1000))
     print(json.dumps(res["config0_rosen_1e4_m5_bt"]), flush=True)
