@@ -114,7 +114,7 @@ int lbk_axpy_dot(lbk_ctx* c, double* qout, const double* qin, const double* y, c
                  double rho, int ref_alpha, int slot);
 int lbk_mid(lbk_ctx* c, double* rout, const double* qin, const double* y0, double rho0,
             double gamma, int ref_alpha, int slot);
-int lbk_axpy2_dot(lbk_ctx* c, double* r, const double* s, const double* ynext, double rho,
+int lbk_axpy2_dot(lbk_ctx* c, double* r, const double* rin, const double* s, const double* ynext, double rho,
                   int ref_beta, int ref_alpha, int slot);
 int lbk_last(lbk_ctx* c, double* dout, const double* r, const double* s, const double* g,
              double rho, int ref_beta, int ref_alpha, int slot);

@@ -52,6 +52,9 @@ struct lbfgs_ctx {
     int m;
     /* device vectors */
     double *x, *g, *xn, *gn, *d, *q, *r, *gt;
+    double *q2, *r2;    /* ping-pong partners of q and r (two-loop passes write out of place) */
+    const double* rc;   /* the r the last two-loop pass wrote */
+    int pingpong;
     double* S[MMAX + 1];
     double* Y[MMAX + 1];
     /* history: ring[0] oldest .. ring[h-1] newest, indices into the m+1 pair pool */
@@ -189,7 +192,7 @@ void lbfgs_constants_cuda(lbfgs_constants* k) { /* parallel-implementation/const
 int lbfgs_unique_id(void* out128) { return lbk_unique_id(out128) == 0 ? 0 : LBFGS_ERR_RCCL; }
 
 static void free_vectors(lbfgs_ctx* c) {
-    double** v[] = {&c->x, &c->g, &c->xn, &c->gn, &c->d, &c->q, &c->r, &c->gt};
+    double** v[] = {&c->x, &c->g, &c->xn, &c->gn, &c->d, &c->q, &c->r, &c->gt, &c->q2, &c->r2};
     for (size_t i = 0; i < sizeof v / sizeof v[0]; ++i) {
         lbk_vec_free(c->dev, *v[i]);
         *v[i] = NULL;
@@ -350,7 +353,7 @@ static int materialize_d(lbfgs_ctx* c) {
     if (c->d_ready) return 0;
     const int m = c->m;
     if (c->dmode == LBK_D_TWOLOOP) {
-        DEV(lbk_last(c->dev, c->d, c->r, c->S[c->s_last_pair], c->g, c->rho_last, c->ref_b_last,
+        DEV(lbk_last(c->dev, c->d, c->rc, c->S[c->s_last_pair], c->g, c->rho_last, c->ref_b_last,
                      c->ref_a_last, SLOT_LAST(m)));
     } else if (c->dmode == D_VF) {
         DEV(lbk_vf_dir(c->dev, c->vf_h, c->d, c->g, c->vf_S, c->vf_Y, c->vf_cs, c->vf_cy, c->vf_cg));
@@ -591,7 +594,7 @@ static int twoloop_unfused(lbfgs_ctx* c, const double* rho, double gamma) {
 static int commit(lbfgs_ctx* c, int dmode, double alpha, int cslot, double* tot) {
     if (c->unfused) return commit_unfused(c, alpha, tot);
     const int pair = c->free_pair;
-    const double* dsrc = dmode == LBK_D_BUF ? c->d : c->r;
+    const double* dsrc = dmode == LBK_D_BUF ? c->d : c->rc;
     const double* s_last = dmode == LBK_D_TWOLOOP ? c->S[c->s_last_pair] : NULL;
     int obj = c->obj;
     if (c->obj == LBFGS_OBJ_HOST) {
@@ -676,20 +679,33 @@ static int iterate(lbfgs_ctx* c) {
                 DEV(lbk_dot(c->dev, c->S[top], c->g, SLOT_P0));
                 refA[h - 1] = REF(SLOT_P0, 0);
             }
+            /* q and r ping-pong between two buffers when c->pingpong: every pass writes a
+             * different vector than it reads (same values; measured faster) */
             const double* qsrc = c->g;
+            double* qb[2] = {c->q, c->pingpong ? c->q2 : c->q};
+            int qi = 0;
             for (int i = h - 2; i >= 0; --i) {
-                DEV(lbk_axpy_dot(c->dev, c->q, qsrc, c->Y[c->ring[i + 1]], c->S[c->ring[i]], rho[i + 1],
+                double* qout = qb[qi];
+                qi ^= 1;
+                DEV(lbk_axpy_dot(c->dev, qout, qsrc, c->Y[c->ring[i + 1]], c->S[c->ring[i]], rho[i + 1],
                                  refA[i + 1], SLOT_A0 + i));
                 refA[i] = REF(SLOT_A0 + i, 0);
-                qsrc = c->q;
+                qsrc = qout;
             }
             DEV(lbk_mid(c->dev, c->r, qsrc, c->Y[c->ring[0]], rho[0], gamma, refA[0], SLOT_B0(m)));
             refB[0] = REF(SLOT_B0(m), 0);
+            double* rb[2] = {c->r, c->pingpong ? c->r2 : c->r};
+            int ri = 1;
+            const double* rcur = c->r;
             for (int i = 0; i + 1 < h; ++i) {
-                DEV(lbk_axpy2_dot(c->dev, c->r, c->S[c->ring[i]], c->Y[c->ring[i + 1]], rho[i], refB[i],
+                double* rout = rb[ri];
+                ri ^= 1;
+                DEV(lbk_axpy2_dot(c->dev, rout, rcur, c->S[c->ring[i]], c->Y[c->ring[i + 1]], rho[i], refB[i],
                                   refA[i], SLOT_B0(m) + i + 1));
                 refB[i + 1] = REF(SLOT_B0(m) + i + 1, 0);
+                rcur = rout;
             }
+            c->rc = rcur;
             c->rho_last = rho[h - 1];
             c->ref_b_last = refB[h - 1];
             c->ref_a_last = refA[h - 1];
@@ -1035,6 +1051,18 @@ int lbfgs_solver_init(lbfgs_ctx* c, int objective, const lbfgs_host_fn* cb, int 
     }
     c->unfused = (flags & LBFGS_FLAG_UNFUSED) != 0;
     if (c->unfused && (objective == LBFGS_OBJ_HOST || c->geo->world != 1)) return LBFGS_ERR_BAD_ARG;
+    /* ping-pong q/r (LBFGS_PINGPONG=1): measured neutral at n=1e8 and -8 % at n=1e7 (the
+     * in-place passes keep q/r in the Infinity Cache), so in-place is the default */
+    c->pingpong = 0;
+    {
+        const char* e = getenv("LBFGS_PINGPONG");
+        if (e) c->pingpong = atoi(e) != 0;
+    }
+    if (c->pingpong && !c->q2) {
+        c->q2 = lbk_vec_alloc(c->dev);
+        c->r2 = lbk_vec_alloc(c->dev);
+        if (!c->q2 || !c->r2) return LBFGS_ERR_NOMEM;
+    }
     c->vf = (flags & LBFGS_FLAG_VECTOR_FREE) != 0;
     if (c->vf) {
         if (c->unfused || objective == LBFGS_OBJ_HOST || c->m > LBK_VF_HMAX) return LBFGS_ERR_BAD_ARG;
@@ -1252,7 +1280,7 @@ int lbfgs_dev_twoloop(lbfgs_ctx* c, const double* g, const double* const* S, con
     DEV(lbk_mid(c->dev, c->r, qsrc, c->Y[0], rho[0], gamma, refA[0], SLOT_B0(m)));
     refB[0] = REF(SLOT_B0(m), 0);
     for (int i = 0; i + 1 < h; ++i) {
-        DEV(lbk_axpy2_dot(c->dev, c->r, c->S[i], c->Y[i + 1], rho[i], refB[i], refA[i], SLOT_B0(m) + i + 1));
+        DEV(lbk_axpy2_dot(c->dev, c->r, c->r, c->S[i], c->Y[i + 1], rho[i], refB[i], refA[i], SLOT_B0(m) + i + 1));
         refB[i + 1] = REF(SLOT_B0(m) + i + 1, 0);
     }
     DEV(lbk_last(c->dev, c->d, c->r, c->S[h - 1], c->g, rho[h - 1], refB[h - 1], refA[h - 1], SLOT_LAST(m)));

@@ -501,7 +501,8 @@ struct OpMid {  // r = (qin - alpha0 y0) * gamma;  acc += y0 . r      (:134-137,
 
 template <bool NT>
 struct OpAxpy2Dot {  // r += s (alpha - beta);  acc += ynext . r      (:159-164)
-    double* r;
+    double* r;        // out (== rin in place, or the other buffer of a ping-pong pair)
+    const double* rin;
     const double* __restrict__ s;
     const double* __restrict__ yn;
     double coef;
@@ -509,7 +510,7 @@ struct OpAxpy2Dot {  // r += s (alpha - beta);  acc += ynext . r      (:159-164)
         double2 r, s, y;
     };
     __device__ void load(Row& w, int64_t i) const {
-        w.r = ldv<NT>(r + i);
+        w.r = ldv<NT>(rin + i);
         w.s = ldv<NT>(s + i);
         w.y = ldv<NT>(yn + i);
     }
@@ -620,13 +621,13 @@ __global__ __launch_bounds__(LB_BLOCK) void k_mid(double* __restrict__ rout, con
 
 // beta = rho * total(pb), alpha = rho * total(pa)
 template <bool NT>
-__global__ __launch_bounds__(LB_BLOCK) void k_axpy2_dot(double* r, const double* __restrict__ sv,
+__global__ __launch_bounds__(LB_BLOCK) void k_axpy2_dot(double* r, const double* rin, const double* __restrict__ sv,
                                                         const double* __restrict__ yn, double rho,
                                                         const double* __restrict__ pb, const double* __restrict__ pa,
                                                         Geo geo, Red red) {
     const double beta = rho * slot_total(pb);
     const double alpha = rho * slot_total(pa);
-    run_pass<OpAxpy2Dot<NT>, 1>(OpAxpy2Dot<NT>{r, sv, yn, alpha - beta}, geo, red);
+    run_pass<OpAxpy2Dot<NT>, 1>(OpAxpy2Dot<NT>{r, rin, sv, yn, alpha - beta}, geo, red);
 }
 
 template <bool NT>
@@ -1643,14 +1644,14 @@ int lbk_mid(lbk_ctx* c, double* rout, const double* qin, const double* y0, doubl
     });
 }
 
-int lbk_axpy2_dot(lbk_ctx* c, double* rr, const double* s, const double* ynext, double rho, int ref_beta,
-                  int ref_alpha, int slot) {
+int lbk_axpy2_dot(lbk_ctx* c, double* rr, const double* rin, const double* s, const double* ynext, double rho,
+                  int ref_beta, int ref_alpha, int slot) {
     Geo g = kgeo(c);
     Red r = kred(c, slot);
     const double* pb = sref(c, ref_beta);
     const double* pa = sref(c, ref_alpha);
     return launch(c, LBK_K_AXPY2_DOT, 4, slot, [&] {
-        NT_DISPATCH(c, hipLaunchKernelGGL(k_axpy2_dot<NT_>, dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, rr, s, ynext, rho, pb, pa, g, r));
+        NT_DISPATCH(c, hipLaunchKernelGGL(k_axpy2_dot<NT_>, dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, rr, rin, s, ynext, rho, pb, pa, g, r));
     });
 }
 
