@@ -156,3 +156,18 @@ def test_vector_free_sharded_emulated_bit_exact(world, obj, ls):
     for c in ctxs:
         c.close()
     grp.close()
+
+
+@pytest.mark.parametrize("m,ls", [(20, "backtracking"), (14, "wolfe"), (16, "interpolation")])
+def test_vector_free_large_history_buckets(m, ls):
+    """h grows to m over the run, so every register bucket up to 20 (12, 16, 20: the
+    AGPR-spilling instantiations) is exercised; bit-exact vs the oracle's restatement."""
+    n, iters = 50_001, m + 8
+    x0 = L.x0_uniform(n, 5, -2.0, 2.0)
+    with L.Context(n, m) as c:
+        r = c.minimize("rosenbrock", x0, ls, iters, trace=True, vector_free=True)
+    o = O.lbfgs("rosenbrock", x0, ls, m, iters, 1e-5, mode=O.CANON, vector_free=True)
+    assert r["iterations"] == o["iters"] == iters
+    assert np.array_equal(bits(r["tr_f"]), bits(o["f"]))
+    assert np.array_equal(bits(r["x"]), bits(o["x"]))
+    assert "Skipping" not in o["messages"]  # the history really reaches h = m
