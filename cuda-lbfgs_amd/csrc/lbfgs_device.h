@@ -66,7 +66,7 @@ extern "C" {
 enum {
     LBK_K_DOT = 0, LBK_K_AXPY_DOT, LBK_K_MID, LBK_K_AXPY2_DOT, LBK_K_LAST, LBK_K_NEGDOT,
     LBK_K_EVAL, LBK_K_TRIAL_F, LBK_K_TRIAL_FG, LBK_K_COMMIT, LBK_K_POINT, LBK_K_CHECKSUM,
-    LBK_K_UPDATE, LBK_K_VF_COMMIT, LBK_K_VF_DIR, LBK_K_COUNT
+    LBK_K_UPDATE, LBK_K_VF_COMMIT, LBK_K_VF_DIR, LBK_K_SMALL_ITER, LBK_K_COUNT
 };
 
 typedef struct {
@@ -141,6 +141,16 @@ int lbk_vf_dir(lbk_ctx* c, int h, double* d, const double* g, const double* cons
 int lbk_vf_bucket(int h);
 /* sharded vector-free: fill the ghost cells of x and g from the neighbours (solver start) */
 int lbk_vf_ghost_init(lbk_ctx* c, double* x, double* g, int wslot);
+
+/* small n (nseg within the context's limit, one rank, 1 <= h <= 16): the two-loop passes
+ * (P0 dot unless p0_ref >= 0, axpy_dot, mid, axpy2_dot into the given slots) and the TWOLOOP
+ * commit at a0 into slot_c, in one single-workgroup launch; the same slot contents and vectors as
+ * the multi-launch sequence. S/Y in ring order (oldest first). */
+int lbk_small_ok(const lbk_ctx* c, int h);
+int lbk_small_iter(lbk_ctx* c, int obj, int h, const double* g, double* q, double* r, const double* const* S,
+                   const double* const* Y, const double* rho, double gamma, int p0_ref, double a0, const double* x,
+                   double* xn, double* gn, double* so, double* yo, int slot_p0, int slot_a0, int slot_b0,
+                   int slot_c);
 
 /* unfused mode: out = op(a, b) with device-side coefficients (see k_update) */
 enum { LBK_U_AXPY_Q = 0, LBK_U_AXPY_R, LBK_U_SCALE, LBK_U_NEG, LBK_U_SUB, LBK_U_POINT };

@@ -643,6 +643,8 @@ static int iterate(lbfgs_ctx* c) {
 
     /* ---- search direction (:87-143) ---- */
     int dmode = LBK_D_NEG_G;
+    int small_done = 0;
+    const int small = c->obj != LBFGS_OBJ_HOST && !c->unfused && c->geo->world == 1 && lbk_small_ok(c->dev, h);
     c->d_ready = 0;
     c->spec_valid = 0;
     c->gt_valid = 0;
@@ -668,6 +670,27 @@ static int iterate(lbfgs_ctx* c) {
             rc = twoloop_unfused(c, rho, gamma);
             if (rc) return rc;
             dmode = LBK_D_BUF;
+        } else if (dmode == LBK_D_TWOLOOP && small) {
+            /* one single-workgroup launch: the passes below and the commit at a0 */
+            double rho[MMAX];
+            const double* Sr[MMAX];
+            const double* Yr[MMAX];
+            for (int i = 0; i < h; ++i) {
+                rho[i] = 1.0 / c->sy[c->ring[i]];
+                Sr[i] = c->S[c->ring[i]];
+                Yr[i] = c->Y[c->ring[i]];
+            }
+            const int top = c->ring[h - 1];
+            const int p0_ref = c->sg_valid ? c->sg_ref : -1;
+            DEV(lbk_small_iter(c->dev, c->obj, h, c->g, c->q, c->r, Sr, Yr, rho, gamma, p0_ref, c->K.initial_step,
+                               c->x, c->xn, c->gn, c->S[c->free_pair], c->Y[c->free_pair], SLOT_P0, SLOT_A0,
+                               SLOT_B0(m), SLOT_COMMIT0 + (k & 1)));
+            c->rho_last = rho[h - 1];
+            c->ref_b_last = REF(SLOT_B0(m) + h - 1, 0);
+            c->ref_a_last = p0_ref >= 0 ? p0_ref : REF(SLOT_P0, 0); /* alpha_{h-1}: s_{h-1} . g */
+            c->s_last_pair = top;
+            c->rc = c->r;
+            small_done = 1;
         } else if (dmode == LBK_D_TWOLOOP) {
             int refA[MMAX], refB[MMAX];
             double rho[MMAX];
@@ -729,8 +752,13 @@ static int iterate(lbfgs_ctx* c) {
             rc = materialize_d(c);
             if (rc) return rc;
         }
-        rc = commit(c, c->dmode, c->a0, cslot, tot);
-        if (rc) return rc;
+        if (small_done) { /* the commit at a0 ran inside lbk_small_iter */
+            DEVNC(lbk_fetch(c->dev, cslot, 7, tot));
+            c->commits++;
+        } else {
+            rc = commit(c, c->dmode, c->a0, cslot, tot);
+            if (rc) return rc;
+        }
         gd = tot[LBK_C_GD];
         if (gd >= 0) {
             say(c, "Warning: Not a descent direction, using gradient\n");

@@ -1122,6 +1122,157 @@ __global__ void k_vf_ghosts(const double* __restrict__ slot, double* x, double* 
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// Small-n persistent iteration (one workgroup): the whole two-loop recursion and the fused
+// first-trial commit of one iteration in ONE launch, for n small enough that the m-deep ring
+// sits in L2 and kernel boundaries, not bytes, set the time (SURVEY §7 step 5's persistent
+// two-loop, in the regime where it pays). The workgroup's 256-thread quarters each take a
+// segment and compute exactly what a workgroup of the multi-launch path computes for it; segment
+// partials stay in LDS; stage 2 (group trees, fixed-order total) runs in-kernel and every pass's
+// alpha / beta feeds the next pass from LDS. Each pass's 8 group values are also written to its
+// result slot, so everything after it (line search, a materialised d, a recommit) reads the same
+// slots as after the multi-launch sequence: bit-identical results.
+// ---------------------------------------------------------------------------------------
+#define LBK_SMALL_HMAX 16
+#define LBK_SMALL_SEGMAX 256
+#define LBK_SMALL_THREADS 512  // two segments at a time; 1024 would cap VGPRs at 128 and spill
+
+struct SmallArgs {
+    int h, p0_from_slot;
+    const double* g;
+    double* q;
+    double* r;
+    const double* S[LBK_SMALL_HMAX];
+    const double* Y[LBK_SMALL_HMAX];
+    double rho[LBK_SMALL_HMAX];
+    double gamma, a0;
+    const double* p0_slot;  // previous commit's slot, component SG (p0_from_slot)
+    const double* x;
+    double *xn, *gn, *so, *yo;
+    double* slots;          // slot base (LBK_SLOT doubles per slot)
+    int slot_p0, slot_a0, slot_b0, slot_c;
+};
+
+__device__ __forceinline__ Seg seg_at(const Geo& geo, int64_t sidx, int tq) {
+    Seg s;
+    s.sbeg = sidx * geo.L;
+    const int64_t send = min(s.sbeg + geo.L, geo.n);
+    s.len = send - s.sbeg;
+    s.lb = s.sbeg - geo.elem_lo;
+    s.lane = tq & 63;
+    s.w = tq >> 6;
+    const int nrow_tot = (int)((s.len + 127) / 128);
+    s.nrows = nrow_tot > s.w ? (nrow_tot - s.w + 3) / 4 : 0;
+    return s;
+}
+
+// one pass of Op over all segments; the K fixed-order totals land in tot[] (every thread)
+template <int K, class Op>
+__device__ void small_pass(const Op& op, const Geo& geo, double* slot, double (&tot)[K],
+                           double (*part)[LBK_SMALL_SEGMAX], double (*wl)[16]) {
+    const int t = threadIdx.x, qtr = t >> 8, tq = t & 255, lane = t & 63, wv = t >> 6;
+    for (int64_t s0 = 0; s0 < geo.nseg; s0 += LBK_SMALL_THREADS / 256) {
+        const int64_t sidx = s0 + qtr;
+        double acc[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) acc[k] = 0.0;
+        if (sidx < geo.nseg) {
+            const Seg sg = seg_at(geo, sidx, tq);
+            stream(op, sg, geo, acc);
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const double v = wave_sum(acc[k]);
+            if (lane == 0) wl[k][wv] = v;
+        }
+        __syncthreads();
+        if (tq == 0 && sidx < geo.nseg) {
+            const int w0 = 4 * qtr;
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+                part[k][sidx] = (wl[k][w0] + wl[k][w0 + 1]) + (wl[k][w0 + 2] + wl[k][w0 + 3]);
+        }
+        __syncthreads();
+    }
+    // stage 2: group 0 holds every segment (nseg <= 1024); groups 1..7 are trees of zeros
+    if (t < 256) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            double p[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int j = 4 * t + i;
+                p[i] = j < geo.nseg ? part[k][j] : 0.0;
+            }
+            const double v = wave_sum((p[0] + p[1]) + (p[2] + p[3]));
+            if (lane == 0) wl[k][wv] = v;
+        }
+    }
+    __syncthreads();
+    if (t < K) {
+        const int k = t;
+        const double q0 = (wl[k][0] + wl[k][1]) + (wl[k][2] + wl[k][3]);
+        for (int g = 0; g < LBK_GROUPS; ++g) slot[g * LBK_KMAX + k] = g == 0 ? q0 : 0.0;
+        double tt = q0;
+        for (int g = 1; g < LBK_GROUPS; ++g) tt = tt + 0.0;
+        wl[k][8] = tt;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < K; ++k) tot[k] = wl[k][8];
+    // this pass's vector writes are read by other waves in the next one (the commit's halo)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+template <int OBJ>
+__global__ __launch_bounds__(LBK_SMALL_THREADS) void k_small_iter(SmallArgs a, Geo geo) {
+    __shared__ double part[LBK_KMAX][LBK_SMALL_SEGMAX];
+    __shared__ double wl[LBK_KMAX][16];
+    __shared__ double TA[LBK_SMALL_HMAX], TB[LBK_SMALL_HMAX];
+    const int h = a.h;
+    double t1[1];
+    // alpha_{h-1} = rho_{h-1} (s_{h-1} . g): from the previous commit (SG) or a dot pass
+    if (a.p0_from_slot) {
+        t1[0] = slot_total(a.p0_slot);
+    } else {
+        small_pass<1>(OpDot<false>{a.S[h - 1], a.g}, geo, a.slots + (int64_t)a.slot_p0 * LBK_SLOT, t1, part, wl);
+    }
+    if (threadIdx.x == 0) TA[h - 1] = t1[0];
+    double alpha = a.rho[h - 1] * t1[0];
+    const double* qsrc = a.g;
+    for (int i = h - 2; i >= 0; --i) {  // q = q - alpha_{i+1} y_{i+1};  s_i . q
+        small_pass<1>(OpAxpyDot<false>{a.q, qsrc, a.Y[i + 1], a.S[i], alpha}, geo,
+                      a.slots + (int64_t)(a.slot_a0 + i) * LBK_SLOT, t1, part, wl);
+        if (threadIdx.x == 0) TA[i] = t1[0];
+        alpha = a.rho[i] * t1[0];
+        qsrc = a.q;
+    }
+    small_pass<1>(OpMid<false>{a.r, qsrc, a.Y[0], alpha, a.gamma}, geo, a.slots + (int64_t)a.slot_b0 * LBK_SLOT, t1,
+                  part, wl);
+    if (threadIdx.x == 0) TB[0] = t1[0];
+    __syncthreads();
+    for (int i = 0; i + 1 < h; ++i) {  // r += s_i (alpha_i - beta_i);  y_{i+1} . r
+        const double beta = a.rho[i] * TB[i];
+        const double alph = a.rho[i] * TA[i];
+        small_pass<1>(OpAxpy2Dot<false>{a.r, a.r, a.S[i], a.Y[i + 1], alph - beta}, geo,
+                      a.slots + (int64_t)(a.slot_b0 + i + 1) * LBK_SLOT, t1, part, wl);
+        if (threadIdx.x == 0) TB[i + 1] = t1[0];
+        __syncthreads();
+    }
+    // the last second-loop update, the first trial at a0 and the commit (k_commit TWOLOOP)
+    DirArgs da = {a.r, a.S[h - 1], a.g, 0.0, nullptr, nullptr, a.rho[h - 1], nullptr, geo.g_lo, geo.g_hi};
+    {
+        const double beta = a.rho[h - 1] * TB[h - 1];
+        const double alph = a.rho[h - 1] * TA[h - 1];
+        da.coef = alph - beta;
+    }
+    double t7[7];
+    small_pass<7>(OpCommit<OBJ, LBK_D_TWOLOOP, false>{a.x, da, a.a0, a.xn, a.gn, a.so, a.yo, geo.n, geo.n_loc}, geo,
+                  a.slots + (int64_t)a.slot_c * LBK_SLOT, t7, part, wl);
+}
+
 // z = x + alpha d over the whole local range incl. ghosts (host-callback objectives)
 __global__ void k_point(double* __restrict__ z, const double* __restrict__ x, const double* __restrict__ d,
                         double alpha, int64_t lo, int64_t hi) {
@@ -1267,6 +1418,7 @@ struct lbk_ctx {
     int ghost_slot;  // sharded: slot holding the all-gathered edge d values (-1: none)
     int ticket;      // reduction mode (see reduce_publish)
     lbk_group* grp;  // emulated ranks: host exchange group (tests; NULL with RCCL)
+    int small_seg_max;  // persistent single-workgroup iteration when nseg <= this (0: off)
 };
 
 namespace {
@@ -1493,6 +1645,12 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
     c->ticket = (G.seg_hi - G.seg_lo) <= 64 ? 1 : 0;
     if (const char* e = getenv("LBFGS_TICKET")) c->ticket = atoi(e) != 0;
     c->vec_doubles = LBK_FRONT + ((G.n_loc + 511) / 512) * 512 + 512;
+    // small n: the whole two-loop + commit in one single-workgroup launch (LBFGS_SMALL_SEGS=N
+    // enables it for nseg <= N). Measured 1.8x slower at n=1e4 and 5x at 3e4 than the launch
+    // sequence (profiles/r01/small_persistent.txt): one workgroup pays an L2 round trip per
+    // segment step, more than the kernel boundaries it removes. Off by default.
+    c->small_seg_max = 0;
+    if (const char* e = getenv("LBFGS_SMALL_SEGS")) c->small_seg_max = atoi(e);
     *out = c;
 #define CK(expr)                                                                             \
     do {                                                                                     \
@@ -1868,6 +2026,54 @@ int lbk_vf_dir(lbk_ctx* c, int h, double* d, const double* g, const double* cons
 #undef VF_CASE
     }
     return -1;
+}
+
+int lbk_small_iter(lbk_ctx* c, int obj, int h, const double* g, double* q, double* r, const double* const* S,
+                   const double* const* Y, const double* rho, double gamma, int p0_ref, double a0, const double* x,
+                   double* xn, double* gn, double* so, double* yo, int slot_p0, int slot_a0, int slot_b0,
+                   int slot_c) {
+    if (!lbk_small_ok(c, h)) return -1;
+    SmallArgs a;
+    memset(&a, 0, sizeof a);
+    a.h = h;
+    a.p0_from_slot = p0_ref >= 0;
+    a.p0_slot = p0_ref >= 0 ? sref(c, p0_ref) : nullptr;
+    a.g = g;
+    a.q = q;
+    a.r = r;
+    for (int i = 0; i < h; ++i) {
+        a.S[i] = S[i];
+        a.Y[i] = Y[i];
+        a.rho[i] = rho[i];
+    }
+    a.gamma = gamma;
+    a.a0 = a0;
+    a.x = x;
+    a.xn = xn;
+    a.gn = gn;
+    a.so = so;
+    a.yo = yo;
+    a.slots = c->slots;
+    a.slot_p0 = slot_p0;
+    a.slot_a0 = slot_a0;
+    a.slot_b0 = slot_b0;
+    a.slot_c = slot_c;
+    Geo geo = kgeo(c);
+    // algorithmic bytes: the multi-launch sequence's passes (P0 dot if computed, 4 per pair
+    // pass, 3 for mid, 8 for the commit)
+    const double vec = (p0_ref >= 0 ? 0.0 : 2.0) + 4.0 * (h - 1) + 3.0 + 4.0 * (h - 1) + 8.0;
+    return launch(c, LBK_K_SMALL_ITER, vec, -1, [&] {
+        switch (obj) {
+            case LBK_OBJ_ROSENBROCK: hipLaunchKernelGGL(k_small_iter<LBK_OBJ_ROSENBROCK>, dim3(1), dim3(LBK_SMALL_THREADS), 0, c->stream, a, geo); break;
+            case LBK_OBJ_QUAD_TRIDIAG: hipLaunchKernelGGL(k_small_iter<LBK_OBJ_QUAD_TRIDIAG>, dim3(1), dim3(LBK_SMALL_THREADS), 0, c->stream, a, geo); break;
+            default: hipLaunchKernelGGL(k_small_iter<LBK_OBJ_QUAD_SEPARABLE>, dim3(1), dim3(LBK_SMALL_THREADS), 0, c->stream, a, geo); break;
+        }
+    });
+}
+
+int lbk_small_ok(const lbk_ctx* c, int h) {
+    return c->small_seg_max > 0 && c->geo.world == 1 && c->geo.nseg <= c->small_seg_max &&
+           c->geo.nseg <= LBK_SMALL_SEGMAX && h >= 1 && h <= LBK_SMALL_HMAX;
 }
 
 int lbk_update(lbk_ctx* c, int op, double* out, const double* a, const double* b, double rho, int slot_a,

@@ -1,0 +1,5 @@
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/small_trace -o run --output-format csv -- python3 bench.py --size 1e4 --history 5 --steps 200 --warmup 20 --no-cpu-baseline --no-vector-free --no-prof > gpurun_out/small_trace.log 2>&1; echo "rc=$?"
+tail -1 gpurun_out/small_trace.log
