@@ -1015,7 +1015,11 @@ __device__ __forceinline__ void stream_vf(const Op& op, const Seg& s, const Geo&
     if (r0 >= r1) return;
     const bool full = s.len == geo.L;
     const bool last_lane = s.lane == 63;
-    double zl = (s.lane == 0) ? op.z_at(s.lb + (int64_t)r0 * 128 - 1) : 0.0;
+    // both ends of the run formed up front, branch-free: lane 0 at the left neighbour, every
+    // other lane at the right one (lane 63 keeps it for the last deferred element), so their
+    // loads overlap the first row's instead of waiting behind a lane-divergent branch
+    const double zedge = op.z_at(s.lane == 0 ? s.lb + (int64_t)r0 * 128 - 1 : s.lb + (int64_t)r1 * 128);
+    double zl = zedge;
     double pz_m = 0.0, pz_c = 0.0, px = 0.0, pg = 0.0;  // lane 63: deferred element of the previous row
     int64_t pi = 0, pe = 0;
     bool pvalid = false;
@@ -1041,10 +1045,7 @@ __device__ __forceinline__ void stream_vf(const Op& op, const Seg& s, const Geo&
         }
         zl = __shfl(r.z.y, 63, 64);
     }
-    if (last_lane && pvalid) {
-        const double zp = op.z_at(s.lb + (int64_t)r1 * 128);
-        op.finish(pz_m, pz_c, zp, px, pg, park[s.w], pi, pe, acc);
-    }
+    if (last_lane && pvalid) op.finish(pz_m, pz_c, zedge, px, pg, park[s.w], pi, pe, acc);
 }
 
 template <int OBJ, int HB, bool NT>
