@@ -9,6 +9,7 @@
  */
 #ifndef LBFGS_DEVICE_H
 #define LBFGS_DEVICE_H
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -101,6 +102,8 @@ int lbk_unique_id(void* out128);
 /* memory */
 double* lbk_vec_alloc(lbk_ctx* c);
 void lbk_vec_free(lbk_ctx* c, double* v);
+void* lbk_host_alloc(size_t bytes); /* pinned host memory (NULL on failure) */
+void lbk_host_free(void* p);
 int lbk_upload(lbk_ctx* c, double* dst, const double* host_global);     /* incl. ghosts */
 int lbk_download(lbk_ctx* c, double* host_global, const double* src);   /* local part */
 int lbk_copy(lbk_ctx* c, double* dst, const double* src);               /* incl. ghosts */

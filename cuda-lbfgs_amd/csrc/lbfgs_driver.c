@@ -289,8 +289,8 @@ void lbfgs_ctx_destroy(lbfgs_ctx* c) {
     if (!c) return;
     free_vectors(c);
     lbk_destroy(c->dev);
-    free(c->hx);
-    free(c->hg);
+    lbk_host_free(c->hx);
+    lbk_host_free(c->hg);
     free(c->msg);
     free(c->tr_f);
     free(c->tr_gn);
@@ -328,8 +328,9 @@ int lbfgs_sync(lbfgs_ctx* c) { return lbk_sync(c->dev) == 0 ? 0 : LBFGS_ERR_HIP;
  * Host-callback objective helpers (LBFGS_OBJ_HOST; single rank)
  * ---------------------------------------------------------------------------------------- */
 static int host_bufs(lbfgs_ctx* c) {
-    if (!c->hx) c->hx = (double*)malloc(sizeof(double) * (size_t)c->n);
-    if (!c->hg) c->hg = (double*)malloc(sizeof(double) * (size_t)c->n);
+    /* pinned: the per-trial x download and gradient upload are direct DMA, no staging copy */
+    if (!c->hx) c->hx = (double*)lbk_host_alloc(sizeof(double) * (size_t)c->n);
+    if (!c->hg) c->hg = (double*)lbk_host_alloc(sizeof(double) * (size_t)c->n);
     return (c->hx && c->hg) ? 0 : LBFGS_ERR_NOMEM;
 }
 

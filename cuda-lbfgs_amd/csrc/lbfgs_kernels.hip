@@ -1729,6 +1729,15 @@ void lbk_vec_free(lbk_ctx* c, double* v) {
     if (v) (void)hipFree(v - LBK_FRONT);
 }
 
+void* lbk_host_alloc(size_t bytes) {
+    void* p = nullptr;
+    return hipHostMalloc(&p, bytes, hipHostMallocDefault) == hipSuccess ? p : nullptr;
+}
+
+void lbk_host_free(void* p) {
+    if (p) (void)hipHostFree(p);
+}
+
 int lbk_upload(lbk_ctx* c, double* dst, const double* host_global) {
     // local range plus the ghosts that exist globally
     const int64_t lo = c->geo.elem_lo > 0 ? c->geo.elem_lo - 1 : 0;
