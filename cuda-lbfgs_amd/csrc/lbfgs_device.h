@@ -42,6 +42,8 @@ extern "C" {
 #define LBK_VF_YG 4  /* y_new . g_new        */
 #define LBK_VF_GGO 5 /* g_new . g_old        */
 #define LBK_VF_YB 6  /* + l: y_new . b_l (l < 2h); g_new . b_l at LBK_VF_YB + 2 HB + l */
+/* + j at LBK_VF_YB + 4 HB: f(x + cand_j d) at the line search's next candidate steps */
+#define LBK_VF_NA 1
 
 /* objective ids (match include/lbfgs_hip.h) */
 #define LBK_OBJ_ROSENBROCK 0
@@ -138,7 +140,8 @@ int lbk_point(lbk_ctx* c, double* z, const double* x, const double* d, double al
  * that fixes the component layout. lbk_vf_dir materialises d. */
 int lbk_vf_commit(lbk_ctx* c, int obj, int h, const double* x, const double* g, const double* const* S,
                   const double* const* Y, const double* cs, const double* cy, double cg, double alpha,
-                  double* xn, double* gn, double* so, double* yo, int wslot, int* hb_out);
+                  const double* cand /* LBK_VF_NA */, double* xn, double* gn, double* so, double* yo, int wslot,
+                  int* hb_out);
 int lbk_vf_dir(lbk_ctx* c, int h, double* d, const double* g, const double* const* S, const double* const* Y,
                const double* cs, const double* cy, double cg);
 int lbk_vf_bucket(int h);

@@ -89,6 +89,9 @@ struct lbfgs_ctx {
     double vf_cs[MMAX], vf_cy[MMAX], vf_cg; /* d = sum cs s + sum cy y + cg g */
     double vf_tot[LBK_KW], vf_spec[LBK_KW];
     int vf_hb;
+    /* f at the backtracking candidates a0 beta, a0 beta^2, reduced by the first commit pass */
+    double vf_cand[LBK_VF_NA], vf_cand_f[LBK_VF_NA];
+    int vf_cand_valid;
     /* counters */
     int64_t trials_f, trials_fg, commits, passes;
     /* messages / trace */
@@ -376,6 +379,13 @@ static int trial(lbfgs_ctx* c, double alpha, int need_g, double* f, double* dphi
         *f = c->spec_f;
         if (dphi) *dphi = c->spec_dphi;
         return 0;
+    }
+    if (c->vf && c->vf_cand_valid && !need_g) { /* f already reduced by the first commit pass */
+        for (int j = 0; j < LBK_VF_NA; ++j)
+            if (alpha == c->vf_cand[j]) {
+                *f = c->vf_cand_f[j];
+                return 0;
+            }
     }
     int rc = materialize_d(c);
     if (rc) return rc;
@@ -877,8 +887,8 @@ static double vf_dot_y(const lbfgs_ctx* c, int i, const double* ds, const double
 static int vf_commit(lbfgs_ctx* c, double alpha, double* tot) {
     int hb = 0;
     DEV(lbk_vf_commit(c->dev, c->obj, c->vf_h, c->x, c->g, c->vf_S, c->vf_Y, c->vf_cs, c->vf_cy, c->vf_cg, alpha,
-                      c->xn, c->gn, c->S[c->free_pair], c->Y[c->free_pair], LBK_WSLOT0, &hb));
-    DEVNC(lbk_fetch(c->dev, LBK_WSLOT0, LBK_VF_YB + 4 * hb, tot));
+                      c->vf_cand, c->xn, c->gn, c->S[c->free_pair], c->Y[c->free_pair], LBK_WSLOT0, &hb));
+    DEVNC(lbk_fetch(c->dev, LBK_WSLOT0, LBK_VF_YB + 4 * hb + LBK_VF_NA, tot));
     c->vf_hb = hb;
     c->commits++;
     return 0;
@@ -964,10 +974,15 @@ static int iterate_vf(lbfgs_ctx* c) {
 
     /* ---- fused first trial + commit at a0, then the line search (:156) ---- */
     c->a0 = c->K.initial_step;
+    c->vf_cand[0] = c->a0 * c->K.backtracking_alpha; /* the steps line_search.cpp:27 would try next */
+    for (int j = 1; j < LBK_VF_NA; ++j) c->vf_cand[j] = c->vf_cand[j - 1] * c->K.backtracking_alpha;
+    c->vf_cand_valid = 0;
     rc = vf_commit(c, c->a0, c->vf_spec);
     if (rc) return rc;
     const double* T = c->vf_spec;
     const int gb = LBK_VF_YB + 2 * c->vf_hb; /* g_new . b_l components */
+    for (int j = 0; j < LBK_VF_NA; ++j) c->vf_cand_f[j] = T[LBK_VF_YB + 4 * c->vf_hb + j];
+    c->vf_cand_valid = 1;
     double dgn = 0.0;                        /* g_new . d */
     for (int j = 0; j < h; ++j) dgn = dgn + c->vf_cs[j] * T[gb + j];
     for (int j = 0; j < h; ++j) dgn = dgn + c->vf_cy[j] * T[gb + h + j];

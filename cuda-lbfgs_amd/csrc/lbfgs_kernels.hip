@@ -880,12 +880,14 @@ __device__ __forceinline__ double vf_dir1(const VfBasis<HB>& B, const double* __
 // f terms, gradient, x_new, s, y, and the dots (components LBK_VF_*)
 template <int OBJ, int HB, bool NT>
 struct OpVfCommit {
-    static constexpr int K = LBK_VF_YB + 4 * HB;
+    static constexpr int K = LBK_VF_YB + 4 * HB + LBK_VF_NA;
+    static constexpr int FC = LBK_VF_YB + 4 * HB;  // f at the candidate steps ac[j]
     static constexpr int NB = 2 * HB;
     const double* __restrict__ x;
     const double* __restrict__ g;
     VfBasis<HB> B;
     double alpha;
+    double ac[LBK_VF_NA];  // the line search's next candidate steps (alpha * beta^j)
     double* __restrict__ xn;
     double* __restrict__ gn;
     double* __restrict__ so;
@@ -893,10 +895,11 @@ struct OpVfCommit {
     int64_t n, n_loc;
     struct Row {
         double2 x, g, z;
+        double2 zc[LBK_VF_NA];
         double2 b[2 * HB > 0 ? 2 * HB : 1];
         double zh;
     };
-    // x, g, the basis and z = x + alpha d of local elements i, i+1
+    // x, g, the basis and z = x + alpha d (and x + ac[j] d) of local elements i, i+1
     __device__ void load(Row& r, int64_t i) const {
         r.x = ldv<NT>(x + i);
         r.g = ldv<NT>(g + i);
@@ -925,6 +928,11 @@ struct OpVfCommit {
         }
         r.z.x = r.x.x + alpha * d.x;
         r.z.y = r.x.y + alpha * d.y;
+#pragma unroll
+        for (int j = 0; j < LBK_VF_NA; ++j) {
+            r.zc[j].x = r.x.x + ac[j] * d.x;
+            r.zc[j].y = r.x.y + ac[j] * d.y;
+        }
         r.zh = 0.0;
     }
     // lane 63: keep the basis values of its last element for finish()
@@ -936,9 +944,13 @@ struct OpVfCommit {
     // the deferred last element of a row (local i, global e) once its right neighbour zp is
     // known: the second element of apply() for lane 63, in the same operation order
     __device__ void finish(double zm, double zc, double zp, double xv, double gv, const double* pk, int64_t i,
-                           int64_t e, double (&acc)[K]) const {
+                           int64_t e, const double* pzc, const double* zpc, double (&acc)[K]) const {
         const bool p1 = e + 1 < n;
         if (obj_has_term<OBJ>(p1)) acc[LBK_VF_F] = acc[LBK_VF_F] + obj_term<OBJ>(zc, zp, p1);
+        if (obj_has_term<OBJ>(p1)) {
+#pragma unroll
+            for (int j = 0; j < LBK_VF_NA; ++j) acc[FC + j] = acc[FC + j] + obj_term<OBJ>(pzc[j], zpc[j], p1);
+        }
         const double g2 = obj_grad<OBJ>(zm, zc, zp, true, p1);
         gn[i] = g2;
         xn[i] = zc;
@@ -958,10 +970,11 @@ struct OpVfCommit {
             }
         }
     }
-    // z at one local element (-1 <= hi <= n_loc) formed from memory (segment edges only)
-    __device__ double z_at(int64_t hi) const {
-        if (!needs_halo<OBJ>()) return 0.0;
-        return (hi >= -1 && hi <= n_loc) ? x[hi] + alpha * vf_dir1<HB>(B, g, hi) : 0.0;
+    // (x, d) at one local element (-1 <= hi <= n_loc) formed from memory (segment edges only);
+    // z = x + alpha d for any step alpha
+    __device__ double2 xd_at(int64_t hi) const {
+        if (!needs_halo<OBJ>() || hi < -1 || hi > n_loc) return make_double2(0.0, 0.0);
+        return make_double2(x[hi], vf_dir1<HB>(B, g, hi));
     }
     template <bool MASK>
     __device__ void apply(Row& r, int64_t i, int64_t e0, bool v0, bool v1, double (&acc)[K]) const {
@@ -980,6 +993,17 @@ struct OpVfCommit {
         acc[LBK_VF_GG] = fma2<MASK>(g2, g2, acc[LBK_VF_GG], v0, v1);
         acc[LBK_VF_YG] = fma2<MASK>(yv, g2, acc[LBK_VF_YG], v0, v1);
         acc[LBK_VF_GGO] = fma2<MASK>(g2, r.g, acc[LBK_VF_GGO], v0, v1);
+        // f at the candidate steps: the same terms as objective_pair's, right neighbours only
+        {
+            const bool p0 = e0 + 1 < n, p1 = e0 + 2 < n;
+#pragma unroll
+            for (int j = 0; j < LBK_VF_NA; ++j) {
+                const double nr = __shfl_down(r.zc[j].x, 1, 64);
+                if ((!MASK || v0) && obj_has_term<OBJ>(p0))
+                    acc[FC + j] = acc[FC + j] + obj_term<OBJ>(r.zc[j].x, r.zc[j].y, p0);
+                if ((!MASK || v1) && obj_has_term<OBJ>(p1)) acc[FC + j] = acc[FC + j] + obj_term<OBJ>(r.zc[j].y, nr, p1);
+            }
+        }
 #if LBK_VF_EXP == 2
         if (B.h < 0)
 #endif
@@ -1018,7 +1042,14 @@ __device__ __forceinline__ void stream_vf(const Op& op, const Seg& s, const Geo&
     // both ends of the run formed up front, branch-free: lane 0 at the left neighbour, every
     // other lane at the right one (lane 63 keeps it for the last deferred element), so their
     // loads overlap the first row's instead of waiting behind a lane-divergent branch
-    const double zedge = op.z_at(s.lane == 0 ? s.lb + (int64_t)r0 * 128 - 1 : s.lb + (int64_t)r1 * 128);
+    const double2 xd = op.xd_at(s.lane == 0 ? s.lb + (int64_t)r0 * 128 - 1 : s.lb + (int64_t)r1 * 128);
+    const double zedge = xd.x + op.alpha * xd.y;
+    double zedge_c[LBK_VF_NA], pzc[LBK_VF_NA], zfc[LBK_VF_NA];
+#pragma unroll
+    for (int j = 0; j < LBK_VF_NA; ++j) {
+        zedge_c[j] = xd.x + op.ac[j] * xd.y;
+        pzc[j] = 0.0;
+    }
     double zl = zedge;
     double pz_m = 0.0, pz_c = 0.0, px = 0.0, pg = 0.0;  // lane 63: deferred element of the previous row
     int64_t pi = 0, pe = 0;
@@ -1028,7 +1059,9 @@ __device__ __forceinline__ void stream_vf(const Op& op, const Seg& s, const Geo&
         typename Op::Row r;
         op.load(r, s.lb + o);
         const double zfirst = __shfl(r.z.x, 0, 64);
-        if (last_lane && row > r0 && pvalid) op.finish(pz_m, pz_c, zfirst, px, pg, park[s.w], pi, pe, acc);
+#pragma unroll
+        for (int j = 0; j < LBK_VF_NA; ++j) zfc[j] = __shfl(r.zc[j].x, 0, 64);
+        if (last_lane && row > r0 && pvalid) op.finish(pz_m, pz_c, zfirst, px, pg, park[s.w], pi, pe, pzc, zfc, acc);
         r.zh = zl;  // lane 0's left neighbour; lane 63's right neighbour is deferred
         const bool v0 = full || o < s.len;
         const bool v1 = !last_lane && (full || o + 1 < s.len);
@@ -1036,6 +1069,8 @@ __device__ __forceinline__ void stream_vf(const Op& op, const Seg& s, const Geo&
         if (last_lane) {
             pz_m = r.z.x;
             pz_c = r.z.y;
+#pragma unroll
+            for (int j = 0; j < LBK_VF_NA; ++j) pzc[j] = r.zc[j].y;
             px = r.x.y;
             pg = r.g.y;
             op.park(r, park[s.w]);
@@ -1045,7 +1080,7 @@ __device__ __forceinline__ void stream_vf(const Op& op, const Seg& s, const Geo&
         }
         zl = __shfl(r.z.y, 63, 64);
     }
-    if (last_lane && pvalid) op.finish(pz_m, pz_c, zedge, px, pg, park[s.w], pi, pe, acc);
+    if (last_lane && pvalid) op.finish(pz_m, pz_c, zedge, px, pg, park[s.w], pi, pe, pzc, zedge_c, acc);
 }
 
 template <int OBJ, int HB, bool NT>
@@ -1961,15 +1996,15 @@ VfBasis<HB> vf_basis(int h, const double* const* S, const double* const* Y, cons
 
 template <int HB>
 int vf_commit_hb(lbk_ctx* c, int obj, int h, const double* x, const double* g, const double* const* S,
-                 const double* const* Y, const double* cs, const double* cy, double cg, double alpha, double* xn,
-                 double* gn, double* so, double* yo, int wslot) {
+                 const double* const* Y, const double* cs, const double* cy, double cg, double alpha,
+                 const double* cand, double* xn, double* gn, double* so, double* yo, int wslot) {
     Geo geo = kgeo(c);
     Red r = kred(c, wslot);
     const VfBasis<HB> B = vf_basis<HB>(h, S, Y, cs, cy, cg);
-    constexpr int K = LBK_VF_YB + 4 * HB;
+    constexpr int K = LBK_VF_YB + 4 * HB + LBK_VF_NA;
     const int rc = launch(c, LBK_K_VF_COMMIT, 2.0 * h + 6.0, wslot, [&] {
         OBJ_DISPATCH(obj, {
-            OpVfCommit<O_, HB, NT_> op{x, g, B, alpha, xn, gn, so, yo, geo.n, geo.n_loc};
+            OpVfCommit<O_, HB, NT_> op{x, g, B, alpha, {cand[0]}, xn, gn, so, yo, geo.n, geo.n_loc};
             hipLaunchKernelGGL((k_vf_commit<O_, HB, NT_>), dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, op, geo, r);
         });
         return 0;
@@ -2009,7 +2044,7 @@ int lbk_vf_bucket(int h) {
 
 int lbk_vf_commit(lbk_ctx* c, int obj, int h, const double* x, const double* g, const double* const* S,
                   const double* const* Y, const double* cs, const double* cy, double cg, double alpha,
-                  double* xn, double* gn, double* so, double* yo, int wslot, int* hb_out) {
+                  const double* cand, double* xn, double* gn, double* so, double* yo, int wslot, int* hb_out) {
     const int hb = lbk_vf_bucket(h);
     if (hb < 0 || wslot < LBK_WSLOT0 || wslot >= LBK_WSLOT0 + LBK_NWSLOTS) {
         snprintf(c->err, sizeof c->err, "lbk_vf_commit: h=%d (max %d), slot %d", h, LBK_VF_HMAX, wslot);
@@ -2018,7 +2053,7 @@ int lbk_vf_commit(lbk_ctx* c, int obj, int h, const double* x, const double* g, 
     *hb_out = hb;
     switch (hb) {
 #define VF_CASE(HB) \
-    case HB: return vf_commit_hb<HB>(c, obj, h, x, g, S, Y, cs, cy, cg, alpha, xn, gn, so, yo, wslot);
+    case HB: return vf_commit_hb<HB>(c, obj, h, x, g, S, Y, cs, cy, cg, alpha, cand, xn, gn, so, yo, wslot);
         VF_BUCKETS(VF_CASE)
 #undef VF_CASE
     }

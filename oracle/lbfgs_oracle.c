@@ -449,11 +449,13 @@ static double ls_wolfe(ctx_t* c, const double* x, const double* d, const double*
  * derived as alpha (d . v). Every host sum runs s terms, y terms, then g, from 0.0. The line
  * searches are those of line_search.cpp with f(x) and g.d evaluated once (identical values).
  * ---------------------------------------------------------------------------------------- */
+#define VF_NA 1 /* backtracking candidates reduced by the first commit pass */
 typedef struct {
     ctx_t* C;
     const double *x, *d;
     double* gt;    /* trial gradient scratch */
     double a0, f0, dphi0; /* the fused first trial */
+    double cand[VF_NA], fc[VF_NA]; /* f at a0 beta^j, j = 1, 2, in the ORC_CANON_VF order */
 } vf_ls_t;
 
 static double vf_trial(vf_ls_t* L, double alpha, int need_g, double* dphi) {
@@ -462,6 +464,9 @@ static double vf_trial(vf_ls_t* L, double alpha, int need_g, double* dphi) {
         if (dphi) *dphi = L->dphi0;
         return L->f0;
     }
+    if (!need_g)
+        for (int j = 0; j < VF_NA; ++j)
+            if (alpha == L->cand[j]) return L->fc[j];
     trial_point(L->x, L->d, alpha, c->n, c->tmp);
     double f = F(c, c->tmp);
     if (need_g) {
@@ -707,7 +712,13 @@ static int orc_lbfgs_vf(const orc_opts* o, const double* x0, double* x_out, doub
                 for (int j = 0; j < h; ++j) dgn = dgn + cs[j] * GB[j];
                 for (int j = 0; j < h; ++j) dgn = dgn + cy[j] * GB[h + j];
                 dgn = dgn + cg * ggo;
-                vf_ls_t L = {C, x, d, gt, o->initial_step, fN, dgn};
+                vf_ls_t L = {C, x, d, gt, o->initial_step, fN, dgn, {0.0}, {0.0}};
+                L.cand[0] = o->initial_step * o->backtracking_alpha;
+                for (int j = 1; j < VF_NA; ++j) L.cand[j] = L.cand[j - 1] * o->backtracking_alpha;
+                for (int j = 0; j < VF_NA; ++j) {
+                    trial_point(x, d, L.cand[j], n, C->tmp);
+                    L.fc[j] = orc_f(o->obj, C->tmp, n, ORC_CANON_VF);
+                }
                 alpha = vf_ls(&L, f_cur, gd);
                 if (ntr < trace_cap) tr_alpha[ntr] = alpha;
                 ntr++;
