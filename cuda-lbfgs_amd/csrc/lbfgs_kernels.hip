@@ -1004,9 +1004,6 @@ struct OpVfCommit {
                 if ((!MASK || v1) && obj_has_term<OBJ>(p1)) acc[FC + j] = acc[FC + j] + obj_term<OBJ>(r.zc[j].y, nr, p1);
             }
         }
-#if LBK_VF_EXP == 2
-        if (B.h < 0)
-#endif
 #pragma unroll
         for (int l = 0; l < 2 * HB; ++l) {
             if (l < 2 * B.h) {
@@ -1016,10 +1013,6 @@ struct OpVfCommit {
         }
     }
 };
-
-#ifndef LBK_VF_EXP
-#define LBK_VF_EXP 0
-#endif
 
 // The segment walk of the vector-free commit. Wave w takes a contiguous run of rows
 // [wR, min((w+1)R, nrow)), R = ceil(nrow / 4) (the ORC_CANON_VF order), so a row's left stencil
