@@ -4,9 +4,10 @@ n=1e4, one row per line search, GPU against the sequential CPU code. Here the GP
 (default and vector-free modes), the CPU is the reference's own sequential sources compiled
 unmodified (oracle/_ref/ref_lbfgs) on one core of the same box.
 
-Each cell is the mean time per iteration over the same 1000 iterations (m = 5, x0 from
-std::mt19937(42), tol 1e-5 — none of the four converges within 1000 iterations at this n, so every
-run takes exactly 1000 steps), and the table reports the speedups.
+Each cell is the time of the same 1000 iterations (m = 5, x0 from std::mt19937(42), tol 1e-5 —
+none of the four converges within 1000 iterations at this n, so every run takes exactly 1000
+steps), best of 3 runs on each side (the box's shared host cores make single CPU timings vary by
+±20 %), and the table reports the speedups.
 
 usage: python tools/paper_table.py [out.json]
 """
@@ -61,9 +62,10 @@ def cpu(ls):
 def main():
     rows = {}
     for ls in ["backtracking", "interpolation", "backtracking_wolfe", "wolfe"]:
-        gd = gpu(ls, False)
-        gv = gpu(ls, True)
-        c = cpu(ls)
+        best = lambda f: min((f() for _ in range(3)), key=lambda r: r["seconds"])  # noqa: E731
+        gd = best(lambda: gpu(ls, False))
+        gv = best(lambda: gpu(ls, True))
+        c = best(lambda: cpu(ls))
         rows[ls] = dict(published_speedup_T4=PUBLISHED[ls], cpu_reference=c, gpu_default=gd, gpu_vector_free=gv,
                         speedup_default=c["seconds"] / gd["seconds"], speedup_vector_free=c["seconds"] / gv["seconds"])
         print(ls, json.dumps(rows[ls]), flush=True)
