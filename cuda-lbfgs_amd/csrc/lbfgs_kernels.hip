@@ -1647,6 +1647,9 @@ int lbk_geometry_plan(int64_t n, int rank, int world, lbk_geo* out) {
     const int64_t per = (n + LBK_SEGS - 1) / LBK_SEGS;
     G.L = ((per + 127) / 128) * 128;
     if (G.L < 512) G.L = 512;
+#ifdef LBK_DEBUG_SEGLEN  // timing experiments only (tools/gpu_ab_shardgeo.sh): breaks the canonical order
+    G.L = LBK_DEBUG_SEGLEN;
+#endif
     G.nseg = (n + G.L - 1) / G.L;
     G.rank = rank;
     G.world = world;
@@ -1684,7 +1687,10 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
     if (const char* e = getenv("LBFGS_NT")) c->nt = atoi(e) != 0;
     // stage-2 reduction: separate 8-workgroup kernel by default; in-launch tickets only for
     // tiny grids where the extra launch dominates (override: LBFGS_TICKET=0/1)
-    c->ticket = (G.seg_hi - G.seg_lo) <= 64 ? 1 : 0;
+    // sharded runs with long segments too: one rank of an 8-GPU n = 1e8 run (1017 workgroups of
+    // L = 12288 per pass) measured 1 % faster with tickets on one GPU (tools/gpu_ab_shardgeo.sh),
+    // and the stage-2 launch before each all-gather disappears
+    c->ticket = ((G.seg_hi - G.seg_lo) <= 64 || (world > 1 && G.L >= 8192)) ? 1 : 0;
     if (const char* e = getenv("LBFGS_TICKET")) c->ticket = atoi(e) != 0;
     c->vec_doubles = LBK_FRONT + ((G.n_loc + 511) / 512) * 512 + 512;
     // small n: the whole two-loop + commit in one single-workgroup launch (LBFGS_SMALL_SEGS=N

@@ -254,10 +254,11 @@ def test_host_callback_objective_matches_device_objective():
     assert np.array_equal(rh["tr_c1"], rd["tr_c1"])
 
 
+@pytest.mark.parametrize("ticket", ["0", "1"])
 @pytest.mark.parametrize("world", [2, 4, 8])
 @pytest.mark.parametrize("obj,ls", [("rosenbrock", "backtracking"), ("rosenbrock", "wolfe"),
                                     ("quad_tridiag", "wolfe")])
-def test_sharded_emulated_bit_exact(world, obj, ls):
+def test_sharded_emulated_bit_exact(world, obj, ls, ticket, monkeypatch):
     """The sharded data path (group ownership, halo of d through the all-gathered slot,
     x ghosts, per-rank slices) with `world` emulated ranks on this GPU — threads with one
     stream each, exchanging through host memory exactly where RCCL all-gathers — must give
@@ -269,6 +270,7 @@ def test_sharded_emulated_bit_exact(world, obj, ls):
     m, iters = 5, 12
     x0 = L.x0_uniform(n, 42, -2.0, 2.0)
     ref = ctx(n, m).minimize(obj, x0, ls, iters, trace=True)
+    monkeypatch.setenv("LBFGS_TICKET", ticket)  # both stage-2 forms under sharding (read at creation)
     grp = L.HostGroup(world)
     ctxs = [L.Context(n, m, rank=r, group=grp) for r in range(world)]
     out = [None] * world

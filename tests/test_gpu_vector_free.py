@@ -113,10 +113,11 @@ def test_vector_free_rejects_unsupported():
             c.minimize("rosenbrock", np.zeros(100), "backtracking", 5, vector_free=True)
 
 
+@pytest.mark.parametrize("ticket", ["0", "1"])
 @pytest.mark.parametrize("world", [2, 4, 8])
 @pytest.mark.parametrize("obj,ls", [("rosenbrock", "backtracking"), ("rosenbrock", "wolfe"),
                                     ("quad_tridiag", "wolfe")])
-def test_vector_free_sharded_emulated_bit_exact(world, obj, ls):
+def test_vector_free_sharded_emulated_bit_exact(world, obj, ls, ticket, monkeypatch):
     """Sharded vector-free mode (one wide all-gather per commit carrying the reductions and the
     ranks' edge values of x, g, s, y into the neighbours' ghost cells) with `world` emulated
     ranks on this GPU gives the single-GPU trajectory bit for bit."""
@@ -127,6 +128,7 @@ def test_vector_free_sharded_emulated_bit_exact(world, obj, ls):
     x0 = L.x0_uniform(n, 42, -2.0, 2.0)
     with L.Context(n, m) as c:
         ref = c.minimize(obj, x0, ls, iters, trace=True, vector_free=True)
+    monkeypatch.setenv("LBFGS_TICKET", ticket)
     grp = L.HostGroup(world)
     ctxs = [L.Context(n, m, rank=r, group=grp) for r in range(world)]
     out = [None] * world
