@@ -55,6 +55,9 @@ def parse():
                    help="Gram-matrix two-loop, one fused pass per iteration (opt-in mode)")
     p.add_argument("--no-vector-free", action="store_true",
                    help="skip the vector-free measurement reported beside the default mode")
+    p.add_argument("--exchange", choices=["xgmi", "rccl"], default="xgmi",
+                   help="sharded runs: reductions through the xGMI peer mailboxes (falls back to RCCL "
+                        "when any rank's self-test fails) or RCCL all-gathers")
     return p.parse_args()
 
 
@@ -87,8 +90,17 @@ class Dist:
         import torch
 
         t = torch.tensor([v], dtype=torch.float64)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX if op == "max" else self.dist.ReduceOp.SUM)
+        ops = {"max": self.dist.ReduceOp.MAX, "min": self.dist.ReduceOp.MIN, "sum": self.dist.ReduceOp.SUM}
+        self.dist.all_reduce(t, op=ops[op])
         return float(t.item())
+
+    def allgather_bytes(self, b):
+        out = [None] * self.world
+        self.dist.all_gather_object(out, b)
+        return out
+
+    def all_ok(self, ok):
+        return self.allreduce(1.0 if ok else 0.0, "min") > 0.5
 
     def close(self):
         if self.dist:
@@ -162,6 +174,13 @@ def measure(a, D, n, x0, dev, rank, world, uid, unfused=False, vector_free=False
     """W warm-up steps, then EXACTLY K timed steps (barrier + device sync on both sides, no
     instrumentation), then a separate event-instrumented pass for per-kernel durations."""
     ctx = L.Context(n, a.history, device=dev, rank=rank, world=world, uid=uid)
+    if world > 1 and a.exchange == "xgmi":
+        ok, msg = ctx.connect_peers(D.allgather_bytes, D.all_ok)
+        if msg:
+            print(f"rank {rank}: {msg}", file=sys.stderr, flush=True)
+        if not ok and uid is None:
+            raise L.LbfgsError("xGMI peer exchange unavailable and no RCCL communicator")
+    backend = ctx.backend
     ctx.init(a.objective, x0, a.line_search, tolerance=1e-5, unfused=unfused, vector_free=vector_free)
     ctx.step(a.warmup)
     ctx.sync()
@@ -190,7 +209,7 @@ def measure(a, D, n, x0, dev, rank, world, uid, unfused=False, vector_free=False
                 prof[kname] = p
     ctx.close()
     done_steps = a.steps if res["status"] == "running" else max(res["iterations"] - a.warmup, 1)
-    return T, res, prof, bytes_all, done_steps
+    return T, res, prof, bytes_all, done_steps, backend
 
 
 def roofline(prof, n, world):
@@ -214,12 +233,16 @@ def main():
     n = int(a.size)
     D = Dist(a.gpus)
     world, rank = a.gpus, D.rank
-    uid = D.broadcast_bytes(L.unique_id() if (world > 1 and rank == 0) else None) if world > 1 else None
+    # BENCH_DEVICE_MOD (several ranks on one GPU) cannot create an RCCL communicator: RCCL
+    # refuses two ranks on one device; those rehearsals run on the peer exchange alone
+    rehearsal = "BENCH_DEVICE_MOD" in os.environ
+    need_uid = world > 1 and not rehearsal
+    uid = D.broadcast_bytes(L.unique_id() if (need_uid and rank == 0) else None) if need_uid else None
 
     x0 = L.x0_uniform(n, 42, -2.0, 2.0)
     # BENCH_DEVICE_MOD=k maps rank -> device local_rank % k (rehearsing several ranks on fewer GPUs)
     dev = D.local_rank % int(os.environ["BENCH_DEVICE_MOD"]) if "BENCH_DEVICE_MOD" in os.environ else D.local_rank
-    T, res, prof, bytes_all, done_steps = measure(a, D, n, x0, dev, rank, world, uid,
+    T, res, prof, bytes_all, done_steps, backend = measure(a, D, n, x0, dev, rank, world, uid,
                                                   unfused=a.unfused, vector_free=a.vector_free)
     # the opt-in vector-free mode alongside the default (outside the bit-parity contract with
     # the reference's operation order); sharded runs need a fresh RCCL id
@@ -228,8 +251,8 @@ def main():
         # a failure here is deterministic across ranks (same arguments everywhere) and must not
         # cost the headline line above
         try:
-            uid2 = D.broadcast_bytes(L.unique_id() if rank == 0 else None) if world > 1 else None
-            Tv, rv, pv, bv, dv = measure(a, D, n, x0, dev, rank, world, uid2, vector_free=True)
+            uid2 = D.broadcast_bytes(L.unique_id() if rank == 0 else None) if need_uid else None
+            Tv, rv, pv, bv, dv, _ = measure(a, D, n, x0, dev, rank, world, uid2, vector_free=True)
             vf = dict(value=round(dv / Tv, 4), ms_per_step=round(Tv / dv * 1e3, 4), steps=dv,
                       achieved_hbm_gbps=round(bv / Tv / 1e9, 1), roofline=roofline(pv, n, world),
                       solver={"status": rv["status"], "f": rv["f"], "gnorm": rv["gnorm"],
@@ -279,7 +302,8 @@ def main():
                                     + (" (BASELINE configs[2])" if n == 10 ** 8 else "")),
                        "kernels": "unfused" if a.unfused else "vector_free" if a.vector_free else "fused",
                        "n": n, "m": a.history, "line_search": a.line_search,
-                       "parallelism": f"shard{world}" if world > 1 else "single"},
+                       "parallelism": f"shard{world}" if world > 1 else "single",
+                       "exchange": backend},
             "achieved_hbm_gbps": round(bytes_all / T / 1e9, 1),
             "bytes_per_step": bytes_all / max(done_steps, 1),
             "roofline": roof,

@@ -87,7 +87,8 @@ typedef struct {
 typedef struct lbk_ctx lbk_ctx;
 typedef struct lbk_group lbk_group; /* host exchange group for emulated ranks (tests) */
 
-/* lifecycle. world > 1: RCCL communicator from nccl_id, or the host group grp */
+/* lifecycle. world > 1: RCCL communicator from nccl_id (may be NULL: peer exchange only), or
+ * the host group grp */
 int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const void* nccl_id,
                lbk_group* grp);
 /* canonical geometry and this rank's shard, no device needed (0, or < 0 if not shardable) */
@@ -100,6 +101,14 @@ void lbk_destroy(lbk_ctx* c);
 const lbk_geo* lbk_geometry(const lbk_ctx* c);
 const char* lbk_last_error(const lbk_ctx* c);
 int lbk_unique_id(void* out128);
+/* sharded contexts (world > 1, one process per GPU): peer mailboxes over xGMI (lbfgs_xgmi.h).
+ * handle: LBK_PEER_HANDLE_BYTES = 64; connect maps all peers' mailboxes (world handles in rank
+ * order) and self-tests the exchange; enable switches every later exchange to it. */
+int lbk_peer_handle(lbk_ctx* c, void* out);
+int lbk_peer_connect(lbk_ctx* c, const void* handles);
+int lbk_peer_enable(lbk_ctx* c, int on);
+/* 0 none (one rank), 1 RCCL, 2 xGMI peer mailboxes, 3 host group (emulated ranks) */
+int lbk_exchange_backend(const lbk_ctx* c);
 
 /* memory */
 double* lbk_vec_alloc(lbk_ctx* c);

@@ -238,7 +238,6 @@ static int ctx_create(lbfgs_ctx** out, int64_t n, int m, int device, int rank, i
     *out = NULL;
     if (n < 1 || m < 1 || m > MMAX || world < 1 || (8 % world) != 0 || rank < 0 || rank >= world)
         return LBFGS_ERR_BAD_ARG;
-    if (world > 1 && !unique_id && !grp) return LBFGS_ERR_BAD_ARG;
     lbfgs_ctx* c = (lbfgs_ctx*)calloc(1, sizeof(lbfgs_ctx));
     if (!c) return LBFGS_ERR_NOMEM;
     c->n = n;
@@ -326,6 +325,28 @@ int lbfgs_local_range(const lbfgs_ctx* c, int64_t* elem_lo, int64_t* n_loc) {
 }
 
 int lbfgs_sync(lbfgs_ctx* c) { return lbk_sync(c->dev) == 0 ? 0 : LBFGS_ERR_HIP; }
+
+int lbfgs_peer_handle(lbfgs_ctx* c, void* out) {
+    if (!c || !out || lbk_peer_handle(c->dev, out) != 0) return LBFGS_ERR_BAD_ARG;
+    return 0;
+}
+
+int lbfgs_peer_connect(lbfgs_ctx* c, const void* handles) {
+    if (!c || !handles || c->geo->world <= 1) return LBFGS_ERR_BAD_ARG;
+    const int rc = lbk_peer_connect(c->dev, handles);
+    if (rc != 0) {
+        snprintf(c->err, sizeof c->err, "%s", lbk_last_error(c->dev));
+        return rc == -1 ? LBFGS_ERR_BAD_ARG : rc == -3 ? LBFGS_ERR_RCCL : LBFGS_ERR_HIP;
+    }
+    return 0;
+}
+
+int lbfgs_peer_enable(lbfgs_ctx* c, int on) {
+    if (!c || c->geo->world <= 1) return LBFGS_ERR_BAD_ARG;
+    return lbk_peer_enable(c->dev, on) == 0 ? 0 : LBFGS_ERR_STATE;
+}
+
+int lbfgs_exchange_backend(const lbfgs_ctx* c) { return c ? lbk_exchange_backend(c->dev) : LBFGS_ERR_BAD_ARG; }
 
 /* ------------------------------------------------------------------------------------------
  * Host-callback objective helpers (LBFGS_OBJ_HOST; single rank)

@@ -40,6 +40,7 @@
 #include <vector>
 
 #include "lbfgs_device.h"
+#include "lbfgs_xgmi.h"
 
 #define LB_BLOCK 256
 #define LBK_FRONT 32
@@ -1460,6 +1461,9 @@ struct lbk_ctx {
     int ghost_slot;  // sharded: slot holding the all-gathered edge d values (-1: none)
     int ticket;      // reduction mode (see reduce_publish)
     lbk_group* grp;  // emulated ranks: host exchange group (tests; NULL with RCCL)
+    lbk_xgmi* xg;    // sharded, one process per GPU: peer mailboxes over xGMI (lbfgs_xgmi.hip)
+    int xg_on;       // 1: exchanges go through xg instead of RCCL
+    uint64_t* d_ckslot;  // [LBK_GROUPS][2] checksum words for the peer exchange
     int small_seg_max;  // persistent single-workgroup iteration when nseg <= this (0: off)
 };
 
@@ -1563,6 +1567,17 @@ int exchange_slot(lbk_ctx* c, int slot) {
         HIPCHK(c, hipMemcpy(base, G->table, sizeof(double) * LBK_GROUPS * ks, hipMemcpyHostToDevice));
         pthread_barrier_wait(&G->bar);
         return 0;
+    }
+    if (c->xg_on) {
+        if (lbk_xgmi_exchange(c->xg, c->stream, base, ks, c->geo.g_lo, c->geo.g_hi) != 0) {
+            snprintf(c->err, sizeof c->err, "xgmi exchange launch failed");
+            return -3;
+        }
+        return 0;
+    }
+    if (!c->comm) {
+        snprintf(c->err, sizeof c->err, "sharded context has no exchange backend (no RCCL id, peers not enabled)");
+        return -3;
     }
     ncclResult_t r = ncclAllGather(base + c->geo.g_lo * ks, base, (size_t)per, ncclDouble, c->comm, c->stream);
     if (r != ncclSuccess) {
@@ -1725,6 +1740,11 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
     CK(hipDeviceSynchronize());
 #undef CK
     if (world > 1 && !grp) {
+        const int xrc = lbk_xgmi_create(&c->xg, device, rank, world, LBK_WSLOT, c->err, sizeof c->err);
+        if (xrc != 0) return xrc;
+        if (hipMalloc(&c->d_ckslot, sizeof(uint64_t) * LBK_GROUPS * 2) != hipSuccess) return -2;
+    }
+    if (world > 1 && !grp && nccl_id) {
         ncclUniqueId id;
         memcpy(&id, nccl_id, sizeof id);
         ncclResult_t r = ncclCommInitRank(&c->comm, world, id, rank);
@@ -1743,6 +1763,8 @@ void lbk_destroy(lbk_ctx* c) {
     prof_flush(c);
     for (auto e : c->ev_free) (void)hipEventDestroy(e);
     if (c->comm) ncclCommDestroy(c->comm);
+    lbk_xgmi_destroy(c->xg);
+    if (c->d_ckslot) (void)hipFree(c->d_ckslot);
     (void)hipFree(c->partials);
     (void)hipFree(c->cnt);
     (void)hipFree(c->slots);
@@ -2175,7 +2197,33 @@ int lbk_checksum(lbk_ctx* c, const double* x, uint64_t* c1, uint64_t* c2) {
         hipLaunchKernelGGL(k_checksum, dim3(nb), dim3(256), 0, c->stream, x, c->geo.n_loc, c->geo.elem_lo, c->d_ck);
         HIPCHK(c, hipGetLastError());
     }
+    if (c->geo.world > 1 && !c->grp && c->xg_on) {
+        // integer sums: gather every rank's pair through the peer mailboxes, add on the host
+        uint64_t w[LBK_GROUPS * 2];
+        HIPCHK(c, hipMemsetAsync(c->d_ckslot, 0, sizeof w, c->stream));
+        HIPCHK(c, hipMemcpyAsync(c->d_ckslot + 2 * c->geo.g_lo, c->d_ck, 2 * sizeof(uint64_t), hipMemcpyDeviceToDevice,
+                                 c->stream));
+        if (lbk_xgmi_exchange_u64(c->xg, c->stream, c->d_ckslot, 2, c->geo.g_lo, c->geo.g_hi) != 0) return -3;
+        HIPCHK(c, hipMemcpyAsync(w, c->d_ckslot, sizeof w, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (lbk_xgmi_failed(c->xg)) {
+            snprintf(c->err, sizeof c->err, "xgmi exchange timed out waiting for a peer");
+            return -3;
+        }
+        uint64_t a = 0, b = 0;
+        for (int g = 0; g < LBK_GROUPS; ++g) {
+            a += w[2 * g];
+            b += w[2 * g + 1];
+        }
+        *c1 = a;
+        *c2 = b;
+        return 0;
+    }
     if (c->geo.world > 1 && !c->grp) {
+        if (!c->comm) {
+            snprintf(c->err, sizeof c->err, "sharded context has no exchange backend");
+            return -3;
+        }
         ncclResult_t r = ncclAllReduce(c->d_ck, c->d_ck, 2, ncclUint64, ncclSum, c->comm, c->stream);
         if (r != ncclSuccess) return -3;
     }
@@ -2211,6 +2259,10 @@ int lbk_fetch_groups(lbk_ctx* c, int slot, double* groups64) {
     const size_t bytes = sizeof(double) * LBK_GROUPS * slot_stride(slot);
     HIPCHK(c, hipMemcpyAsync(h, slot_base(c, slot), bytes, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (c->xg_on && lbk_xgmi_failed(c->xg)) {
+        snprintf(c->err, sizeof c->err, "xgmi exchange timed out waiting for a peer");
+        return -3;
+    }
     memcpy(groups64, h, bytes);
     return 0;
 }
@@ -2231,7 +2283,35 @@ int lbk_fetch(lbk_ctx* c, int slot, int ncomp, double* totals) {
 
 int lbk_sync(lbk_ctx* c) {
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (c->xg_on && lbk_xgmi_failed(c->xg)) {
+        snprintf(c->err, sizeof c->err, "xgmi exchange timed out waiting for a peer");
+        return -3;
+    }
     return 0;
+}
+
+int lbk_peer_handle(lbk_ctx* c, void* out) {
+    if (!c->xg) return -1;
+    return lbk_xgmi_handle(c->xg, out);
+}
+
+int lbk_peer_connect(lbk_ctx* c, const void* handles) {
+    if (!c->xg) return -1;
+    HIPCHK(c, hipSetDevice(c->device));
+    return lbk_xgmi_connect(c->xg, handles, c->stream, c->err, sizeof c->err);
+}
+
+int lbk_peer_enable(lbk_ctx* c, int on) {
+    if (on && !lbk_xgmi_connected(c->xg)) return -5;
+    c->xg_on = on ? 1 : 0;
+    return 0;
+}
+
+int lbk_exchange_backend(const lbk_ctx* c) {
+    if (c->geo.world <= 1) return 0;
+    if (c->grp) return 3;
+    if (c->xg_on) return 2;
+    return c->comm ? 1 : 0;
 }
 
 void lbk_prof_enable(lbk_ctx* c, int on) { c->prof_on = on; }

@@ -105,6 +105,10 @@ def lib():
                                   C.POINTER(C.c_double)]
     L.lbfgs_dev_twoloop.argtypes = [vp, dp, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), C.c_int,
                                     dp, C.POINTER(C.c_double)]
+    L.lbfgs_peer_handle.argtypes = [vp, C.c_char_p]
+    L.lbfgs_peer_connect.argtypes = [vp, C.c_char_p]
+    L.lbfgs_peer_enable.argtypes = [vp, C.c_int]
+    L.lbfgs_exchange_backend.argtypes = [vp]
     L.lbfgs_prof_enable.argtypes = [vp, C.c_int]
     L.lbfgs_prof_enable.restype = None
     L.lbfgs_prof_reset.argtypes = [vp]
@@ -123,8 +127,11 @@ EXPORTED_SYMBOLS = [
     "lbfgs_get_x", "lbfgs_sync", "lbfgs_messages", "lbfgs_trace_len", "lbfgs_trace_get",
     "lbfgs_dev_dot", "lbfgs_dev_norm", "lbfgs_dev_objective", "lbfgs_dev_trial",
     "lbfgs_dev_twoloop", "lbfgs_dev_elementwise", "lbfgs_line_search", "lbfgs_prof_enable",
-    "lbfgs_prof_reset", "lbfgs_prof_get",
+    "lbfgs_prof_reset", "lbfgs_prof_get", "lbfgs_peer_handle", "lbfgs_peer_connect", "lbfgs_peer_enable",
+    "lbfgs_exchange_backend",
 ]
+PEER_HANDLE_BYTES = 64
+BACKENDS = {0: "single", 1: "rccl", 2: "xgmi", 3: "host-group"}
 
 
 def constants(profile="config"):
@@ -224,6 +231,37 @@ class Context:
             self.close()
         except Exception:
             pass
+
+    # ---- sharded runs: xGMI peer exchange ----
+    def peer_handle(self):
+        buf = C.create_string_buffer(PEER_HANDLE_BYTES)
+        rc = lib().lbfgs_peer_handle(self.h, buf)
+        if rc != 0:
+            self._err("lbfgs_peer_handle", rc)
+        return buf.raw
+
+    def connect_peers(self, allgather, agree):
+        """Switch this sharded context's exchanges to the xGMI peer mailboxes.
+        allgather(bytes) -> list of every rank's bytes (rank order); agree(ok: bool) -> True iff
+        every rank passed (e.g. torch.distributed gloo all_gather_object / all_reduce MIN).
+        Returns (enabled, this rank's connect error or None); when a rank fails, no rank enables
+        and the context keeps its RCCL communicator (if it has one)."""
+        handles = allgather(self.peer_handle())
+        rc = lib().lbfgs_peer_connect(self.h, b"".join(handles))
+        msg = None
+        if rc != 0:
+            m = lib().lbfgs_last_error(self.h)
+            msg = f"lbfgs_peer_connect failed ({rc}): {m.decode() if m else ''}"
+        ok = agree(rc == 0)
+        if ok:
+            rc2 = lib().lbfgs_peer_enable(self.h, 1)
+            if rc2 != 0:
+                self._err("lbfgs_peer_enable", rc2)
+        return ok, msg
+
+    @property
+    def backend(self):
+        return BACKENDS.get(lib().lbfgs_exchange_backend(self.h), "unknown")
 
     def _err(self, what, rc):
         msg = lib().lbfgs_last_error(self.h)

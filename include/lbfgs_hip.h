@@ -127,10 +127,29 @@ typedef struct {
 /* n: global problem size; m: history length (1..64); device: HIP device ordinal. */
 int lbfgs_ctx_create(lbfgs_ctx** out, int64_t n, int m, int device);
 /* One process per GPU: shard the vectors across 'world' ranks (world | 8) with an RCCL
- * communicator created from 'unique_id' (128 bytes, from lbfgs_unique_id on rank 0). */
+ * communicator created from 'unique_id' (128 bytes, from lbfgs_unique_id on rank 0), and/or
+ * the xGMI peer exchange (lbfgs_peer_*). */
 int lbfgs_ctx_create_sharded(lbfgs_ctx** out, int64_t n, int m, int device, int rank, int world,
                              const void* unique_id);
 int lbfgs_unique_id(void* out128);
+/* unique_id may be NULL: no RCCL communicator; the context then exchanges its reductions only
+ * through the xGMI peer mailboxes below (lbfgs_peer_*), which must be connected and enabled
+ * before the first solve.
+ *
+ * xGMI peer exchange. Every sharded context owns a small mailbox in uncached device memory;
+ * a one-workgroup kernel stores the rank's group partials straight into every peer's mailbox
+ * and polls its own (no collective library on the solver's critical path).
+ * Bootstrap, on every rank: lbfgs_peer_handle -> all-gather the handles (any host channel,
+ * e.g. torch.distributed gloo) -> lbfgs_peer_connect (maps the peers, self-tests the exchange,
+ * up to ~30 s waiting for peers) -> agree on success across ranks -> lbfgs_peer_enable(1) on all
+ * or none. A peer that stops answering mid-solve ends the wait after 60 s (LBFGS_XGMI_TIMEOUT)
+ * with LBFGS_ERR_RCCL instead of a hang. */
+#define LBFGS_PEER_HANDLE_BYTES 64
+int lbfgs_peer_handle(lbfgs_ctx* ctx, void* out /* LBFGS_PEER_HANDLE_BYTES */);
+int lbfgs_peer_connect(lbfgs_ctx* ctx, const void* handles /* world x LBFGS_PEER_HANDLE_BYTES */);
+int lbfgs_peer_enable(lbfgs_ctx* ctx, int on);
+/* 0: one rank, 1: RCCL all-gathers, 2: xGMI peer mailboxes, 3: host group (emulated ranks) */
+int lbfgs_exchange_backend(const lbfgs_ctx* ctx);
 /* Emulated ranks: 'world' contexts driven by threads of ONE process (e.g. on one GPU, one
  * stream each) exchange their reductions through host memory instead of RCCL. Same data path
  * and results as the RCCL shards; used to test sharding on a single GPU. */

@@ -1,0 +1,88 @@
+"""Sharded solves over the xGMI peer exchange (lbfgs_xgmi.hip), one process per rank, no RCCL:
+bit-exact with the single-GPU trajectory.
+
+The box has one GPU, so every rank runs on device 0 and the mailboxes are IPC-mapped between
+processes of the same device: the kernel, wire format, epoch/parity protocol, bootstrap and
+self-test are exactly those of the cross-GPU case; only the xGMI hop itself is not exercised.
+"""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "cuda-lbfgs_amd"))
+import lbfgs_amd as L  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+WORKER = os.path.join(os.path.dirname(os.path.abspath(__file__)), "xgmi_worker.py")
+
+
+def bits(a):
+    return np.asarray(a, dtype=np.float64).view(np.uint64)
+
+
+def run_ranks(tmp_path, world, n, m, obj, ls, iters, mode, env=None):
+    e = dict(os.environ)
+    e.update(env or {})
+    procs = [subprocess.Popen([sys.executable, WORKER, str(tmp_path), str(r), str(world), str(n), str(m), obj, ls,
+                               str(iters), mode], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=e)
+             for r in range(world)]
+    outs = []
+    for p in procs:
+        try:
+            out, _ = p.communicate(timeout=240)
+        except subprocess.TimeoutExpired:  # pragma: no cover
+            for q in procs:
+                q.kill()
+            raise
+        outs.append(out)
+    for r, p in enumerate(procs):
+        assert p.returncode == 0, (r, outs[r][-3000:])
+    return [dict(np.load(os.path.join(tmp_path, f"out{r}.npz"))) for r in range(world)]
+
+
+@pytest.mark.parametrize("world,obj,ls,mode,ticket", [
+    (2, "rosenbrock", "backtracking", "default", "0"),
+    (2, "quad_tridiag", "wolfe", "default", "1"),
+    (4, "rosenbrock", "backtracking", "default", "1"),
+    (4, "rosenbrock", "wolfe", "default", "0"),
+    (2, "rosenbrock", "backtracking", "vf", "0"),
+    (4, "rosenbrock", "interpolation", "vf", "1"),
+])
+def test_xgmi_sharded_bit_exact(tmp_path, world, obj, ls, mode, ticket):
+    n = 4_000_003  # every one of up to 8 ranks owns segments
+    m, iters = 5, 12
+    x0 = L.x0_uniform(n, 42, -2.0, 2.0)
+    with L.Context(n, m) as c:
+        ref = c.minimize(obj, x0, ls, iters, trace=True, vector_free=(mode == "vf"))
+    outs = run_ranks(tmp_path, world, n, m, obj, ls, iters, mode, env={"LBFGS_TICKET": ticket})
+    x = np.zeros(n)
+    for r, o in enumerate(outs):
+        for key in ("tr_f", "tr_gnorm", "tr_alpha"):
+            assert np.array_equal(bits(o[key]), bits(ref[key])), (r, key)
+        assert np.array_equal(o["tr_c1"], ref["tr_c1"]) and np.array_equal(o["tr_c2"], ref["tr_c2"]), r
+        lo = int(o["lo"])
+        x[lo:lo + len(o["x"])] = o["x"]
+        assert str(o["messages"]) == ref["messages"]
+    assert np.array_equal(bits(x), bits(ref["x"]))
+
+
+def test_xgmi_silent_peer_times_out(tmp_path):
+    """A peer that publishes its handle but never exchanges must not hang the others: rank 0's
+    self-test gives up after its timeout (LBFGS_XGMI_SELFTEST_TIMEOUT) and no rank enables the
+    peer exchange."""
+    e = dict(os.environ, LBFGS_XGMI_SELFTEST_TIMEOUT="3")
+    args = [str(tmp_path), "", "2", "4000003", "5", "rosenbrock", "backtracking", "3", "default"]
+    procs = []
+    for r, mode in ((0, "default"), (1, "silent")):
+        a = list(args)
+        a[1], a[8] = str(r), mode
+        procs.append(subprocess.Popen([sys.executable, WORKER] + a, stdout=subprocess.PIPE,
+                                      stderr=subprocess.STDOUT, text=True, env=e))
+    outs = [p.communicate(timeout=180)[0] for p in procs]
+    assert procs[0].returncode == 3, outs[0][-2000:]
+    assert "timed out" in outs[0], outs[0][-2000:]
+    assert procs[1].returncode == 0, outs[1][-2000:]
