@@ -1740,8 +1740,15 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
     CK(hipDeviceSynchronize());
 #undef CK
     if (world > 1 && !grp) {
+        // the peer mailbox is an optional accelerator when an RCCL id is given: without it the
+        // context still runs on RCCL all-gathers
         const int xrc = lbk_xgmi_create(&c->xg, device, rank, world, LBK_WSLOT, c->err, sizeof c->err);
-        if (xrc != 0) return xrc;
+        if (xrc != 0) {
+            if (!nccl_id) return xrc;
+            fprintf(stderr, "lbfgs: %s; exchanges stay on RCCL\n", c->err);
+            c->xg = nullptr;
+            c->err[0] = 0;
+        }
         if (hipMalloc(&c->d_ckslot, sizeof(uint64_t) * LBK_GROUPS * 2) != hipSuccess) return -2;
     }
     if (world > 1 && !grp && nccl_id) {

@@ -246,12 +246,20 @@ class Context:
         every rank passed (e.g. torch.distributed gloo all_gather_object / all_reduce MIN).
         Returns (enabled, this rank's connect error or None); when a rank fails, no rank enables
         and the context keeps its RCCL communicator (if it has one)."""
-        handles = allgather(self.peer_handle())
-        rc = lib().lbfgs_peer_connect(self.h, b"".join(handles))
         msg = None
-        if rc != 0:
-            m = lib().lbfgs_last_error(self.h)
-            msg = f"lbfgs_peer_connect failed ({rc}): {m.decode() if m else ''}"
+        try:
+            mine = self.peer_handle()
+        except LbfgsError as e:  # no mailbox on this rank: every rank still joins the collectives
+            mine, msg = b"", str(e)
+        handles = allgather(mine)
+        if all(len(h) == PEER_HANDLE_BYTES for h in handles):
+            rc = lib().lbfgs_peer_connect(self.h, b"".join(handles))
+            if rc != 0:
+                m = lib().lbfgs_last_error(self.h)
+                msg = f"lbfgs_peer_connect failed ({rc}): {m.decode() if m else ''}"
+        else:
+            rc = -1
+            msg = msg or "a peer has no mailbox"
         ok = agree(rc == 0)
         if ok:
             rc2 = lib().lbfgs_peer_enable(self.h, 1)
