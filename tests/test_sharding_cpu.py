@@ -55,8 +55,13 @@ def _worker(rank, world, port, q):
     D.barrier()
     tmax = D.allreduce(1.0 + rank, "max")
     tsum = D.allreduce(2.0 * (rank + 1), "sum")
+    # the xGMI peer bootstrap's host channel: handle all-gather and the all-ranks-ok vote
+    hs = D.allgather_bytes(bytes([rank]) * 64)
+    vote_all = D.all_ok(True)
+    vote_one_fails = D.all_ok(rank != 1)
     D.close()
-    q.put((rank, uid == bytes(range(128)), tmax, tsum))
+    q.put((rank, uid == bytes(range(128)), tmax, tsum, hs == [bytes([0]) * 64, bytes([1]) * 64], vote_all,
+           vote_one_fails))
 
 
 def test_bench_distributed_bootstrap_gloo_world2():
@@ -74,3 +79,5 @@ def test_bench_distributed_bootstrap_gloo_world2():
     assert [r[1] for r in res] == [True, True]
     assert all(r[2] == 2.0 for r in res)  # max over ranks (bench's timing rule)
     assert all(r[3] == 6.0 for r in res)  # sum over ranks (bench's byte count)
+    assert all(r[4] for r in res)  # peer handles gathered in rank order
+    assert all(r[5] and not r[6] for r in res)  # one failing rank vetoes the peer exchange everywhere
