@@ -207,9 +207,19 @@ def measure(a, D, n, x0, dev, rank, world, uid, unfused=False, vector_free=False
             p = ctx.prof_get(kname)
             if p["launches"]:
                 prof[kname] = p
+    # sharded: the cost of one reduction exchange on this machine, per backend available on
+    # every rank (collective calls, same sequence everywhere): the two-loop issues ~2h + 3 of
+    # them per iteration, each on the critical path
+    lat = None
+    if world > 1 and not vector_free and not unfused:
+        lat = {}
+        backends = (["xgmi"] if backend == "xgmi" else []) + (["rccl"] if uid is not None else [])
+        for b in backends:
+            for k in (8, 96):
+                lat[f"{b}_{k * 8}doubles"] = round(ctx.exchange_latency(b, k, 200), 2)
     ctx.close()
     done_steps = a.steps if res["status"] == "running" else max(res["iterations"] - a.warmup, 1)
-    return T, res, prof, bytes_all, done_steps, backend
+    return T, res, prof, bytes_all, done_steps, (backend, lat)
 
 
 def roofline(prof, n, world):
@@ -242,7 +252,7 @@ def main():
     x0 = L.x0_uniform(n, 42, -2.0, 2.0)
     # BENCH_DEVICE_MOD=k maps rank -> device local_rank % k (rehearsing several ranks on fewer GPUs)
     dev = D.local_rank % int(os.environ["BENCH_DEVICE_MOD"]) if "BENCH_DEVICE_MOD" in os.environ else D.local_rank
-    T, res, prof, bytes_all, done_steps, backend = measure(a, D, n, x0, dev, rank, world, uid,
+    T, res, prof, bytes_all, done_steps, (backend, xlat) = measure(a, D, n, x0, dev, rank, world, uid,
                                                   unfused=a.unfused, vector_free=a.vector_free)
     # the opt-in vector-free mode alongside the default (outside the bit-parity contract with
     # the reference's operation order); sharded runs need a fresh RCCL id
@@ -307,6 +317,7 @@ def main():
             "achieved_hbm_gbps": round(bytes_all / T / 1e9, 1),
             "bytes_per_step": bytes_all / max(done_steps, 1),
             "roofline": roof,
+            "exchange_latency_us": xlat,
             "cpu_baseline": cpu,
             "solver": {"status": res["status"], "f": res["f"], "gnorm": res["gnorm"],
                        "trials_f": res["trials_f"], "commits": res["commits"],

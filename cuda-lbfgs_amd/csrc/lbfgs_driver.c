@@ -348,6 +348,14 @@ int lbfgs_peer_enable(lbfgs_ctx* c, int on) {
 
 int lbfgs_exchange_backend(const lbfgs_ctx* c) { return c ? lbk_exchange_backend(c->dev) : LBFGS_ERR_BAD_ARG; }
 
+int lbfgs_exchange_latency(lbfgs_ctx* c, int backend, int components, int iters, double* us) {
+    if (!c || !us) return LBFGS_ERR_BAD_ARG;
+    const int rc = lbk_exchange_bench(c->dev, backend, components, iters, us);
+    if (rc == 0) return 0;
+    snprintf(c->err, sizeof c->err, "%s", lbk_last_error(c->dev));
+    return rc == -1 ? LBFGS_ERR_BAD_ARG : rc == -5 ? LBFGS_ERR_STATE : rc == -3 ? LBFGS_ERR_RCCL : LBFGS_ERR_HIP;
+}
+
 /* ------------------------------------------------------------------------------------------
  * Host-callback objective helpers (LBFGS_OBJ_HOST; single rank)
  * ---------------------------------------------------------------------------------------- */

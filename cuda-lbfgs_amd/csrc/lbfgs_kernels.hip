@@ -36,6 +36,7 @@
 #include <cstdlib>
 #include <pthread.h>
 #include <cstring>
+#include <ctime>
 #include <new>
 #include <vector>
 
@@ -1554,10 +1555,8 @@ int prof_flush(lbk_ctx* c) {
 // Sharded runs: each rank owns groups [g_lo, g_hi) of every result slot; gather them so
 // every rank holds all 8 (one RCCL all-gather of (8/world) x KMAX doubles per reduction, in
 // place, on the solver stream), or through the host group for emulated ranks.
-int exchange_slot(lbk_ctx* c, int slot) {
-    const int ks = slot_stride(slot);
+int exchange_buf(lbk_ctx* c, double* base, int ks) {
     const int per = (c->geo.g_hi - c->geo.g_lo) * ks;
-    double* base = slot_base(c, slot);
     if (c->grp) {
         lbk_group* G = c->grp;
         HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -1586,6 +1585,8 @@ int exchange_slot(lbk_ctx* c, int slot) {
     }
     return 0;
 }
+
+int exchange_slot(lbk_ctx* c, int slot) { return exchange_buf(c, slot_base(c, slot), slot_stride(slot)); }
 
 // launch wrapper: byte accounting, optional event timing, all-gather of group partials
 template <class F>
@@ -2312,6 +2313,30 @@ int lbk_peer_enable(lbk_ctx* c, int on) {
     if (on && !lbk_xgmi_connected(c->xg)) return -5;
     c->xg_on = on ? 1 : 0;
     return 0;
+}
+
+int lbk_exchange_bench(lbk_ctx* c, int backend, int ks, int iters, double* us) {
+    if (c->geo.world <= 1 || c->grp || ks < 1 || ks > LBK_KW || iters < 1) return -1;
+    if (backend == 2 && !lbk_xgmi_connected(c->xg)) return -5;
+    if (backend == 1 && !c->comm) return -5;
+    if (backend != 1 && backend != 2) return -1;
+    const int saved = c->xg_on;
+    c->xg_on = backend == 2;
+    double* buf = nullptr;
+    HIPCHK(c, hipMalloc(&buf, sizeof(double) * LBK_WSLOT));
+    HIPCHK(c, hipMemsetAsync(buf, 0, sizeof(double) * LBK_WSLOT, c->stream));
+    int rc = exchange_buf(c, buf, ks);  // warm-up, also lines the ranks up
+    if (rc == 0 && hipStreamSynchronize(c->stream) != hipSuccess) rc = -2;
+    timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (int i = 0; i < iters && rc == 0; ++i) rc = exchange_buf(c, buf, ks);
+    if (rc == 0 && hipStreamSynchronize(c->stream) != hipSuccess) rc = -2;
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    c->xg_on = saved;
+    (void)hipFree(buf);
+    if (rc == 0 && backend == 2 && lbk_xgmi_failed(c->xg)) rc = -3;
+    *us = ((double)(t1.tv_sec - t0.tv_sec) * 1e6 + (double)(t1.tv_nsec - t0.tv_nsec) * 1e-3) / iters;
+    return rc;
 }
 
 int lbk_exchange_backend(const lbk_ctx* c) {

@@ -109,6 +109,7 @@ def lib():
     L.lbfgs_peer_connect.argtypes = [vp, C.c_char_p]
     L.lbfgs_peer_enable.argtypes = [vp, C.c_int]
     L.lbfgs_exchange_backend.argtypes = [vp]
+    L.lbfgs_exchange_latency.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_double)]
     L.lbfgs_prof_enable.argtypes = [vp, C.c_int]
     L.lbfgs_prof_enable.restype = None
     L.lbfgs_prof_reset.argtypes = [vp]
@@ -128,7 +129,7 @@ EXPORTED_SYMBOLS = [
     "lbfgs_dev_dot", "lbfgs_dev_norm", "lbfgs_dev_objective", "lbfgs_dev_trial",
     "lbfgs_dev_twoloop", "lbfgs_dev_elementwise", "lbfgs_line_search", "lbfgs_prof_enable",
     "lbfgs_prof_reset", "lbfgs_prof_get", "lbfgs_peer_handle", "lbfgs_peer_connect", "lbfgs_peer_enable",
-    "lbfgs_exchange_backend",
+    "lbfgs_exchange_backend", "lbfgs_exchange_latency",
 ]
 PEER_HANDLE_BYTES = 64
 BACKENDS = {0: "single", 1: "rccl", 2: "xgmi", 3: "host-group"}
@@ -266,6 +267,15 @@ class Context:
             if rc2 != 0:
                 self._err("lbfgs_peer_enable", rc2)
         return ok, msg
+
+    def exchange_latency(self, backend, components=8, iters=200):
+        """Collective: microseconds per exchange through 'rccl' or 'xgmi' (every rank calls)."""
+        us = C.c_double()
+        rc = lib().lbfgs_exchange_latency(self.h, {"rccl": 1, "xgmi": 2}[backend], int(components), int(iters),
+                                          C.byref(us))
+        if rc != 0:
+            self._err("lbfgs_exchange_latency", rc)
+        return us.value
 
     @property
     def backend(self):

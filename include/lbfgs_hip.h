@@ -150,6 +150,10 @@ int lbfgs_peer_connect(lbfgs_ctx* ctx, const void* handles /* world x LBFGS_PEER
 int lbfgs_peer_enable(lbfgs_ctx* ctx, int on);
 /* 0: one rank, 1: RCCL all-gathers, 2: xGMI peer mailboxes, 3: host group (emulated ranks) */
 int lbfgs_exchange_backend(const lbfgs_ctx* ctx);
+/* collective diagnostic (every rank calls it with the same arguments): `iters` back-to-back
+ * exchanges of a `components`-wide result slot (8 = a two-loop reduction, up to 96) through
+ * backend 1 (RCCL) or 2 (xGMI mailboxes); *us = host wall time per exchange */
+int lbfgs_exchange_latency(lbfgs_ctx* ctx, int backend, int components, int iters, double* us);
 /* Emulated ranks: 'world' contexts driven by threads of ONE process (e.g. on one GPU, one
  * stream each) exchange their reductions through host memory instead of RCCL. Same data path
  * and results as the RCCL shards; used to test sharding on a single GPU. */
