@@ -82,6 +82,7 @@ typedef struct {
     int64_t n_loc;   /* local elements */
     int g_lo, g_hi;  /* groups owned by this rank */
     int rank, world;
+    int vf_f;        /* vector-free commit segment = vf_f canonical segments (lbk_vf_factor) */
 } lbk_geo;
 
 typedef struct lbk_ctx lbk_ctx;
@@ -93,6 +94,9 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
                lbk_group* grp);
 /* canonical geometry and this rank's shard, no device needed (0, or < 0 if not shardable) */
 int lbk_geometry_plan(int64_t n, int rank, int world, lbk_geo* out);
+/* segments of the vector-free commit, in canonical segments: the largest F in {1, 2, 4, 8}
+ * with F L <= 8192 and ceil(n / (F L)) >= 1024 (restated as orc_vf_factor) */
+int lbk_vf_factor(int64_t n);
 lbk_group* lbk_group_create(int world);
 void lbk_group_destroy(lbk_group* g);
 /* sharded: the slot whose all-gather carries the neighbours' edge d (after lbk_last/negdot) */

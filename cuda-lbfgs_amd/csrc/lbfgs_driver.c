@@ -785,10 +785,13 @@ static int iterate(lbfgs_ctx* c) {
     c->a0 = c->K.initial_step;
     const int sharded = c->geo->world > 1;
     if (c->obj != LBFGS_OBJ_HOST && !c->unfused) {
-        /* single GPU: last two-loop pass + first trial at a0 + commit fused in one pass.
-         * Sharded: d is materialised first so that its edge values reach the neighbouring
-         * ranks (halo of the stencil) through the all-gather of its reduction slot. */
-        if (sharded) {
+        /* last two-loop pass + first trial at a0 + commit fused in one pass. Sharded, the
+         * stencil's halo of d at the rank edges comes from the neighbours' edge r (published
+         * with the last second-loop pass's reduction) and s_{h-1}'s ghost cells; d = -g is
+         * materialised first so that its edge values reach the neighbours through its slot. */
+        if (sharded && c->dmode == LBK_D_TWOLOOP) {
+            lbk_set_ghost_slot(c->dev, SLOT_B0(m) + h - 1);
+        } else if (sharded) {
             rc = materialize_d(c);
             if (rc) return rc;
         }

@@ -51,6 +51,7 @@ namespace {
 struct Geo {
     int64_t n, L, nseg, seg_lo, elem_lo, n_loc;
     int g_lo, g_hi;
+    int spg;            // segments per group (1024; fewer, longer segments in the vector-free commit)
     double* edge_slot;  // sharded: where d[0] / d[n_loc-1] of this rank are published
 };
 
@@ -149,7 +150,7 @@ __device__ __forceinline__ int64_t row_off(const Seg& s, int u) {
 // boundary (reduce-kernel mode).
 template <int K, bool ATOMIC>
 __device__ __forceinline__ void group_tree(const double* partials, int64_t lbase, int64_t gseg0, int64_t nseg,
-                                           double* slot_g, double (&lds)[4][K > 0 ? K : 1]) {
+                                           int spg, double* slot_g, double (&lds)[4][K > 0 ? K : 1]) {
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     double q[K];
     // components in chunks of 8 with every load of a chunk issued before the first butterfly:
@@ -167,7 +168,7 @@ __device__ __forceinline__ void group_tree(const double* partials, int64_t lbase
             for (int i = 0; i < 4; ++i) {
                 const int64_t j = 4 * t + i;
                 const double* src = partials + (int64_t)(k0 + kc) * LBK_SEGS + lbase + j;
-                if (gseg0 + j < nseg)
+                if (j < spg && gseg0 + j < nseg)
                     p[kc][i] = ATOMIC ? bitsd(__hip_atomic_load(reinterpret_cast<const unsigned long long*>(src),
                                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
                                       : *src;
@@ -214,7 +215,7 @@ __device__ __forceinline__ void reduce_publish(double (&acc)[K], const Geo& geo,
     __syncthreads();
     const int64_t b = blockIdx.x;
     const int64_t sg = geo.seg_lo + b;
-    const int g = (int)(sg / LBK_SEG_PER_GROUP);
+    const int g = (int)(sg / geo.spg);
     if (!red.ticket) {
         if (t == 0) {
 #pragma unroll
@@ -232,16 +233,16 @@ __device__ __forceinline__ void reduce_publish(double (&acc)[K], const Geo& geo,
                                dbits(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const int64_t hi = min(geo.nseg, (int64_t)(g + 1) * LBK_SEG_PER_GROUP);
-        const unsigned expect = (unsigned)(hi - (int64_t)g * LBK_SEG_PER_GROUP);
+        const int64_t hi = min(geo.nseg, (int64_t)(g + 1) * geo.spg);
+        const unsigned expect = (unsigned)(hi - (int64_t)g * geo.spg);
         const unsigned old = __hip_atomic_fetch_add(red.cnt + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         last_flag = (old + 1u == expect);
     }
     __syncthreads();
     if (!last_flag) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const int64_t gseg0 = (int64_t)g * LBK_SEG_PER_GROUP;
-    group_tree<K, true>(red.partials, gseg0 - geo.seg_lo, gseg0, geo.nseg, red.slot + g * red.kstride, lds);
+    const int64_t gseg0 = (int64_t)g * geo.spg;
+    group_tree<K, true>(red.partials, gseg0 - geo.seg_lo, gseg0, geo.nseg, geo.spg, red.slot + g * red.kstride, lds);
     if (t == 0) __hip_atomic_store(red.cnt + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -251,8 +252,8 @@ __global__ __launch_bounds__(LB_BLOCK) void k_group_reduce(const double* __restr
                                                            double* __restrict__ slot, int kstride) {
     __shared__ double lds[4][K];
     const int g = geo.g_lo + (int)blockIdx.x;
-    const int64_t gseg0 = (int64_t)g * LBK_SEG_PER_GROUP;
-    group_tree<K, false>(partials, gseg0 - geo.seg_lo, gseg0, geo.nseg, slot + g * kstride, lds);
+    const int64_t gseg0 = (int64_t)g * geo.spg;
+    group_tree<K, false>(partials, gseg0 - geo.seg_lo, gseg0, geo.nseg, geo.spg, slot + g * kstride, lds);
 }
 
 // The same stage 2 for a runtime number of components (wide slots): blockIdx.y takes
@@ -265,7 +266,7 @@ __global__ __launch_bounds__(LB_BLOCK) void k_group_reduce_wide(const double* __
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int g = geo.g_lo + (int)blockIdx.x;
     const int k0 = KC * (int)blockIdx.y;
-    const int64_t gseg0 = (int64_t)g * LBK_SEG_PER_GROUP;
+    const int64_t gseg0 = (int64_t)g * geo.spg;
     const int64_t lbase = gseg0 - geo.seg_lo;
     double p[KC][4];
 #pragma unroll
@@ -273,7 +274,7 @@ __global__ __launch_bounds__(LB_BLOCK) void k_group_reduce_wide(const double* __
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int64_t j = 4 * t + i;
-            p[c][i] = (k0 + c < K && gseg0 + j < geo.nseg) ? partials[(int64_t)(k0 + c) * LBK_SEGS + lbase + j] : 0.0;
+            p[c][i] = (k0 + c < K && j < geo.spg && gseg0 + j < geo.nseg) ? partials[(int64_t)(k0 + c) * LBK_SEGS + lbase + j] : 0.0;
         }
 #pragma unroll
     for (int c = 0; c < KC; ++c) {
@@ -491,12 +492,27 @@ struct OpAxpyDot {  // q = qin - alpha y;  acc += s . q       (lbfgs.cpp:133-137
     }
 };
 
+// Sharded runs: the rank's first and last value of a pass's output vector (d, or the r of the
+// last second-loop pass) are written into spare components of the pass's result slot (group
+// g_lo comp 1, group g_hi-1 comp 2), which the slot exchange delivers to the neighbouring
+// ranks as their halo.
+__device__ __forceinline__ void publish_edges(double* edge_slot, int64_t i, int64_t n_loc, int g_lo, int g_hi,
+                                              double2 d, bool v0, bool v1) {
+    if (!edge_slot) return;
+    if (i == 0 && v0) edge_slot[g_lo * LBK_KMAX + 1] = d.x;
+    if (i + 1 == n_loc - 1 && v1) edge_slot[(g_hi - 1) * LBK_KMAX + 2] = d.y;
+    if (i == n_loc - 1 && v0) edge_slot[(g_hi - 1) * LBK_KMAX + 2] = d.x;
+}
+
 template <bool NT>
 struct OpMid {  // r = (qin - alpha0 y0) * gamma;  acc += y0 . r      (:134-137, :150-154, :160)
     double* __restrict__ rout;
     const double* __restrict__ qin;
     const double* __restrict__ y0;
     double alpha, gamma;
+    double* edge_slot;  // sharded: this rank's edge r for the neighbours' commit halo
+    int64_t n_loc;
+    int g_lo, g_hi;
     struct Row {
         double2 q, y;
     };
@@ -510,6 +526,7 @@ struct OpMid {  // r = (qin - alpha0 y0) * gamma;  acc += y0 . r      (:134-137,
         rr.x = (r.q.x - alpha * r.y.x) * gamma;
         rr.y = (r.q.y - alpha * r.y.y) * gamma;
         st2<MASK, NT>(rout + i, rr, v0, v1);
+        publish_edges(edge_slot, i, n_loc, g_lo, g_hi, rr, v0, v1);
         acc[0] = fma2<MASK>(r.y, rr, acc[0], v0, v1);
     }
 };
@@ -521,6 +538,9 @@ struct OpAxpy2Dot {  // r += s (alpha - beta);  acc += ynext . r      (:159-164)
     const double* __restrict__ s;
     const double* __restrict__ yn;
     double coef;
+    double* edge_slot;  // sharded: this rank's edge r for the neighbours' commit halo
+    int64_t n_loc;
+    int g_lo, g_hi;
     struct Row {
         double2 r, s, y;
     };
@@ -535,20 +555,10 @@ struct OpAxpy2Dot {  // r += s (alpha - beta);  acc += ynext . r      (:159-164)
         rn.x = w.r.x + w.s.x * coef;
         rn.y = w.r.y + w.s.y * coef;
         st2<MASK, NT>(r + i, rn, v0, v1);
+        publish_edges(edge_slot, i, n_loc, g_lo, g_hi, rn, v0, v1);
         acc[0] = fma2<MASK>(w.y, rn, acc[0], v0, v1);
     }
 };
-
-// Sharded runs: the rank's first and last d are written into spare components of the
-// result slot (group g_lo comp 1, group g_hi-1 comp 2), which the slot all-gather delivers
-// to the neighbouring ranks as their halo of d.
-__device__ __forceinline__ void publish_edges(double* edge_slot, int64_t i, int64_t n_loc, int g_lo, int g_hi,
-                                              double2 d, bool v0, bool v1) {
-    if (!edge_slot) return;
-    if (i == 0 && v0) edge_slot[g_lo * LBK_KMAX + 1] = d.x;
-    if (i + 1 == n_loc - 1 && v1) edge_slot[(g_hi - 1) * LBK_KMAX + 2] = d.y;
-    if (i == n_loc - 1 && v0) edge_slot[(g_hi - 1) * LBK_KMAX + 2] = d.x;
-}
 
 template <bool NT>
 struct OpLast {  // d = -(r + s (alpha - beta));  acc += g . d        (:163-171)
@@ -631,7 +641,8 @@ __global__ __launch_bounds__(LB_BLOCK) void k_mid(double* __restrict__ rout, con
                                                   const double* __restrict__ y0, double rho0, double gamma,
                                                   const double* __restrict__ prev, Geo geo, Red red) {
     const double alpha = rho0 * slot_total(prev);
-    run_pass<OpMid<NT>, 1>(OpMid<NT>{rout, qin, y0, alpha, gamma}, geo, red);
+    run_pass<OpMid<NT>, 1>(OpMid<NT>{rout, qin, y0, alpha, gamma, geo.edge_slot, geo.n_loc, geo.g_lo, geo.g_hi}, geo,
+                           red);
 }
 
 // beta = rho * total(pb), alpha = rho * total(pa)
@@ -642,7 +653,8 @@ __global__ __launch_bounds__(LB_BLOCK) void k_axpy2_dot(double* r, const double*
                                                         Geo geo, Red red) {
     const double beta = rho * slot_total(pb);
     const double alpha = rho * slot_total(pa);
-    run_pass<OpAxpy2Dot<NT>, 1>(OpAxpy2Dot<NT>{r, rin, sv, yn, alpha - beta}, geo, red);
+    run_pass<OpAxpy2Dot<NT>, 1>(
+        OpAxpy2Dot<NT>{r, rin, sv, yn, alpha - beta, geo.edge_slot, geo.n_loc, geo.g_lo, geo.g_hi}, geo, red);
 }
 
 template <bool NT>
@@ -728,6 +740,8 @@ __device__ __forceinline__ double halo_z(const double* __restrict__ x, const Dir
                     double dh;
                     if (DMODE == LBK_D_BUF && da.ghost && (hi == -1 || hi == n_loc))
                         dh = ghost_d(da, hi, n_loc);
+                    else if (DMODE == LBK_D_TWOLOOP && da.ghost && (hi == -1 || hi == n_loc))
+                        dh = -(ghost_d(da, hi, n_loc) + da.s[hi] * da.coef);  // neighbour's edge r, s ghost
                     else
                         dh = load_dir1<DMODE>(da, hi);
                     zh = x[hi] + alpha * dh;
@@ -858,11 +872,25 @@ __global__ __launch_bounds__(LB_BLOCK) void k_commit(const double* __restrict__ 
         const double alph = da.rho * slot_total(da.pa);
         da.coef = alph - beta;  // r[j] += s[j] * (alpha[i] - beta)  (lbfgs.cpp:137)
     }
-    // sharded: keep the x ghosts current (x_new = x + alpha d at the neighbours' edge elements)
-    if (DMODE == LBK_D_BUF && da.ghost && threadIdx.x == 0) {
-        if (blockIdx.x == 0 && geo.elem_lo > 0) xn[-1] = x[-1] + alpha * ghost_d(da, -1, geo.n_loc);
-        if (blockIdx.x == gridDim.x - 1 && geo.elem_lo + geo.n_loc < geo.n)
-            xn[geo.n_loc] = x[geo.n_loc] + alpha * ghost_d(da, geo.n_loc, geo.n_loc);
+    // sharded: keep the x and s ghosts current (x_new = x + alpha d and s = x_new - x at the
+    // neighbours' edge elements: the owner's operands, so the owner's bits). The s ghosts let a
+    // later TWOLOOP commit form the neighbours' edge d from their published edge r.
+    if ((DMODE == LBK_D_BUF || DMODE == LBK_D_TWOLOOP) && da.ghost && threadIdx.x == 0) {
+        if (blockIdx.x == 0 && geo.elem_lo > 0) {
+            const double dh = DMODE == LBK_D_BUF ? ghost_d(da, -1, geo.n_loc)
+                                                 : -(ghost_d(da, -1, geo.n_loc) + da.s[-1] * da.coef);
+            const double z = x[-1] + alpha * dh;
+            xn[-1] = z;
+            so[-1] = z - x[-1];
+        }
+        if (blockIdx.x == gridDim.x - 1 && geo.elem_lo + geo.n_loc < geo.n) {
+            const int64_t e = geo.n_loc;
+            const double dh = DMODE == LBK_D_BUF ? ghost_d(da, e, geo.n_loc)
+                                                 : -(ghost_d(da, e, geo.n_loc) + da.s[e] * da.coef);
+            const double z = x[e] + alpha * dh;
+            xn[e] = z;
+            so[e] = z - x[e];
+        }
     }
     run_pass<OpCommit<OBJ, DMODE, NT>, 7>(OpCommit<OBJ, DMODE, NT>{x, da, alpha, xn, gn, so, yo, geo.n, geo.n_loc}, geo, red);
 }
@@ -1490,8 +1518,29 @@ Geo kgeo(const lbk_ctx* c) {
     g.n_loc = c->geo.n_loc;
     g.g_lo = c->geo.g_lo;
     g.g_hi = c->geo.g_hi;
+    g.spg = LBK_SEG_PER_GROUP;
     g.edge_slot = nullptr;
     return g;
+}
+
+// Geometry of the vector-free commit (ORC_CANON_VF): segments of F canonical segments
+// (F = lbk_geo.vf_f, a function of n only), 1024 / F of them per group, so a rank owns the same
+// elements in both geometries. Short canonical segments (n <= ~1e7) leave each wave of the
+// vector-free commit only 1-3 rows, and its fixed costs per segment (the two wave-run edges,
+// a 4h+7-component reduction) dominate; F up to 8 restores runs of ~10 rows.
+Geo vgeo(const lbk_ctx* c) {
+    Geo g = kgeo(c);
+    const int F = c->geo.vf_f;
+    if (F <= 1) return g;
+    g.L = c->geo.L * F;
+    g.nseg = (c->geo.n + g.L - 1) / g.L;
+    g.spg = LBK_SEG_PER_GROUP / F;
+    g.seg_lo = std::min<int64_t>((int64_t)c->geo.g_lo * g.spg, g.nseg);
+    return g;
+}
+
+int geo_blocks(const lbk_ctx* c, const Geo& g) {
+    return (int)(std::min<int64_t>((int64_t)c->geo.g_hi * g.spg, g.nseg) - g.seg_lo);
 }
 
 // regular slots 0..LBK_NSLOTS-1 (LBK_KMAX components), wide slots LBK_WSLOT0 + w (LBK_KW)
@@ -1590,7 +1639,8 @@ int exchange_slot(lbk_ctx* c, int slot) { return exchange_buf(c, slot_base(c, sl
 
 // launch wrapper: byte accounting, optional event timing, all-gather of group partials
 template <class F>
-int launch(lbk_ctx* c, int kind, double vec_passes, int slot, F&& fn, int K = 1, bool exchange = true) {
+int launch(lbk_ctx* c, int kind, double vec_passes, int slot, F&& fn, int K = 1, bool exchange = true,
+           const Geo* gv = nullptr) {
     const double bytes = vec_passes * 8.0 * (double)c->geo.n_loc;
     c->bytes_total += bytes;
     hipEvent_t a = nullptr, b = nullptr;
@@ -1605,7 +1655,7 @@ int launch(lbk_ctx* c, int kind, double vec_passes, int slot, F&& fn, int K = 1,
         HIPCHK(c, hipGetLastError());
     }
     if (slot >= 0 && !c->ticket) {
-        const Geo g = kgeo(c);
+        const Geo g = gv ? *gv : kgeo(c);
         double* sl = slot_base(c, slot);
         const int ks = slot_stride(slot);
         const dim3 grid(c->geo.g_hi - c->geo.g_lo), blk(LB_BLOCK);
@@ -1654,6 +1704,20 @@ int lbk_unique_id(void* out128) {
     return 0;
 }
 
+int lbk_vf_factor(int64_t n) {
+    const int64_t per = (n + LBK_SEGS - 1) / LBK_SEGS;
+    int64_t L = ((per + 127) / 128) * 128;
+    if (L < 512) L = 512;
+    int F = 1;
+#ifdef LBK_VF_FMAX  // experiments: cap the factor (1 = the original vector-free geometry)
+    const int fmax = LBK_VF_FMAX;
+#else
+    const int fmax = 8;
+#endif
+    while (F < fmax && 2 * F * L <= 8192 && (n + 2 * F * L - 1) / (2 * F * L) >= 1024) F *= 2;
+    return F;
+}
+
 int lbk_geometry_plan(int64_t n, int rank, int world, lbk_geo* out) {
     if (n < 1 || world < 1 || (LBK_GROUPS % world) != 0 || rank < 0 || rank >= world) return -1;
     lbk_geo& G = *out;
@@ -1676,6 +1740,7 @@ int lbk_geometry_plan(int64_t n, int rank, int world, lbk_geo* out) {
     G.elem_lo = std::min<int64_t>(G.seg_lo * G.L, n);
     const int64_t elem_hi = std::min<int64_t>(G.seg_hi * G.L, n);
     G.n_loc = elem_hi - G.elem_lo;
+    G.vf_f = lbk_vf_factor(n);
     // every rank must own at least one segment (n > (8 - 8/world) * 1024 * L)
     if (world > 1 && (G.nseg <= (int64_t)(LBK_GROUPS - LBK_GROUPS / world) * LBK_SEG_PER_GROUP)) return -7;
     return 0;
@@ -1884,6 +1949,7 @@ int lbk_mid(lbk_ctx* c, double* rout, const double* qin, const double* y0, doubl
     Geo g = kgeo(c);
     Red r = kred(c, slot);
     const double* pa = sref(c, ref_alpha);
+    if (c->geo.world > 1) g.edge_slot = r.slot;
     return launch(c, LBK_K_MID, 3, slot, [&] {
         NT_DISPATCH(c, hipLaunchKernelGGL(k_mid<NT_>, dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, rout, qin, y0, rho0, gamma, pa, g, r));
     });
@@ -1895,6 +1961,7 @@ int lbk_axpy2_dot(lbk_ctx* c, double* rr, const double* rin, const double* s, co
     Red r = kred(c, slot);
     const double* pb = sref(c, ref_beta);
     const double* pa = sref(c, ref_alpha);
+    if (c->geo.world > 1) g.edge_slot = r.slot;
     return launch(c, LBK_K_AXPY2_DOT, 4, slot, [&] {
         NT_DISPATCH(c, hipLaunchKernelGGL(k_axpy2_dot<NT_>, dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, rr, rin, s, ynext, rho, pb, pa, g, r));
     });
@@ -1971,7 +2038,7 @@ int lbk_commit(lbk_ctx* c, int obj, int dmode, const double* x, const double* ds
     Geo g = kgeo(c);
     Red r = kred(c, slot);
     DirArgs da = {dsrc, s_last, gg, 0.0, nullptr, nullptr, rho,
-                  dmode == LBK_D_BUF ? ghost_ptr(c) : nullptr, c->geo.g_lo, c->geo.g_hi};
+                  (dmode == LBK_D_BUF || dmode == LBK_D_TWOLOOP) ? ghost_ptr(c) : nullptr, c->geo.g_lo, c->geo.g_hi};
     if (dmode == LBK_D_TWOLOOP) {
         da.pa = sref(c, ref_alpha);
         da.pb = sref(c, ref_beta);
@@ -2040,17 +2107,18 @@ template <int HB>
 int vf_commit_hb(lbk_ctx* c, int obj, int h, const double* x, const double* g, const double* const* S,
                  const double* const* Y, const double* cs, const double* cy, double cg, double alpha,
                  const double* cand, double* xn, double* gn, double* so, double* yo, int wslot) {
-    Geo geo = kgeo(c);
+    Geo geo = vgeo(c);
     Red r = kred(c, wslot);
     const VfBasis<HB> B = vf_basis<HB>(h, S, Y, cs, cy, cg);
     constexpr int K = LBK_VF_YB + 4 * HB + LBK_VF_NA;
     const int rc = launch(c, LBK_K_VF_COMMIT, 2.0 * h + 6.0, wslot, [&] {
         OBJ_DISPATCH(obj, {
             OpVfCommit<O_, HB, NT_> op{x, g, B, alpha, {cand[0]}, xn, gn, so, yo, geo.n, geo.n_loc};
-            hipLaunchKernelGGL((k_vf_commit<O_, HB, NT_>), dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, op, geo, r);
+            hipLaunchKernelGGL((k_vf_commit<O_, HB, NT_>), dim3(geo_blocks(c, geo)), dim3(LB_BLOCK), 0, c->stream, op,
+                               geo, r);
         });
         return 0;
-    }, K, false);
+    }, K, false, &geo);
     if (rc || c->geo.world == 1) return rc;
     return vf_exchange_ghosts(c, wslot, xn, gn, so, yo);
 }

@@ -99,6 +99,17 @@ void orc_canon_geometry(int64_t n, int64_t* seg_len, int64_t* nseg) {
     *nseg = (n + L - 1) / L;
 }
 
+/* The vector-free commit's segments (lbfgs_kernels.hip vgeo / lbk_vf_factor): F canonical
+ * segments each, F the largest of {1, 2, 4, 8} with F L <= 8192 and ceil(n / (F L)) >= 1024;
+ * 1024 / F of them per group, placed first in the group's 1024-entry tree (0.0 behind). */
+int orc_vf_factor(int64_t n) {
+    int64_t L, nseg;
+    orc_canon_geometry(n, &L, &nseg);
+    int F = 1;
+    while (F < 8 && 2 * F * L <= 8192 && (n + 2 * F * L - 1) / (2 * F * L) >= 1024) F *= 2;
+    return F;
+}
+
 static double tree_sum(double* a, int count) { /* balanced, natural order, in place */
     for (int w = count; w > 1; w >>= 1)
         for (int j = 0; j < w / 2; ++j) a[j] = a[2 * j] + a[2 * j + 1];
@@ -114,6 +125,13 @@ static void canon_groups_mode(const double* a, const double* b, int64_t n, int64
                               double* q8) {
     int64_t L, nseg;
     orc_canon_geometry(n, &L, &nseg);
+    int64_t spg = CANON_SEG_PER_GROUP;
+    if (contig) {
+        const int F = orc_vf_factor(n);
+        L *= F;
+        nseg = (n + L - 1) / L;
+        spg /= F;
+    }
     double* segp = (double*)calloc(CANON_SEGS, sizeof(double));
     double acc[256];
     for (int64_t s = 0; s < nseg; ++s) {
@@ -141,7 +159,7 @@ static void canon_groups_mode(const double* a, const double* b, int64_t n, int64
             }
             acc[t] = v;
         }
-        segp[s] = tree_sum(acc, 256);
+        segp[(s / spg) * CANON_SEG_PER_GROUP + s % spg] = tree_sum(acc, 256);
     }
     for (int g = 0; g < CANON_GROUPS; ++g) q8[g] = tree_sum(segp + g * CANON_SEG_PER_GROUP, CANON_SEG_PER_GROUP);
     free(segp);

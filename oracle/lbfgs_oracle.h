@@ -56,6 +56,7 @@ void orc_x0_uniform(double* x, int64_t n, uint32_t seed, double lo, double hi);
 double orc_dot(const double* a, const double* b, int64_t n, int mode);
 double orc_sum(const double* t, int64_t n, int64_t limit, int mode); /* terms t[e], e < limit */
 void orc_canon_geometry(int64_t n, int64_t* seg_len, int64_t* nseg);
+int orc_vf_factor(int64_t n); /* vector-free commit segment, in canonical segments */
 /* group partials Q_0..Q_7 of the canonical order (total = sequential sum of the 8). */
 void orc_canon_dot_groups(const double* a, const double* b, int64_t n, double* q8);
 

@@ -113,6 +113,12 @@ def geometry(n):
     return L.value, ns.value
 
 
+def vf_factor(n):
+    """canonical segments per vector-free commit segment (orc_vf_factor)"""
+    lib().orc_vf_factor.argtypes = [C.c_int64]
+    return lib().orc_vf_factor(n)
+
+
 def f(obj, x, mode=CANON):
     return lib().orc_f(OBJ[obj], np.ascontiguousarray(x, np.float64), len(x), mode)
 

@@ -102,3 +102,16 @@ int main() {
     subprocess.run(["g++", "-std=c++17", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe),
                     L.LIB_PATH, "-Wl,-rpath," + PKG], check=True, capture_output=True)
     assert exe.exists()
+
+
+@pytest.mark.parametrize("n,F", [(10_000, 1), (1_000_000, 1), (1_500_000, 2), (2_200_000, 4), (3_000_000, 4),
+                                 (4_000_003, 4), (4_194_304, 8), (10_000_000, 4), (20_000_000, 2), (40_000_000, 1),
+                                 (100_000_000, 1), (1_000_000_000, 1)])
+def test_vector_free_segment_factor_matches_oracle(n, F):
+    """The vector-free commit's segment length (F canonical segments) is a function of n only,
+    stated once in the library (lbk_vf_factor) and once in the oracle (orc_vf_factor)."""
+    _ensure_built()
+    lib = ctypes.CDLL(L.LIB_PATH)
+    lib.lbk_vf_factor.argtypes = [ctypes.c_int64]
+    assert lib.lbk_vf_factor(n) == F
+    assert O.vf_factor(n) == F

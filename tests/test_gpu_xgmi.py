@@ -51,6 +51,8 @@ def run_ranks(tmp_path, world, n, m, obj, ls, iters, mode, env=None):
     (4, "rosenbrock", "wolfe", "default", "0"),
     (2, "rosenbrock", "backtracking", "vf", "0"),
     (4, "rosenbrock", "interpolation", "vf", "1"),
+    (8, "rosenbrock", "backtracking", "default", "1"),
+    (8, "quad_tridiag", "wolfe", "vf", "0"),
 ])
 def test_xgmi_sharded_bit_exact(tmp_path, world, obj, ls, mode, ticket):
     n = 4_000_003  # every one of up to 8 ranks owns segments
