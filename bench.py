@@ -55,6 +55,8 @@ def parse():
                    help="Gram-matrix two-loop, one fused pass per iteration (opt-in mode)")
     p.add_argument("--no-vector-free", action="store_true",
                    help="skip the vector-free measurement reported beside the default mode")
+    p.add_argument("--no-config4", action="store_true",
+                   help="8 ranks: skip the n=1e9 measurement (BASELINE configs[4]) after the headline")
     p.add_argument("--exchange", choices=["xgmi", "rccl"], default="xgmi",
                    help="sharded runs: reductions through the xGMI peer mailboxes (falls back to RCCL "
                         "when any rank's self-test fails) or RCCL all-gathers")
@@ -222,6 +224,67 @@ def measure(a, D, n, x0, dev, rank, world, uid, unfused=False, vector_free=False
     return T, res, prof, bytes_all, done_steps, (backend, lat)
 
 
+def config4(a, D, dev, rank, world):
+    """BASELINE configs[4]: Rosenbrock n = 1e9, m = 10, sharded over 8 GPUs, default mode, the
+    xGMI peer exchange (no RCCL communicator: a rank that fails early cannot strand the others in
+    a collective init). Every rank generates the full x0 (std::mt19937(42), as everywhere) and
+    uploads its slice. Each step that can fail is followed by a gloo vote, so all ranks skip
+    together."""
+    n9 = 10 ** 9
+    t0 = time.perf_counter()
+    try:
+        x0 = L.x0_uniform(n9, 42, -2.0, 2.0)
+    except MemoryError:
+        x0 = None
+    if not D.all_ok(x0 is not None):
+        return {"skipped": "x0 allocation failed on a rank"}
+    gen_s = time.perf_counter() - t0
+    ctx, err = None, None
+    try:
+        ctx = L.Context(n9, a.history, device=dev, rank=rank, world=world, uid=None)
+    except L.LbfgsError as e:
+        err = str(e)
+    if not D.all_ok(ctx is not None):
+        if ctx:
+            ctx.close()
+        return {"skipped": f"context creation failed on a rank ({err})"}
+    ok, msg = ctx.connect_peers(D.allgather_bytes, D.all_ok)
+    if not ok:
+        ctx.close()
+        return {"skipped": f"xGMI peer exchange unavailable ({msg})"}
+    res, T, err = None, None, None
+    try:
+        ctx.init(a.objective, x0, a.line_search, tolerance=1e-5)
+        del x0
+        ctx.step(a.warmup)
+        ctx.sync()
+    except L.LbfgsError as e:
+        err = str(e)
+    if D.all_ok(err is None):
+        D.barrier()
+        t1 = time.perf_counter()
+        try:
+            res = ctx.step(a.steps)
+            ctx.sync()
+        except L.LbfgsError as e:
+            err = str(e)
+        t_local = time.perf_counter() - t1
+        D.barrier()
+        T = D.allreduce(t_local, "max")
+        bytes_all = D.allreduce(res["bytes"] if res else 0.0, "sum")
+    ok = D.all_ok(err is None and res is not None)
+    ctx.close()
+    if not ok:
+        return {"skipped": f"solve failed on a rank ({err})"}
+    steps = a.steps if res["status"] == "running" else max(res["iterations"] - a.warmup, 1)
+    return {"workload": f"{a.objective} n=1e9 m={a.history} {a.line_search}, sharded over {world} GPUs "
+                        "(BASELINE configs[4])",
+            "value": round(steps / T, 4), "unit": "iters/s", "steps": steps, "warmup": a.warmup,
+            "ms_per_step": round(T / steps * 1e3, 4), "achieved_hbm_gbps": round(bytes_all / T / 1e9, 1),
+            "exchange": "xgmi", "x0_generation_s": round(gen_s, 1),
+            "solver": {"status": res["status"], "f": res["f"], "gnorm": res["gnorm"]}}
+
+
 def roofline(prof, n, world):
     if not prof:
         return None
@@ -273,6 +336,9 @@ def main():
         except L.LbfgsError as e:
             vf = {"error": str(e)}
     del x0
+    c4 = None
+    if world == 8 and n == 10 ** 8 and not (a.unfused or a.vector_free or a.no_config4):
+        c4 = config4(a, D, dev, rank, world)
 
     out = None
     if rank == 0:
@@ -323,6 +389,7 @@ def main():
                        "trials_f": res["trials_f"], "commits": res["commits"],
                        "passes": res["passes"]},
             "vector_free": vf,
+            "config4_n1e9": c4,
         }
         print(json.dumps(out), flush=True)
     D.close()
