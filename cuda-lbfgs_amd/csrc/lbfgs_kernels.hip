@@ -52,6 +52,7 @@ struct Geo {
     int64_t n, L, nseg, seg_lo, elem_lo, n_loc;
     int g_lo, g_hi;
     int spg;            // segments per group (1024; fewer, longer segments in the vector-free commit)
+    int rev;            // 1: workgroup b takes the rank's segment nblocks-1-b (see LBFGS_REV)
     double* edge_slot;  // sharded: where d[0] / d[n_loc-1] of this rank are published
 };
 
@@ -124,9 +125,14 @@ struct Seg {
     int lane, w;
 };
 
+// this workgroup's segment, relative to the rank's first: launch order or reversed
+__device__ __forceinline__ int64_t seg_block(const Geo& geo) {
+    return geo.rev ? (int64_t)gridDim.x - 1 - blockIdx.x : (int64_t)blockIdx.x;
+}
+
 __device__ __forceinline__ Seg seg_setup(const Geo& geo) {
     Seg s;
-    const int64_t sg = geo.seg_lo + blockIdx.x;
+    const int64_t sg = geo.seg_lo + seg_block(geo);
     s.sbeg = sg * geo.L;
     const int64_t send = min(s.sbeg + geo.L, geo.n);
     s.len = send - s.sbeg;
@@ -213,7 +219,7 @@ __device__ __forceinline__ void reduce_publish(double (&acc)[K], const Geo& geo,
         for (int k = 0; k < K; ++k) lds[w][k] = acc[k];
     }
     __syncthreads();
-    const int64_t b = blockIdx.x;
+    const int64_t b = seg_block(geo);
     const int64_t sg = geo.seg_lo + b;
     const int g = (int)(sg / geo.spg);
     if (!red.ticket) {
@@ -876,14 +882,14 @@ __global__ __launch_bounds__(LB_BLOCK) void k_commit(const double* __restrict__ 
     // neighbours' edge elements: the owner's operands, so the owner's bits). The s ghosts let a
     // later TWOLOOP commit form the neighbours' edge d from their published edge r.
     if ((DMODE == LBK_D_BUF || DMODE == LBK_D_TWOLOOP) && da.ghost && threadIdx.x == 0) {
-        if (blockIdx.x == 0 && geo.elem_lo > 0) {
+        if (seg_block(geo) == 0 && geo.elem_lo > 0) {
             const double dh = DMODE == LBK_D_BUF ? ghost_d(da, -1, geo.n_loc)
                                                  : -(ghost_d(da, -1, geo.n_loc) + da.s[-1] * da.coef);
             const double z = x[-1] + alpha * dh;
             xn[-1] = z;
             so[-1] = z - x[-1];
         }
-        if (blockIdx.x == gridDim.x - 1 && geo.elem_lo + geo.n_loc < geo.n) {
+        if (seg_block(geo) == gridDim.x - 1 && geo.elem_lo + geo.n_loc < geo.n) {
             const int64_t e = geo.n_loc;
             const double dh = DMODE == LBK_D_BUF ? ghost_d(da, e, geo.n_loc)
                                                  : -(ghost_d(da, e, geo.n_loc) + da.s[e] * da.coef);
@@ -1494,6 +1500,9 @@ struct lbk_ctx {
     int xg_on;       // 1: exchanges go through xg instead of RCCL
     uint64_t* d_ckslot;  // [LBK_GROUPS][2] checksum words for the peer exchange
     int small_seg_max;  // persistent single-workgroup iteration when nseg <= this (0: off)
+    // LBFGS_REV=1: every other pass walks its segments last to first, so a pass starts on the
+    // tail of the vector its predecessor wrote last (still in the Infinity Cache / L2)
+    int rev_on, rev_par;
 };
 
 namespace {
@@ -1519,6 +1528,7 @@ Geo kgeo(const lbk_ctx* c) {
     g.g_lo = c->geo.g_lo;
     g.g_hi = c->geo.g_hi;
     g.spg = LBK_SEG_PER_GROUP;
+    g.rev = c->rev_on ? c->rev_par : 0;
     g.edge_slot = nullptr;
     return g;
 }
@@ -1653,6 +1663,7 @@ int launch(lbk_ctx* c, int kind, double vec_passes, int slot, F&& fn, int K = 1,
     if (nblocks(c) > 0) {
         fn();
         HIPCHK(c, hipGetLastError());
+        c->rev_par ^= 1;
     }
     if (slot >= 0 && !c->ticket) {
         const Geo g = gv ? *gv : kgeo(c);
@@ -1780,6 +1791,10 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
     // segment step, more than the kernel boundaries it removes. Off by default.
     c->small_seg_max = 0;
     if (const char* e = getenv("LBFGS_SMALL_SEGS")) c->small_seg_max = atoi(e);
+    // measured +1 % at n = 1e7 (default and vector-free), +1 % vector-free and neutral default at
+    // 1e8 (profiles/r01/rev_ab.txt); bit-identical either way (per-segment partials)
+    c->rev_on = 1;
+    if (const char* e = getenv("LBFGS_REV")) c->rev_on = atoi(e) != 0;
     *out = c;
 #define CK(expr)                                                                             \
     do {                                                                                     \
