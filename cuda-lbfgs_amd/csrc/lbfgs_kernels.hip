@@ -60,6 +60,7 @@ struct Red {
     double* partials;  // [LBK_KW][LBK_SEGS], local segment index
     unsigned* cnt;     // [LBK_GROUPS] tickets
     double* slot;      // this launch's result slot [LBK_GROUPS][kstride]
+    double* hslot;     // its pinned host mirror, written alongside (one rank), or nullptr
     int ticket;        // 1: in-launch last-arriver stage 2; 0: k_group_reduce after the launch
     int kstride;       // LBK_KMAX (regular slots) or LBK_KW (wide slots)
 };
@@ -156,7 +157,8 @@ __device__ __forceinline__ int64_t row_off(const Seg& s, int u) {
 // boundary (reduce-kernel mode).
 template <int K, bool ATOMIC>
 __device__ __forceinline__ void group_tree(const double* partials, int64_t lbase, int64_t gseg0, int64_t nseg,
-                                           int spg, double* slot_g, double (&lds)[4][K > 0 ? K : 1]) {
+                                           int spg, double* slot_g, double* hslot_g,
+                                           double (&lds)[4][K > 0 ? K : 1]) {
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     double q[K];
     // components in chunks of 8 with every load of a chunk issued before the first butterfly:
@@ -196,7 +198,11 @@ __device__ __forceinline__ void group_tree(const double* partials, int64_t lbase
     __syncthreads();
     if (t == 0) {
 #pragma unroll
-        for (int k = 0; k < K; ++k) slot_g[k] = (lds[0][k] + lds[1][k]) + (lds[2][k] + lds[3][k]);
+        for (int k = 0; k < K; ++k) {
+            const double v = (lds[0][k] + lds[1][k]) + (lds[2][k] + lds[3][k]);
+            slot_g[k] = v;
+            if (hslot_g) hslot_g[k] = v;
+        }
     }
 }
 
@@ -248,25 +254,28 @@ __device__ __forceinline__ void reduce_publish(double (&acc)[K], const Geo& geo,
     if (!last_flag) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const int64_t gseg0 = (int64_t)g * geo.spg;
-    group_tree<K, true>(red.partials, gseg0 - geo.seg_lo, gseg0, geo.nseg, geo.spg, red.slot + g * red.kstride, lds);
+    group_tree<K, true>(red.partials, gseg0 - geo.seg_lo, gseg0, geo.nseg, geo.spg, red.slot + g * red.kstride,
+                        red.hslot ? red.hslot + g * red.kstride : nullptr, lds);
     if (t == 0) __hip_atomic_store(red.cnt + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Reduce-kernel mode: one workgroup per group of this rank (stage 2 after the boundary).
 template <int K>
 __global__ __launch_bounds__(LB_BLOCK) void k_group_reduce(const double* __restrict__ partials, Geo geo,
-                                                           double* __restrict__ slot, int kstride) {
+                                                           double* __restrict__ slot, double* hslot, int kstride) {
     __shared__ double lds[4][K];
     const int g = geo.g_lo + (int)blockIdx.x;
     const int64_t gseg0 = (int64_t)g * geo.spg;
-    group_tree<K, false>(partials, gseg0 - geo.seg_lo, gseg0, geo.nseg, geo.spg, slot + g * kstride, lds);
+    group_tree<K, false>(partials, gseg0 - geo.seg_lo, gseg0, geo.nseg, geo.spg, slot + g * kstride,
+                         hslot ? hslot + g * kstride : nullptr, lds);
 }
 
 // The same stage 2 for a runtime number of components (wide slots): blockIdx.y takes
 // components [8 y, 8 y + 8), all their partial loads issued before the first butterfly;
 // identical arithmetic per component as group_tree.
 __global__ __launch_bounds__(LB_BLOCK) void k_group_reduce_wide(const double* __restrict__ partials, Geo geo,
-                                                                double* __restrict__ slot, int K, int kstride) {
+                                                                double* __restrict__ slot, double* hslot, int K,
+                                                                int kstride) {
     constexpr int KC = 8;
     __shared__ double lds[4][KC];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -288,7 +297,11 @@ __global__ __launch_bounds__(LB_BLOCK) void k_group_reduce_wide(const double* __
         if (lane == 0) lds[w][c] = q;
     }
     __syncthreads();
-    if (t < KC && k0 + t < K) slot[g * kstride + k0 + t] = (lds[0][t] + lds[1][t]) + (lds[2][t] + lds[3][t]);
+    if (t < KC && k0 + t < K) {
+        const double v = (lds[0][t] + lds[1][t]) + (lds[2][t] + lds[3][t]);
+        slot[g * kstride + k0 + t] = v;
+        if (hslot) hslot[g * kstride + k0 + t] = v;
+    }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1228,6 +1241,7 @@ struct SmallArgs {
     const double* x;
     double *xn, *gn, *so, *yo;
     double* slots;          // slot base (LBK_SLOT doubles per slot)
+    double* hslots;         // host mirror base, or nullptr
     int slot_p0, slot_a0, slot_b0, slot_c;
 };
 
@@ -1246,7 +1260,7 @@ __device__ __forceinline__ Seg seg_at(const Geo& geo, int64_t sidx, int tq) {
 
 // one pass of Op over all segments; the K fixed-order totals land in tot[] (every thread)
 template <int K, class Op>
-__device__ void small_pass(const Op& op, const Geo& geo, double* slot, double (&tot)[K],
+__device__ void small_pass(const Op& op, const Geo& geo, double* slot, double* hslot, double (&tot)[K],
                            double (*part)[LBK_SMALL_SEGMAX], double (*wl)[16]) {
     const int t = threadIdx.x, qtr = t >> 8, tq = t & 255, lane = t & 63, wv = t >> 6;
     for (int64_t s0 = 0; s0 < geo.nseg; s0 += LBK_SMALL_THREADS / 256) {
@@ -1290,7 +1304,10 @@ __device__ void small_pass(const Op& op, const Geo& geo, double* slot, double (&
     if (t < K) {
         const int k = t;
         const double q0 = (wl[k][0] + wl[k][1]) + (wl[k][2] + wl[k][3]);
-        for (int g = 0; g < LBK_GROUPS; ++g) slot[g * LBK_KMAX + k] = g == 0 ? q0 : 0.0;
+        for (int g = 0; g < LBK_GROUPS; ++g) {
+            slot[g * LBK_KMAX + k] = g == 0 ? q0 : 0.0;
+            if (hslot) hslot[g * LBK_KMAX + k] = g == 0 ? q0 : 0.0;
+        }
         double tt = q0;
         for (int g = 1; g < LBK_GROUPS; ++g) tt = tt + 0.0;
         wl[k][8] = tt;
@@ -1304,6 +1321,7 @@ __device__ void small_pass(const Op& op, const Geo& geo, double* slot, double (&
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
+#define HS(sl) (a.hslots ? a.hslots + (int64_t)(sl) * LBK_SLOT : nullptr)  // host-fetched slots only
 template <int OBJ>
 __global__ __launch_bounds__(LBK_SMALL_THREADS) void k_small_iter(SmallArgs a, Geo geo) {
     __shared__ double part[LBK_KMAX][LBK_SMALL_SEGMAX];
@@ -1315,19 +1333,19 @@ __global__ __launch_bounds__(LBK_SMALL_THREADS) void k_small_iter(SmallArgs a, G
     if (a.p0_from_slot) {
         t1[0] = slot_total(a.p0_slot);
     } else {
-        small_pass<1>(OpDot<false>{a.S[h - 1], a.g}, geo, a.slots + (int64_t)a.slot_p0 * LBK_SLOT, t1, part, wl);
+        small_pass<1>(OpDot<false>{a.S[h - 1], a.g}, geo, a.slots + (int64_t)a.slot_p0 * LBK_SLOT, nullptr, t1, part, wl);
     }
     if (threadIdx.x == 0) TA[h - 1] = t1[0];
     double alpha = a.rho[h - 1] * t1[0];
     const double* qsrc = a.g;
     for (int i = h - 2; i >= 0; --i) {  // q = q - alpha_{i+1} y_{i+1};  s_i . q
         small_pass<1>(OpAxpyDot<false>{a.q, qsrc, a.Y[i + 1], a.S[i], alpha}, geo,
-                      a.slots + (int64_t)(a.slot_a0 + i) * LBK_SLOT, t1, part, wl);
+                      a.slots + (int64_t)(a.slot_a0 + i) * LBK_SLOT, nullptr, t1, part, wl);
         if (threadIdx.x == 0) TA[i] = t1[0];
         alpha = a.rho[i] * t1[0];
         qsrc = a.q;
     }
-    small_pass<1>(OpMid<false>{a.r, qsrc, a.Y[0], alpha, a.gamma}, geo, a.slots + (int64_t)a.slot_b0 * LBK_SLOT, t1,
+    small_pass<1>(OpMid<false>{a.r, qsrc, a.Y[0], alpha, a.gamma}, geo, a.slots + (int64_t)a.slot_b0 * LBK_SLOT, nullptr, t1,
                   part, wl);
     if (threadIdx.x == 0) TB[0] = t1[0];
     __syncthreads();
@@ -1335,7 +1353,7 @@ __global__ __launch_bounds__(LBK_SMALL_THREADS) void k_small_iter(SmallArgs a, G
         const double beta = a.rho[i] * TB[i];
         const double alph = a.rho[i] * TA[i];
         small_pass<1>(OpAxpy2Dot<false>{a.r, a.r, a.S[i], a.Y[i + 1], alph - beta}, geo,
-                      a.slots + (int64_t)(a.slot_b0 + i + 1) * LBK_SLOT, t1, part, wl);
+                      a.slots + (int64_t)(a.slot_b0 + i + 1) * LBK_SLOT, nullptr, t1, part, wl);
         if (threadIdx.x == 0) TB[i + 1] = t1[0];
         __syncthreads();
     }
@@ -1348,7 +1366,7 @@ __global__ __launch_bounds__(LBK_SMALL_THREADS) void k_small_iter(SmallArgs a, G
     }
     double t7[7];
     small_pass<7>(OpCommit<OBJ, LBK_D_TWOLOOP, false>{a.x, da, a.a0, a.xn, a.gn, a.so, a.yo, geo.n, geo.n_loc}, geo,
-                  a.slots + (int64_t)a.slot_c * LBK_SLOT, t7, part, wl);
+                  a.slots + (int64_t)a.slot_c * LBK_SLOT, HS(a.slot_c), t7, part, wl);
 }
 
 // z = x + alpha d over the whole local range incl. ghosts (host-callback objectives)
@@ -1472,8 +1490,14 @@ struct lbk_ctx {
     unsigned* cnt;      // LBK_GROUPS
     double* slots;      // LBK_NSLOTS * LBK_SLOT
     double* h_slots;    // pinned mirror
+    double* dh_slots;   // the mirror as the device addresses it
     double* wslots;     // LBK_NWSLOTS * LBK_WSLOT (wide slots)
     double* h_wslots;   // pinned mirror
+    double* dh_wslots;
+    // one rank: stage 2 writes every result slot into its pinned host mirror too, so a fetch is a
+    // stream synchronisation and no copy (LBFGS_DIRECT=0: hipMemcpyAsync of the slot instead)
+    int direct;
+    unsigned char slot_mirror[LBK_NSLOTS + LBK_NWSLOTS];  // last write of the slot went to the mirror
     unsigned long long* d_ck;
     unsigned long long* h_ck;
     int64_t vec_doubles;  // allocation per vector
@@ -1563,12 +1587,24 @@ double* slot_host(const lbk_ctx* c, int slot) {
                              : c->h_wslots + (int64_t)(slot - LBK_WSLOT0) * LBK_WSLOT;
 }
 int slot_stride(int slot) { return slot < LBK_NSLOTS ? LBK_KMAX : LBK_KW; }
+// The host mirror as kernels address it, or nullptr. Mirrored: the slots the host reads back
+// (multi-component reductions: commit, trials, objective; wide slots). A single-component
+// two-loop reduction only feeds the next pass on the device; writing it over PCIe as well would
+// hold every pass's completion behind a host-memory write (measured -6..-11 % at n = 1e6).
+bool mirrored(const lbk_ctx* c, int slot, int K) { return c->direct && (K >= 2 || slot >= LBK_NSLOTS); }
+double* slot_dhost(const lbk_ctx* c, int slot) {
+    if (!c->direct) return nullptr;
+    return slot < LBK_NSLOTS ? c->dh_slots + (int64_t)slot * LBK_SLOT
+                             : c->dh_wslots + (int64_t)(slot - LBK_WSLOT0) * LBK_WSLOT;
+}
 
-Red kred(const lbk_ctx* c, int slot) {
+Red kred(lbk_ctx* c, int slot, int K = 1) {
     Red r;
     r.partials = c->partials;
     r.cnt = c->cnt;
     r.slot = slot_base(c, slot);
+    r.hslot = mirrored(c, slot, K) ? slot_dhost(c, slot) : nullptr;
+    c->slot_mirror[slot < LBK_NSLOTS ? slot : LBK_NSLOTS + slot - LBK_WSLOT0] = r.hslot != nullptr;
     r.kstride = slot_stride(slot);
     r.ticket = c->ticket;
     return r;
@@ -1668,15 +1704,16 @@ int launch(lbk_ctx* c, int kind, double vec_passes, int slot, F&& fn, int K = 1,
     if (slot >= 0 && !c->ticket) {
         const Geo g = gv ? *gv : kgeo(c);
         double* sl = slot_base(c, slot);
+        double* hs = mirrored(c, slot, K) ? slot_dhost(c, slot) : nullptr;
         const int ks = slot_stride(slot);
         const dim3 grid(c->geo.g_hi - c->geo.g_lo), blk(LB_BLOCK);
         switch (K) {
-            case 1: hipLaunchKernelGGL(k_group_reduce<1>, grid, blk, 0, c->stream, c->partials, g, sl, ks); break;
-            case 2: hipLaunchKernelGGL(k_group_reduce<2>, grid, blk, 0, c->stream, c->partials, g, sl, ks); break;
-            case 7: hipLaunchKernelGGL(k_group_reduce<7>, grid, blk, 0, c->stream, c->partials, g, sl, ks); break;
+            case 1: hipLaunchKernelGGL(k_group_reduce<1>, grid, blk, 0, c->stream, c->partials, g, sl, hs, ks); break;
+            case 2: hipLaunchKernelGGL(k_group_reduce<2>, grid, blk, 0, c->stream, c->partials, g, sl, hs, ks); break;
+            case 7: hipLaunchKernelGGL(k_group_reduce<7>, grid, blk, 0, c->stream, c->partials, g, sl, hs, ks); break;
             default:
                 hipLaunchKernelGGL(k_group_reduce_wide, dim3(c->geo.g_hi - c->geo.g_lo, (K + 7) / 8), blk, 0, c->stream,
-                                   c->partials, g, sl, K, ks);
+                                   c->partials, g, sl, hs, K, ks);
                 break;
         }
         HIPCHK(c, hipGetLastError());
@@ -1795,6 +1832,9 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
     // 1e8 (profiles/r01/rev_ab.txt); bit-identical either way (per-segment partials)
     c->rev_on = 1;
     if (const char* e = getenv("LBFGS_REV")) c->rev_on = atoi(e) != 0;
+    // sharded slots are completed by the exchange on the device: those fetch with a copy
+    c->direct = world == 1 ? 1 : 0;
+    if (const char* e = getenv("LBFGS_DIRECT")) c->direct = world == 1 && atoi(e) != 0;
     *out = c;
 #define CK(expr)                                                                             \
     do {                                                                                     \
@@ -1809,12 +1849,17 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
     CK(hipMalloc(&c->partials, sizeof(double) * LBK_KW * LBK_SEGS));
     CK(hipMalloc(&c->cnt, sizeof(unsigned) * 16));
     CK(hipMalloc(&c->slots, sizeof(double) * LBK_NSLOTS * LBK_SLOT));
-    CK(hipHostMalloc(&c->h_slots, sizeof(double) * LBK_NSLOTS * LBK_SLOT, hipHostMallocDefault));
+    CK(hipHostMalloc(&c->h_slots, sizeof(double) * LBK_NSLOTS * LBK_SLOT, hipHostMallocMapped | hipHostMallocCoherent));
+    memset(c->h_slots, 0, sizeof(double) * LBK_NSLOTS * LBK_SLOT);
+    CK(hipHostGetDevicePointer((void**)&c->dh_slots, c->h_slots, 0));
     CK(hipMalloc(&c->d_ck, 2 * sizeof(unsigned long long)));
     CK(hipHostMalloc(&c->h_ck, 2 * sizeof(unsigned long long), hipHostMallocDefault));
     CK(hipMemset(c->partials, 0, sizeof(double) * LBK_KW * LBK_SEGS));
     CK(hipMalloc(&c->wslots, sizeof(double) * LBK_NWSLOTS * LBK_WSLOT));
-    CK(hipHostMalloc(&c->h_wslots, sizeof(double) * LBK_NWSLOTS * LBK_WSLOT, hipHostMallocDefault));
+    CK(hipHostMalloc(&c->h_wslots, sizeof(double) * LBK_NWSLOTS * LBK_WSLOT,
+                     hipHostMallocMapped | hipHostMallocCoherent));
+    memset(c->h_wslots, 0, sizeof(double) * LBK_NWSLOTS * LBK_WSLOT);
+    CK(hipHostGetDevicePointer((void**)&c->dh_wslots, c->h_wslots, 0));
     CK(hipMemset(c->wslots, 0, sizeof(double) * LBK_NWSLOTS * LBK_WSLOT));
     CK(hipMemset(c->cnt, 0, sizeof(unsigned) * 16));
     CK(hipMemset(c->slots, 0, sizeof(double) * LBK_NSLOTS * LBK_SLOT));
@@ -2021,7 +2066,7 @@ int lbk_negdot(lbk_ctx* c, double* dout, const double* gg, int slot) {
 
 int lbk_eval(lbk_ctx* c, int obj, const double* x, double* gout, int slot) {
     Geo g = kgeo(c);
-    Red r = kred(c, slot);
+    Red r = kred(c, slot, 2);
     DirArgs da = {nullptr, nullptr, nullptr, 0.0, nullptr, nullptr, 0.0, nullptr, c->geo.g_lo, c->geo.g_hi};
     return launch(c, LBK_K_EVAL, gout ? 2 : 1, slot, [&] {
         OBJ_DISPATCH(obj, hipLaunchKernelGGL((k_objective<O_, true, true, NT_>), dim3(nblocks(c)), dim3(LB_BLOCK), 0,
@@ -2032,7 +2077,7 @@ int lbk_eval(lbk_ctx* c, int obj, const double* x, double* gout, int slot) {
 
 int lbk_trial(lbk_ctx* c, int obj, const double* x, const double* d, double alpha, double* gout, int slot) {
     Geo g = kgeo(c);
-    Red r = kred(c, slot);
+    Red r = kred(c, slot, 2);
     DirArgs da = {d, nullptr, nullptr, 0.0, nullptr, nullptr, 0.0, ghost_ptr(c), c->geo.g_lo, c->geo.g_hi};
     const int kind = gout ? LBK_K_TRIAL_FG : LBK_K_TRIAL_F;
     return launch(c, kind, gout ? 3 : 2, slot, [&] {
@@ -2051,7 +2096,7 @@ int lbk_commit(lbk_ctx* c, int obj, int dmode, const double* x, const double* ds
                const double* gg, double rho, int ref_beta, int ref_alpha, double alpha, double* xn, double* gn,
                double* s_out, double* y_out, int slot) {
     Geo g = kgeo(c);
-    Red r = kred(c, slot);
+    Red r = kred(c, slot, 7);
     DirArgs da = {dsrc, s_last, gg, 0.0, nullptr, nullptr, rho,
                   (dmode == LBK_D_BUF || dmode == LBK_D_TWOLOOP) ? ghost_ptr(c) : nullptr, c->geo.g_lo, c->geo.g_hi};
     if (dmode == LBK_D_TWOLOOP) {
@@ -2224,6 +2269,10 @@ int lbk_small_iter(lbk_ctx* c, int obj, int h, const double* g, double* q, doubl
     a.so = so;
     a.yo = yo;
     a.slots = c->slots;
+    a.hslots = c->direct ? c->dh_slots : nullptr;
+    c->slot_mirror[slot_p0] = 0;  // single-component passes: device only (see mirrored())
+    for (int i = 0; i < h; ++i) c->slot_mirror[slot_a0 + i] = c->slot_mirror[slot_b0 + i] = 0;
+    c->slot_mirror[slot_c] = c->direct ? 1 : 0;
     a.slot_p0 = slot_p0;
     a.slot_a0 = slot_a0;
     a.slot_b0 = slot_b0;
@@ -2348,7 +2397,8 @@ double lbk_total(const double* groups64, int comp) {
 int lbk_fetch_groups(lbk_ctx* c, int slot, double* groups64) {
     double* h = slot_host(c, slot);
     const size_t bytes = sizeof(double) * LBK_GROUPS * slot_stride(slot);
-    HIPCHK(c, hipMemcpyAsync(h, slot_base(c, slot), bytes, hipMemcpyDeviceToHost, c->stream));
+    if (!c->slot_mirror[slot < LBK_NSLOTS ? slot : LBK_NSLOTS + slot - LBK_WSLOT0])
+        HIPCHK(c, hipMemcpyAsync(h, slot_base(c, slot), bytes, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (c->xg_on && lbk_xgmi_failed(c->xg)) {
         snprintf(c->err, sizeof c->err, "xgmi exchange timed out waiting for a peer");
