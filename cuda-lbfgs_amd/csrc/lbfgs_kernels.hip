@@ -160,6 +160,36 @@ __device__ __forceinline__ void group_tree(const double* partials, int64_t lbase
                                            int spg, double* slot_g, double* hslot_g,
                                            double (&lds)[4][K > 0 ? K : 1]) {
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    // Few valid partials (a group of at most 64 segments: n up to ~6e4, or the tail group): wave w
+    // takes components w, w + 4, ..., lane j entry j, every load in one round trip. The wave
+    // butterfly is the balanced tree over entries 0..63; the tree's upper levels only add
+    // 0.0 subtrees, which is the final "+ 0.0" (bit-identical to the general path below).
+    const int64_t nvalid = min((int64_t)spg, nseg - gseg0);
+    if (nvalid <= 64) {
+        constexpr int KQ = (K + 3) / 4;
+        double p[KQ];
+#pragma unroll
+        for (int i = 0; i < KQ; ++i) {
+            const int k = w + 4 * i;
+            p[i] = 0.0;
+            if (k < K && lane < nvalid) {
+                const double* src = partials + (int64_t)k * LBK_SEGS + lbase + lane;
+                p[i] = ATOMIC ? bitsd(__hip_atomic_load(reinterpret_cast<const unsigned long long*>(src),
+                                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                              : *src;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < KQ; ++i) {
+            const int k = w + 4 * i;
+            const double v = wave_sum(p[i]) + 0.0;
+            if (k < K && lane == 0) {
+                slot_g[k] = v;
+                if (hslot_g) hslot_g[k] = v;
+            }
+        }
+        return;
+    }
     double q[K];
     // components in chunks of 8 with every load of a chunk issued before the first butterfly:
     // the relaxed atomic loads of the ticket path are not batched by the compiler, and one L2
