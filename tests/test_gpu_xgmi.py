@@ -88,3 +88,11 @@ def test_xgmi_silent_peer_times_out(tmp_path):
     assert procs[0].returncode == 3, outs[0][-2000:]
     assert "timed out" in outs[0], outs[0][-2000:]
     assert procs[1].returncode == 0, outs[1][-2000:]
+
+
+def test_xgmi_exchange_latency_collective(tmp_path):
+    """lbfgs_exchange_latency (bench.py's exchange_latency_us) runs as a collective on every rank
+    and returns a positive per-exchange time for both slot widths."""
+    outs = run_ranks(tmp_path, 2, 4_000_003, 5, "rosenbrock", "backtracking", 1, "latency")
+    for o in outs:
+        assert 0.0 < float(o["us8"]) < 1e5 and 0.0 < float(o["us96"]) < 1e5

@@ -63,6 +63,13 @@ def main():
         print(f"rank {rank}: peer connect failed: {msg}", flush=True)
         sys.exit(3)
     assert ctx.backend == "xgmi", ctx.backend
+    if mode == "latency":  # lbfgs_exchange_latency through the mailboxes (collective)
+        us8 = ctx.exchange_latency("xgmi", 8, 50)
+        us96 = ctx.exchange_latency("xgmi", 96, 50)
+        np.savez(os.path.join(d, f"out{rank}.npz"), us8=us8, us96=us96)
+        ctx.close()
+        print(f"rank {rank}: {us8:.2f} / {us96:.2f} us per exchange", flush=True)
+        return
     r = ctx.minimize(obj, x0, ls, iters, trace=True, vector_free=(mode == "vf"))
     lo, nl = ctx.elem_lo, ctx.n_loc
     np.savez(os.path.join(d, f"out{rank}.npz"), tr_f=r["tr_f"], tr_gnorm=r["tr_gnorm"], tr_alpha=r["tr_alpha"],
