@@ -1731,6 +1731,18 @@ int launch(lbk_ctx* c, int kind, double vec_passes, int slot, F&& fn, int K = 1,
         HIPCHK(c, hipGetLastError());
         c->rev_par ^= 1;
     }
+    // the pass kernel's own interval ends here; a separate stage 2 is timed as its own kind
+    if (c->prof_on && a && b) {
+        HIPCHK(c, hipEventRecord(b, c->stream));
+        c->pending.push_back({kind, a, b, bytes});
+        a = b = nullptr;
+        if (slot >= 0 && !c->ticket) {
+            a = ev_get(c);
+            b = ev_get(c);
+            if (a) HIPCHK(c, hipEventRecord(a, c->stream));
+            kind = LBK_K_GROUP_REDUCE;
+        }
+    }
     if (slot >= 0 && !c->ticket) {
         const Geo g = gv ? *gv : kgeo(c);
         double* sl = slot_base(c, slot);
@@ -1750,7 +1762,7 @@ int launch(lbk_ctx* c, int kind, double vec_passes, int slot, F&& fn, int K = 1,
     }
     if (c->prof_on && a && b) {
         HIPCHK(c, hipEventRecord(b, c->stream));
-        c->pending.push_back({kind, a, b, bytes});
+        c->pending.push_back({kind, a, b, 0.0});
     }
     if (exchange && c->geo.world > 1 && slot >= 0) return exchange_slot(c, slot);
     return 0;

@@ -21,7 +21,8 @@ LINE_SEARCHES = {"backtracking": 0, "interpolation": 1, "wolfe": 2, "backtrackin
 STATUS = {0: "converged", 1: "max_iter", 2: "ls_failed", 3: "running"}
 FLAG_VERBOSE, FLAG_QUIET, FLAG_TRACE, FLAG_UNFUSED, FLAG_VECTOR_FREE = 1, 2, 4, 8, 16
 KERNELS = ["dot", "axpy_dot", "mid", "axpy2_dot", "last", "negdot", "eval", "trial_f",
-           "trial_fg", "commit", "point", "checksum", "update", "vf_commit", "vf_dir", "small_iter"]
+           "trial_fg", "commit", "point", "checksum", "update", "vf_commit", "vf_dir", "small_iter",
+           "group_reduce"]
 
 
 class LbfgsError(RuntimeError):

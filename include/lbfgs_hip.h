@@ -224,7 +224,8 @@ enum {
     LBFGS_KERNEL_LAST, LBFGS_KERNEL_NEGDOT, LBFGS_KERNEL_EVAL, LBFGS_KERNEL_TRIAL_F,
     LBFGS_KERNEL_TRIAL_FG, LBFGS_KERNEL_COMMIT, LBFGS_KERNEL_POINT, LBFGS_KERNEL_CHECKSUM,
     LBFGS_KERNEL_UPDATE, LBFGS_KERNEL_VF_COMMIT, LBFGS_KERNEL_VF_DIR,
-    LBFGS_KERNEL_SMALL_ITER, LBFGS_KERNEL_COUNT
+    LBFGS_KERNEL_SMALL_ITER, LBFGS_KERNEL_GROUP_REDUCE /* stage 2 of the reductions */,
+    LBFGS_KERNEL_COUNT
 };
 void lbfgs_prof_enable(lbfgs_ctx* ctx, int on);
 void lbfgs_prof_reset(lbfgs_ctx* ctx);
