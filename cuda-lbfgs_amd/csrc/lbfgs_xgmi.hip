@@ -114,7 +114,13 @@ int lbk_xgmi_create(lbk_xgmi** out, int device, int rank, int world, int positio
     x->world = world;
     x->positions = positions;
     const size_t bytes = sizeof(unsigned long long) * 2 * 2 * (size_t)positions;
+    // uncached: the owner's polls and the peers' xGMI stores meet in HBM, never in a stale L2
+    // line; fine-grained memory (coherent, cached per access) is the fallback
     hipError_t e = hipExtMallocWithFlags((void**)&x->mb, bytes, hipDeviceMallocUncached);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        e = hipExtMallocWithFlags((void**)&x->mb, bytes, hipDeviceMallocFinegrained);
+    }
     if (e == hipSuccess) e = hipMemset(x->mb, 0, bytes);
     if (e == hipSuccess) e = hipIpcGetMemHandle(&x->handle, x->mb);
     if (e == hipSuccess) e = hipHostMalloc((void**)&x->err_h, sizeof(unsigned), hipHostMallocMapped);
