@@ -736,6 +736,8 @@ struct DirArgs {
     double rho;
     const double* ghost;  // sharded, D_BUF: all-gathered slot holding the neighbours' edge d
     int g_lo, g_hi;
+    const double* redge;  // cooperative iteration, D_TWOLOOP: first/last r of every segment (sc1)
+    int64_t L;            // ... and the segment length that indexes it
 };
 
 template <int DMODE, bool NT>
@@ -791,7 +793,15 @@ __device__ __forceinline__ double halo_z(const double* __restrict__ x, const Dir
                         dh = ghost_d(da, hi, n_loc);
                     else if (DMODE == LBK_D_TWOLOOP && da.ghost && (hi == -1 || hi == n_loc))
                         dh = -(ghost_d(da, hi, n_loc) + da.s[hi] * da.coef);  // neighbour's edge r, s ghost
-                    else
+                    else if (DMODE == LBK_D_TWOLOOP && da.redge && hi >= 0 && hi < n_loc && hi / da.L != i / da.L) {
+                        // r of another workgroup's segment, written in this launch: its published
+                        // edge (write-through), not the plain-stored vector
+                        const int64_t sg = hi / da.L;
+                        const double rv = bitsd(__hip_atomic_load(
+                            reinterpret_cast<const unsigned long long*>(da.redge + 2 * sg + (hi == sg * da.L ? 0 : 1)),
+                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                        dh = -(rv + da.s[hi] * da.coef);
+                    } else
                         dh = load_dir1<DMODE>(da, hi);
                     zh = x[hi] + alpha * dh;
                 }
@@ -1273,6 +1283,13 @@ struct SmallArgs {
     double* slots;          // slot base (LBK_SLOT doubles per slot)
     double* hslots;         // host mirror base, or nullptr
     int slot_p0, slot_a0, slot_b0, slot_c;
+    // cooperative form (k_coop_iter) only
+    double* part;                 // 2 x 8 x LBK_SEGS partials (double-buffered by pass parity)
+    double* redge;                // 2 per segment: first / last r of the last second-loop pass
+    unsigned long long* bar;      // arrival counter, monotonic across launches
+    unsigned long long bar_base;  // its value when this launch starts
+    unsigned* err;                // pinned: set on a barrier timeout
+    unsigned long long timeout;   // wall-clock ticks
 };
 
 __device__ __forceinline__ Seg seg_at(const Geo& geo, int64_t sidx, int tq) {
@@ -1398,6 +1415,146 @@ __global__ __launch_bounds__(LBK_SMALL_THREADS) void k_small_iter(SmallArgs a, G
     small_pass<7>(OpCommit<OBJ, LBK_D_TWOLOOP, false>{a.x, da, a.a0, a.xn, a.gn, a.so, a.yo, geo.n, geo.n_loc}, geo,
                   a.slots + (int64_t)a.slot_c * LBK_SLOT, HS(a.slot_c), t7, part, wl);
 }
+
+// ---------------------------------------------------------------------------------------
+// Cooperative iteration for small n (the persistent-block two-loop of SURVEY §7 step 5): one
+// workgroup per canonical segment (nseg <= LBK_COOP_SEGMAX, all resident), the whole two-loop
+// and the fused first-trial commit of one iteration in ONE launch, with an in-launch grid
+// barrier between passes instead of a kernel boundary plus a stage-2 kernel:
+//   * each workgroup streams its segment exactly as the pass kernel would, stores its partial
+//     write-through (sc1), drains, and adds to a monotonic agent-scope arrival counter;
+//   * after the counter shows every workgroup of the pass, every workgroup loads the <= 64
+//     partials with sc1 loads and forms the same fixed-order total (group tree + "+ 0.0"
+//     levels, then the 8-group sum) - no last arriver, no second launch;
+//   * partials are double-buffered by pass parity (a workgroup can be at most one pass ahead);
+//   * vectors stay per segment (pass i+1 of a segment reads what the same waves wrote in pass i);
+//     the commit's stencil halo across segments reads the last r pass's published edge values.
+// A barrier that waits past its timeout sets *err (pinned host memory) instead of hanging.
+// ---------------------------------------------------------------------------------------
+#define LBK_COOP_SEGMAX 64
+
+template <int K, class Op>
+__device__ __forceinline__ void coop_pass(const Op& op, const Geo& geo, const SmallArgs& a, int pass,
+                                          double* slot, double* hslot, const double* rvec, double (&tot)[K],
+                                          double (&lds)[4][8], double (&tl)[8]) {
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int64_t b = blockIdx.x;
+    const Seg s = seg_setup(geo);
+    double acc[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) acc[k] = 0.0;
+    stream(op, s, geo, acc);
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const double v = wave_sum(acc[k]);
+        if (lane == 0) lds[w][k] = v;
+    }
+    // this pass's vector stores are read by other waves of the workgroup in the next pass
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    double* P = a.part + (size_t)(pass & 1) * 8 * LBK_SEGS;
+    if (t == 0) {
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            __hip_atomic_store(reinterpret_cast<unsigned long long*>(P + (int64_t)k * LBK_SEGS + b),
+                               dbits((lds[0][k] + lds[1][k]) + (lds[2][k] + lds[3][k])), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        if (rvec) {  // the segment's first and last r, for the neighbours' commit halo
+            __hip_atomic_store(reinterpret_cast<unsigned long long*>(a.redge + 2 * b), dbits(rvec[s.lb]),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(reinterpret_cast<unsigned long long*>(a.redge + 2 * b + 1),
+                               dbits(rvec[s.lb + s.len - 1]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_fetch_add(a.bar, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long target = a.bar_base + (unsigned long long)(pass + 1) * (unsigned long long)geo.nseg;
+        const unsigned long long t0 = wall_clock64();
+        while (__hip_atomic_load(a.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            if (wall_clock64() - t0 > a.timeout) {
+                __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                printf("k_coop_iter: block %d pass %d: counter %llu, waiting for %llu\n", (int)b, pass,
+                       __hip_atomic_load(a.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), target);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    __syncthreads();
+    // every workgroup: the fixed-order totals from the <= 64 partials (wave w: components w, w+4)
+#pragma unroll
+    for (int k = w; k < K; k += 4) {
+        const double p = lane < geo.nseg ? bitsd(__hip_atomic_load(
+                                               reinterpret_cast<const unsigned long long*>(P + (int64_t)k * LBK_SEGS + lane),
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                                         : 0.0;
+        const double q0 = wave_sum(p) + 0.0;  // group 0: the tree's levels above 64 add 0.0
+        if (lane == 0) {
+            double tt = q0;  // slot_total: groups 1..7 hold no segment
+#pragma unroll
+            for (int g = 1; g < LBK_GROUPS; ++g) tt = tt + 0.0;
+            tl[k] = tt;
+            if (b == 0 && slot) {
+                slot[k] = q0;
+                if (hslot) hslot[k] = q0;
+            }
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < K; ++k) tot[k] = tl[k];
+    __syncthreads();  // lds / tl reuse by the next pass
+}
+
+#define SL(sl) (a.slots + (int64_t)(sl) * LBK_SLOT)
+template <int OBJ>
+__global__ __launch_bounds__(LB_BLOCK) void k_coop_iter(SmallArgs a, Geo geo) {
+    __shared__ double lds[4][8];
+    __shared__ double tl[8];
+    __shared__ double TA[LBK_SMALL_HMAX], TB[LBK_SMALL_HMAX];
+    const int h = a.h;
+    int pass = 0;
+    double t1[1];
+    // alpha_{h-1} = rho_{h-1} (s_{h-1} . g): from the previous commit (SG) or a dot pass
+    if (a.p0_from_slot)
+        t1[0] = slot_total(a.p0_slot);
+    else
+        coop_pass<1>(OpDot<false>{a.S[h - 1], a.g}, geo, a, pass++, SL(a.slot_p0), nullptr, nullptr, t1, lds, tl);
+    if (threadIdx.x == 0) TA[h - 1] = t1[0];
+    double alpha = a.rho[h - 1] * t1[0];
+    const double* qsrc = a.g;
+    for (int i = h - 2; i >= 0; --i) {  // q = q - alpha_{i+1} y_{i+1};  s_i . q
+        coop_pass<1>(OpAxpyDot<false>{a.q, qsrc, a.Y[i + 1], a.S[i], alpha}, geo, a, pass++, SL(a.slot_a0 + i),
+                     nullptr, nullptr, t1, lds, tl);
+        if (threadIdx.x == 0) TA[i] = t1[0];
+        alpha = a.rho[i] * t1[0];
+        qsrc = a.q;
+    }
+    coop_pass<1>(OpMid<false>{a.r, qsrc, a.Y[0], alpha, a.gamma}, geo, a, pass++, SL(a.slot_b0), nullptr,
+                 h == 1 ? a.r : nullptr, t1, lds, tl);
+    if (threadIdx.x == 0) TB[0] = t1[0];
+    __syncthreads();
+    for (int i = 0; i + 1 < h; ++i) {  // r += s_i (alpha_i - beta_i);  y_{i+1} . r
+        const double beta = a.rho[i] * TB[i];
+        const double alph = a.rho[i] * TA[i];
+        coop_pass<1>(OpAxpy2Dot<false>{a.r, a.r, a.S[i], a.Y[i + 1], alph - beta}, geo, a, pass++,
+                     SL(a.slot_b0 + i + 1), nullptr, i + 2 == h ? a.r : nullptr, t1, lds, tl);
+        if (threadIdx.x == 0) TB[i + 1] = t1[0];
+        __syncthreads();
+    }
+    // the last second-loop update, the first trial at a0 and the commit (k_commit TWOLOOP)
+    DirArgs da = {a.r, a.S[h - 1], a.g, 0.0, nullptr, nullptr, a.rho[h - 1], nullptr, geo.g_lo, geo.g_hi,
+                  a.redge, geo.L};
+    {
+        const double beta = a.rho[h - 1] * TB[h - 1];
+        const double alph = a.rho[h - 1] * TA[h - 1];
+        da.coef = alph - beta;
+    }
+    double t7[7];
+    coop_pass<7>(OpCommit<OBJ, LBK_D_TWOLOOP, false>{a.x, da, a.a0, a.xn, a.gn, a.so, a.yo, geo.n, geo.n_loc}, geo, a,
+                 pass++, SL(a.slot_c), HS(a.slot_c), nullptr, t7, lds, tl);
+}
+#undef SL
 
 // z = x + alpha d over the whole local range incl. ghosts (host-callback objectives)
 __global__ void k_point(double* __restrict__ z, const double* __restrict__ x, const double* __restrict__ d,
@@ -1557,6 +1714,14 @@ struct lbk_ctx {
     // LBFGS_REV=1: every other pass walks its segments last to first, so a pass starts on the
     // tail of the vector its predecessor wrote last (still in the Infinity Cache / L2)
     int rev_on, rev_par;
+    // cooperative small-n iteration (k_coop_iter): nseg <= coop_max (0: off)
+    int coop_max;
+    unsigned long long* coop_bar;  // device arrival counter
+    unsigned long long coop_base;  // its value at the next launch
+    unsigned* coop_err_h;          // pinned: barrier timeout
+    unsigned* coop_err_d;
+    double* coop_redge;            // 2 per segment
+    double wall_khz;
 };
 
 namespace {
@@ -1870,6 +2035,10 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
     // segment step, more than the kernel boundaries it removes. Off by default.
     c->small_seg_max = 0;
     if (const char* e = getenv("LBFGS_SMALL_SEGS")) c->small_seg_max = atoi(e);
+    // measured +48 % at n = 1e4 (15.1k -> 22.4k it/s) and +41 % at 3e4, bit-identical
+    // (tests/test_gpu_parity.py::test_cooperative_iteration_bit_exact); LBFGS_COOP=0 disables
+    c->coop_max = LBK_COOP_SEGMAX;
+    if (const char* e = getenv("LBFGS_COOP")) c->coop_max = atoi(e) ? LBK_COOP_SEGMAX : 0;
     // measured +1 % at n = 1e7 (default and vector-free), +1 % vector-free and neutral default at
     // 1e8 (profiles/r01/rev_ab.txt); bit-identical either way (per-segment partials)
     c->rev_on = 1;
@@ -1905,6 +2074,17 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
     CK(hipMemset(c->wslots, 0, sizeof(double) * LBK_NWSLOTS * LBK_WSLOT));
     CK(hipMemset(c->cnt, 0, sizeof(unsigned) * 16));
     CK(hipMemset(c->slots, 0, sizeof(double) * LBK_NSLOTS * LBK_SLOT));
+    CK(hipMalloc(&c->coop_bar, sizeof(unsigned long long)));
+    CK(hipMemset(c->coop_bar, 0, sizeof(unsigned long long)));
+    CK(hipMalloc(&c->coop_redge, sizeof(double) * 2 * LBK_COOP_SEGMAX));
+    CK(hipHostMalloc((void**)&c->coop_err_h, sizeof(unsigned), hipHostMallocMapped | hipHostMallocCoherent));
+    *c->coop_err_h = 0;
+    CK(hipHostGetDevicePointer((void**)&c->coop_err_d, c->coop_err_h, 0));
+    {
+        int khz = 0;
+        CK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device));
+        c->wall_khz = khz > 0 ? khz : 100000.0;
+    }
     CK(hipDeviceSynchronize());
 #undef CK
     if (world > 1 && !grp) {
@@ -1941,6 +2121,9 @@ void lbk_destroy(lbk_ctx* c) {
     lbk_xgmi_destroy(c->xg);
     if (c->d_ckslot) (void)hipFree(c->d_ckslot);
     (void)hipFree(c->partials);
+    (void)hipFree(c->coop_bar);
+    (void)hipFree(c->coop_redge);
+    if (c->coop_err_h) (void)hipHostFree(c->coop_err_h);
     (void)hipFree(c->cnt);
     (void)hipFree(c->slots);
     (void)hipHostFree(c->h_slots);
@@ -2323,6 +2506,26 @@ int lbk_small_iter(lbk_ctx* c, int obj, int h, const double* g, double* q, doubl
     // algorithmic bytes: the multi-launch sequence's passes (P0 dot if computed, 4 per pair
     // pass, 3 for mid, 8 for the commit)
     const double vec = (p0_ref >= 0 ? 0.0 : 2.0) + 4.0 * (h - 1) + 3.0 + 4.0 * (h - 1) + 8.0;
+    if (c->coop_max > 0 && c->geo.nseg <= c->coop_max) {
+        // barrier arrivals of this launch: [P0] + (h-1) first-loop + mid + (h-1) second-loop + commit
+        const int passes = (p0_ref >= 0 ? 0 : 1) + 2 * h;
+        a.part = c->partials;
+        a.redge = c->coop_redge;
+        a.bar = c->coop_bar;
+        a.bar_base = c->coop_base;
+        a.err = c->coop_err_d;
+        a.timeout = (unsigned long long)(2.0 * c->wall_khz * 1e3);  // 2 s
+        c->coop_base += (unsigned long long)passes * (unsigned long long)c->geo.nseg;
+        geo.rev = 0;
+        const int nb = (int)c->geo.nseg;
+        return launch(c, LBK_K_SMALL_ITER, vec, -1, [&] {
+            switch (obj) {
+                case LBK_OBJ_ROSENBROCK: hipLaunchKernelGGL(k_coop_iter<LBK_OBJ_ROSENBROCK>, dim3(nb), dim3(LB_BLOCK), 0, c->stream, a, geo); break;
+                case LBK_OBJ_QUAD_TRIDIAG: hipLaunchKernelGGL(k_coop_iter<LBK_OBJ_QUAD_TRIDIAG>, dim3(nb), dim3(LB_BLOCK), 0, c->stream, a, geo); break;
+                default: hipLaunchKernelGGL(k_coop_iter<LBK_OBJ_QUAD_SEPARABLE>, dim3(nb), dim3(LB_BLOCK), 0, c->stream, a, geo); break;
+            }
+        });
+    }
     return launch(c, LBK_K_SMALL_ITER, vec, -1, [&] {
         switch (obj) {
             case LBK_OBJ_ROSENBROCK: hipLaunchKernelGGL(k_small_iter<LBK_OBJ_ROSENBROCK>, dim3(1), dim3(LBK_SMALL_THREADS), 0, c->stream, a, geo); break;
@@ -2333,8 +2536,9 @@ int lbk_small_iter(lbk_ctx* c, int obj, int h, const double* g, double* q, doubl
 }
 
 int lbk_small_ok(const lbk_ctx* c, int h) {
-    return c->small_seg_max > 0 && c->geo.world == 1 && c->geo.nseg <= c->small_seg_max &&
-           c->geo.nseg <= LBK_SMALL_SEGMAX && h >= 1 && h <= LBK_SMALL_HMAX;
+    if (c->geo.world != 1 || h < 1 || h > LBK_SMALL_HMAX) return 0;
+    if (c->coop_max > 0 && c->geo.nseg <= c->coop_max) return 1;
+    return c->small_seg_max > 0 && c->geo.nseg <= c->small_seg_max && c->geo.nseg <= LBK_SMALL_SEGMAX;
 }
 
 int lbk_update(lbk_ctx* c, int op, double* out, const double* a, const double* b, double rho, int slot_a,
@@ -2445,6 +2649,10 @@ int lbk_fetch_groups(lbk_ctx* c, int slot, double* groups64) {
     if (c->xg_on && lbk_xgmi_failed(c->xg)) {
         snprintf(c->err, sizeof c->err, "xgmi exchange timed out waiting for a peer");
         return -3;
+    }
+    if (*(volatile unsigned*)c->coop_err_h) {
+        snprintf(c->err, sizeof c->err, "cooperative iteration: grid barrier timed out");
+        return -2;
     }
     memcpy(groups64, h, bytes);
     return 0;

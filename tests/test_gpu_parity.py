@@ -322,3 +322,24 @@ def test_small_persistent_iteration_bit_exact(monkeypatch, n, m, ls):
     assert np.array_equal(a["tr_c1"], b["tr_c1"]) and a["messages"] == b["messages"]
     o = O.lbfgs("rosenbrock", x0, ls, m, 60, 1e-5, mode=O.CANON)
     assert np.array_equal(bits(b["tr_f"]), bits(o["f"]))
+
+
+@pytest.mark.parametrize("n,m,ls", [(10_000, 5, "backtracking"), (30_001, 16, "wolfe"), (4097, 7, "interpolation"),
+                                    (20_000, 10, "backtracking_wolfe"), (32_768, 1, "backtracking")])
+def test_cooperative_iteration_bit_exact(monkeypatch, n, m, ls):
+    """The cooperative multi-workgroup iteration (LBFGS_COOP: one workgroup per segment, grid
+    barriers between passes, the whole two-loop and the commit at a0 in one launch) against the
+    multi-launch sequence and the oracle: identical bits."""
+    x0 = L.x0_uniform(n, 3, -2.0, 2.0)
+    out = []
+    for coop in ("0", "1"):
+        monkeypatch.setenv("LBFGS_COOP", coop)
+        with L.Context(n, m) as c:
+            out.append(c.minimize("rosenbrock", x0, ls, 60, trace=True))
+    a, b = out
+    assert b["passes"] < a["passes"]  # the cooperative path really ran
+    for key in ("tr_f", "tr_gnorm", "x"):
+        assert np.array_equal(bits(a[key]), bits(b[key])), key
+    assert np.array_equal(a["tr_c1"], b["tr_c1"]) and a["messages"] == b["messages"]
+    o = O.lbfgs("rosenbrock", x0, ls, m, 60, 1e-5, mode=O.CANON)
+    assert np.array_equal(bits(b["tr_f"]), bits(o["f"]))
