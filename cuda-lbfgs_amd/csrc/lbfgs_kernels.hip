@@ -1431,7 +1431,7 @@ __global__ __launch_bounds__(LBK_SMALL_THREADS) void k_small_iter(SmallArgs a, G
 //     the commit's stencil halo across segments reads the last r pass's published edge values.
 // A barrier that waits past its timeout sets *err (pinned host memory) instead of hanging.
 // ---------------------------------------------------------------------------------------
-#define LBK_COOP_SEGMAX 64
+#define LBK_COOP_SEGMAX 512  // one group; resident at 2 workgroups per CU
 
 template <int K, class Op>
 __device__ __forceinline__ void coop_pass(const Op& op, const Geo& geo, const SmallArgs& a, int pass,
@@ -1481,22 +1481,54 @@ __device__ __forceinline__ void coop_pass(const Op& op, const Geo& geo, const Sm
         }
     }
     __syncthreads();
-    // every workgroup: the fixed-order totals from the <= 64 partials (wave w: components w, w+4)
+    // every workgroup: the fixed-order totals of this pass (the group tree of stage 2, then the
+    // 8-group sum with groups 1..7 empty)
+    if (geo.nseg <= 64) {  // wave w: components w, w + 4; lane j: entry j (the small-group form)
 #pragma unroll
-    for (int k = w; k < K; k += 4) {
-        const double p = lane < geo.nseg ? bitsd(__hip_atomic_load(
-                                               reinterpret_cast<const unsigned long long*>(P + (int64_t)k * LBK_SEGS + lane),
-                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-                                         : 0.0;
-        const double q0 = wave_sum(p) + 0.0;  // group 0: the tree's levels above 64 add 0.0
-        if (lane == 0) {
-            double tt = q0;  // slot_total: groups 1..7 hold no segment
+        for (int k = w; k < K; k += 4) {
+            const double p = lane < geo.nseg ? bitsd(__hip_atomic_load(
+                                                   reinterpret_cast<const unsigned long long*>(P + (int64_t)k * LBK_SEGS + lane),
+                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                                             : 0.0;
+            const double q0 = wave_sum(p) + 0.0;  // group 0: the tree's levels above 64 add 0.0
+            if (lane == 0) {
+                double tt = q0;
+#pragma unroll
+                for (int g = 1; g < LBK_GROUPS; ++g) tt = tt + 0.0;
+                tl[k] = tt;
+                if (b == 0 && slot) {
+                    slot[k] = q0;
+                    if (hslot) hslot[k] = q0;
+                }
+            }
+        }
+    } else {  // the general form: thread t entries 4t..4t+3, wave butterfly, ((w0+w1)+(w2+w3))
+        double p[K][4];
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int j = 4 * t + i;
+                p[k][i] = j < geo.nseg ? bitsd(__hip_atomic_load(
+                                              reinterpret_cast<const unsigned long long*>(P + (int64_t)k * LBK_SEGS + j),
+                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                                        : 0.0;
+            }
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const double q = wave_sum((p[k][0] + p[k][1]) + (p[k][2] + p[k][3]));
+            if (lane == 0) lds[w][k] = q;
+        }
+        __syncthreads();
+        if (t < K) {
+            const double q0 = (lds[0][t] + lds[1][t]) + (lds[2][t] + lds[3][t]);
+            double tt = q0;
 #pragma unroll
             for (int g = 1; g < LBK_GROUPS; ++g) tt = tt + 0.0;
-            tl[k] = tt;
+            tl[t] = tt;
             if (b == 0 && slot) {
-                slot[k] = q0;
-                if (hslot) hslot[k] = q0;
+                slot[t] = q0;
+                if (hslot) hslot[t] = q0;
             }
         }
     }
@@ -2035,10 +2067,12 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
     // segment step, more than the kernel boundaries it removes. Off by default.
     c->small_seg_max = 0;
     if (const char* e = getenv("LBFGS_SMALL_SEGS")) c->small_seg_max = atoi(e);
-    // measured +48 % at n = 1e4 (15.1k -> 22.4k it/s) and +41 % at 3e4, bit-identical
-    // (tests/test_gpu_parity.py::test_cooperative_iteration_bit_exact); LBFGS_COOP=0 disables
-    c->coop_max = LBK_COOP_SEGMAX;
-    if (const char* e = getenv("LBFGS_COOP")) c->coop_max = atoi(e) ? LBK_COOP_SEGMAX : 0;
+    // measured (profiles/r01/coop_ab.txt): +48 % at n = 1e4 (14-15k -> 22k it/s), +41 % at 3e4,
+    // +22 % at 1e5 (196 segments); -22 % at 391 segments and -38 % at 508, where the barrier's
+    // fan-in and every workgroup's read of all partials outweigh the saved launches. Bit-identical
+    // (tests/test_gpu_parity.py::test_cooperative_iteration_bit_exact). LBFGS_COOP=<segments>.
+    c->coop_max = 256;
+    if (const char* e = getenv("LBFGS_COOP")) c->coop_max = std::min(atoi(e), LBK_COOP_SEGMAX);  // max segments
     // measured +1 % at n = 1e7 (default and vector-free), +1 % vector-free and neutral default at
     // 1e8 (profiles/r01/rev_ab.txt); bit-identical either way (per-segment partials)
     c->rev_on = 1;

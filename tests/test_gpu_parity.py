@@ -311,6 +311,7 @@ def test_small_persistent_iteration_bit_exact(monkeypatch, n, m, ls):
     identical bits, including every rejected-step recommit that reads its slots."""
     x0 = L.x0_uniform(n, 3, -2.0, 2.0)
     out = []
+    monkeypatch.setenv("LBFGS_COOP", "0")  # the single-workgroup form, not the cooperative one
     for segs in ("0", "256"):
         monkeypatch.setenv("LBFGS_SMALL_SEGS", segs)
         with L.Context(n, m) as c:
@@ -325,14 +326,15 @@ def test_small_persistent_iteration_bit_exact(monkeypatch, n, m, ls):
 
 
 @pytest.mark.parametrize("n,m,ls", [(10_000, 5, "backtracking"), (30_001, 16, "wolfe"), (4097, 7, "interpolation"),
-                                    (20_000, 10, "backtracking_wolfe"), (32_768, 1, "backtracking")])
+                                    (20_000, 10, "backtracking_wolfe"), (32_768, 1, "backtracking"),
+                                    (100_000, 10, "backtracking"), (200_001, 6, "wolfe")])
 def test_cooperative_iteration_bit_exact(monkeypatch, n, m, ls):
     """The cooperative multi-workgroup iteration (LBFGS_COOP: one workgroup per segment, grid
     barriers between passes, the whole two-loop and the commit at a0 in one launch) against the
     multi-launch sequence and the oracle: identical bits."""
     x0 = L.x0_uniform(n, 3, -2.0, 2.0)
     out = []
-    for coop in ("0", "1"):
+    for coop in ("0", "512"):  # LBFGS_COOP = the largest segment count that runs cooperatively
         monkeypatch.setenv("LBFGS_COOP", coop)
         with L.Context(n, m) as c:
             out.append(c.minimize("rosenbrock", x0, ls, 60, trace=True))
