@@ -314,7 +314,11 @@ def main():
 
     x0 = L.x0_uniform(n, 42, -2.0, 2.0)
     # BENCH_DEVICE_MOD=k maps rank -> device local_rank % k (rehearsing several ranks on fewer GPUs)
+    # a launcher that exposes one device per process (HIP_VISIBLE_DEVICES) leaves local_rank >= count
+    ndev = max(L.device_count(), 1)
     dev = D.local_rank % int(os.environ["BENCH_DEVICE_MOD"]) if "BENCH_DEVICE_MOD" in os.environ else D.local_rank
+    if dev >= ndev:
+        dev = dev % ndev
     T, res, prof, bytes_all, done_steps, (backend, xlat) = measure(a, D, n, x0, dev, rank, world, uid,
                                                   unfused=a.unfused, vector_free=a.vector_free)
     # the opt-in vector-free mode alongside the default (outside the bit-parity contract with

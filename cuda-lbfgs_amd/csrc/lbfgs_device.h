@@ -105,6 +105,7 @@ void lbk_destroy(lbk_ctx* c);
 const lbk_geo* lbk_geometry(const lbk_ctx* c);
 const char* lbk_last_error(const lbk_ctx* c);
 int lbk_unique_id(void* out128);
+int lbk_device_count(void);
 /* sharded contexts (world > 1, one process per GPU): peer mailboxes over xGMI (lbfgs_xgmi.h).
  * handle: LBK_PEER_HANDLE_BYTES = 64; connect maps all peers' mailboxes (world handles in rank
  * order) and self-tests the exchange; enable switches every later exchange to it. */

@@ -194,6 +194,8 @@ void lbfgs_constants_cuda(lbfgs_constants* k) { /* parallel-implementation/const
 
 int lbfgs_unique_id(void* out128) { return lbk_unique_id(out128) == 0 ? 0 : LBFGS_ERR_RCCL; }
 
+int lbfgs_device_count(void) { return lbk_device_count(); }
+
 static void free_vectors(lbfgs_ctx* c) {
     double** v[] = {&c->x, &c->g, &c->xn, &c->gn, &c->d, &c->q, &c->r, &c->gt, &c->q2, &c->r2};
     for (size_t i = 0; i < sizeof v / sizeof v[0]; ++i) {

@@ -1984,6 +1984,11 @@ int vf_exchange_ghosts(lbk_ctx* c, int wslot, double* x, double* g, double* s, d
 
 extern "C" {
 
+int lbk_device_count(void) {
+    int n = 0;
+    return hipGetDeviceCount(&n) == hipSuccess ? n : 0;
+}
+
 int lbk_unique_id(void* out128) {
     ncclUniqueId id;
     if (ncclGetUniqueId(&id) != ncclSuccess) return -3;

@@ -73,6 +73,7 @@ def lib():
     L.lbfgs_ctx_create_sharded.argtypes = [C.POINTER(vp), C.c_int64, C.c_int, C.c_int, C.c_int,
                                            C.c_int, C.c_char_p]
     L.lbfgs_unique_id.argtypes = [C.c_char_p]
+    L.lbfgs_device_count.argtypes = []
     L.lbfgs_host_group_create.argtypes = [C.POINTER(vp), C.c_int]
     L.lbfgs_host_group_destroy.argtypes = [vp]
     L.lbfgs_host_group_destroy.restype = None
@@ -130,7 +131,7 @@ EXPORTED_SYMBOLS = [
     "lbfgs_dev_dot", "lbfgs_dev_norm", "lbfgs_dev_objective", "lbfgs_dev_trial",
     "lbfgs_dev_twoloop", "lbfgs_dev_elementwise", "lbfgs_line_search", "lbfgs_prof_enable",
     "lbfgs_prof_reset", "lbfgs_prof_get", "lbfgs_peer_handle", "lbfgs_peer_connect", "lbfgs_peer_enable",
-    "lbfgs_exchange_backend", "lbfgs_exchange_latency",
+    "lbfgs_exchange_backend", "lbfgs_exchange_latency", "lbfgs_device_count",
 ]
 PEER_HANDLE_BYTES = 64
 BACKENDS = {0: "single", 1: "rccl", 2: "xgmi", 3: "host-group"}
@@ -149,6 +150,10 @@ def shard_range(n, rank, world):
     if rc != 0:
         raise LbfgsError(f"cannot shard n={n} over {world} ranks")
     return lo.value, nl.value
+
+
+def device_count():
+    return int(lib().lbfgs_device_count())
 
 
 def unique_id():

@@ -132,6 +132,8 @@ int lbfgs_ctx_create(lbfgs_ctx** out, int64_t n, int m, int device);
 int lbfgs_ctx_create_sharded(lbfgs_ctx** out, int64_t n, int m, int device, int rank, int world,
                              const void* unique_id);
 int lbfgs_unique_id(void* out128);
+/* HIP devices visible to this process (0 when none) */
+int lbfgs_device_count(void);
 /* unique_id may be NULL: no RCCL communicator; the context then exchanges its reductions only
  * through the xGMI peer mailboxes below (lbfgs_peer_*), which must be connected and enabled
  * before the first solve.
