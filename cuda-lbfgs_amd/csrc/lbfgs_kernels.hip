@@ -53,6 +53,7 @@ struct Geo {
     int g_lo, g_hi;
     int spg;            // segments per group (1024; fewer, longer segments in the vector-free commit)
     int rev;            // 1: workgroup b takes the rank's segment nblocks-1-b (see LBFGS_REV)
+    const double* ppart;  // deferred stage 2: the producer's partials of this launch's first source
     double* edge_slot;  // sharded: where d[0] / d[n_loc-1] of this rank are published
 };
 
@@ -332,6 +333,32 @@ __global__ __launch_bounds__(LB_BLOCK) void k_group_reduce_wide(const double* __
         slot[g * kstride + k0 + t] = v;
         if (hslot) hslot[g * kstride + k0 + t] = v;
     }
+}
+
+// Total of a launch's first source slot (the previous pass's reduction). Normally stage 2 ran
+// after the producer (k_group_reduce or tickets) and the slot holds the group values. With a
+// deferred stage 2 (geo.ppart, mid n on one rank) every workgroup of the consuming launch forms
+// the group trees from the producer's partials itself - the same trees, so the same bits - and
+// workgroup 0 stores the group values into the slot for later readers. One kernel boundary and
+// the stage-2 launch per pass disappear; the price is each workgroup reading <= 2048 partials.
+__device__ __forceinline__ double src_total(const double* slot, const Geo& geo) {
+    if (!geo.ppart) return slot_total(slot);
+    __shared__ double gv[LBK_GROUPS];
+    __shared__ double ldt[4][1];
+    const int ng = (int)((geo.nseg + LBK_SEG_PER_GROUP - 1) / LBK_SEG_PER_GROUP);
+    for (int g = 0; g < LBK_GROUPS; ++g) {
+        if (g < ng)
+            group_tree<1, false>(geo.ppart, (int64_t)g * LBK_SEG_PER_GROUP, (int64_t)g * LBK_SEG_PER_GROUP, geo.nseg,
+                                 LBK_SEG_PER_GROUP, &gv[g], nullptr, ldt);
+        else if (threadIdx.x == 0)
+            gv[g] = 0.0;  // a group with no segment: the slot's 0.0
+        __syncthreads();
+    }
+    if (blockIdx.x == 0 && threadIdx.x < ng) const_cast<double*>(slot)[threadIdx.x * LBK_KMAX] = gv[threadIdx.x];
+    double t = gv[0];
+#pragma unroll
+    for (int g = 1; g < LBK_GROUPS; ++g) t = t + gv[g];
+    return t;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -681,7 +708,7 @@ template <bool NT>
 __global__ __launch_bounds__(LB_BLOCK) void k_axpy_dot(double* qout, const double* qin, const double* __restrict__ y,
                                                        const double* __restrict__ sv, double rho,
                                                        const double* __restrict__ prev, Geo geo, Red red) {
-    const double alpha = rho * slot_total(prev);
+    const double alpha = rho * src_total(prev, geo);
     run_pass<OpAxpyDot<NT>, 1>(OpAxpyDot<NT>{qout, qin, y, sv, alpha}, geo, red);
 }
 
@@ -689,7 +716,7 @@ template <bool NT>
 __global__ __launch_bounds__(LB_BLOCK) void k_mid(double* __restrict__ rout, const double* __restrict__ qin,
                                                   const double* __restrict__ y0, double rho0, double gamma,
                                                   const double* __restrict__ prev, Geo geo, Red red) {
-    const double alpha = rho0 * slot_total(prev);
+    const double alpha = rho0 * src_total(prev, geo);
     run_pass<OpMid<NT>, 1>(OpMid<NT>{rout, qin, y0, alpha, gamma, geo.edge_slot, geo.n_loc, geo.g_lo, geo.g_hi}, geo,
                            red);
 }
@@ -700,7 +727,7 @@ __global__ __launch_bounds__(LB_BLOCK) void k_axpy2_dot(double* r, const double*
                                                         const double* __restrict__ yn, double rho,
                                                         const double* __restrict__ pb, const double* __restrict__ pa,
                                                         Geo geo, Red red) {
-    const double beta = rho * slot_total(pb);
+    const double beta = rho * src_total(pb, geo);
     const double alpha = rho * slot_total(pa);
     run_pass<OpAxpy2Dot<NT>, 1>(
         OpAxpy2Dot<NT>{r, rin, sv, yn, alpha - beta, geo.edge_slot, geo.n_loc, geo.g_lo, geo.g_hi}, geo, red);
@@ -711,7 +738,7 @@ __global__ __launch_bounds__(LB_BLOCK) void k_last(double* __restrict__ dout, co
                                                    const double* __restrict__ sv, const double* __restrict__ g,
                                                    double rho, const double* __restrict__ pb,
                                                    const double* __restrict__ pa, Geo geo, Red red) {
-    const double beta = rho * slot_total(pb);
+    const double beta = rho * src_total(pb, geo);
     const double alpha = rho * slot_total(pa);
     run_pass<OpLast<NT>, 1>(OpLast<NT>{dout, r, sv, g, alpha - beta, geo.edge_slot, geo.n_loc, geo.g_lo, geo.g_hi},
                              geo, red);
@@ -927,7 +954,7 @@ __global__ __launch_bounds__(LB_BLOCK) void k_commit(const double* __restrict__ 
                                                      double* __restrict__ so, double* __restrict__ yo,
                                                      Geo geo, Red red) {
     if (DMODE == LBK_D_TWOLOOP) {
-        const double beta = da.rho * slot_total(da.pb);
+        const double beta = da.rho * src_total(da.pb, geo);
         const double alph = da.rho * slot_total(da.pa);
         da.coef = alph - beta;  // r[j] += s[j] * (alpha[i] - beta)  (lbfgs.cpp:137)
     }
@@ -1746,6 +1773,14 @@ struct lbk_ctx {
     // LBFGS_REV=1: every other pass walks its segments last to first, so a pass starts on the
     // tail of the vector its predecessor wrote last (still in the Infinity Cache / L2)
     int rev_on, rev_par;
+    // deferred stage 2 (src_total): single-component two-loop reductions with
+    // coop_max < nseg <= defer_max leave their partials for the consuming pass
+    int defer_max;
+    int defer_now;        // the launch in progress defers its stage 2
+    int defer_region;     // partials region (component) the next deferred producer writes
+    int pend_slot;        // slot whose stage 2 is still pending (-1: none)
+    const double* pend_part;
+    int pend_taken;       // the launch in progress consumes it
     // cooperative small-n iteration (k_coop_iter): nseg <= coop_max (0: off)
     int coop_max;
     unsigned long long* coop_bar;  // device arrival counter
@@ -1780,6 +1815,7 @@ Geo kgeo(const lbk_ctx* c) {
     g.g_hi = c->geo.g_hi;
     g.spg = LBK_SEG_PER_GROUP;
     g.rev = c->rev_on ? c->rev_par : 0;
+    g.ppart = nullptr;
     g.edge_slot = nullptr;
     return g;
 }
@@ -1910,10 +1946,49 @@ int exchange_buf(lbk_ctx* c, double* base, int ks) {
 
 int exchange_slot(lbk_ctx* c, int slot) { return exchange_buf(c, slot_base(c, slot), slot_stride(slot)); }
 
+// Deferred partials live in the two highest components of the partials array: a consuming launch
+// reads them while its own workgroups store their partials (components 0..K-1, K <= 87), and a
+// deferred producer and its consumer alternate between the two.
+double* defer_part(const lbk_ctx* c, int region) { return c->partials + (int64_t)(LBK_KW - 2 + region) * LBK_SEGS; }
+
+// a pending (deferred) stage 2 that no consumer took: run it as the reduce kernel now
+int flush_pending(lbk_ctx* c) {
+    if (c->pend_slot < 0) return 0;
+    const Geo g = kgeo(c);
+    hipLaunchKernelGGL(k_group_reduce<1>, dim3(c->geo.g_hi - c->geo.g_lo), dim3(LB_BLOCK), 0, c->stream, c->pend_part,
+                       g, slot_base(c, c->pend_slot), (double*)nullptr, LBK_KMAX);
+    HIPCHK(c, hipGetLastError());
+    c->pend_slot = -1;
+    return 0;
+}
+
+// A single-component reduction into `slot` may leave its stage 2 to the next pass (returns the
+// Red to launch with; sets defer_now). Only on one rank, with the reduce-kernel stage 2, and for
+// segment counts where every consumer workgroup reading all partials is cheaper than a launch.
+Red kred_deferrable(lbk_ctx* c, int slot) {
+    Red r = kred(c, slot);
+    if (c->geo.world == 1 && !c->ticket && c->geo.nseg > c->coop_max && c->geo.nseg <= c->defer_max) {
+        r.partials = defer_part(c, c->defer_region);
+        c->defer_now = 1;
+    }
+    return r;
+}
+
+// the consumer side: the partials of `ref`'s slot if its stage 2 is pending (and take it)
+const double* take_pending(lbk_ctx* c, int ref) {
+    if (c->pend_slot < 0 || c->pend_slot != ref / LBK_KMAX) return nullptr;
+    c->pend_taken = 1;
+    return c->pend_part;
+}
+
 // launch wrapper: byte accounting, optional event timing, all-gather of group partials
 template <class F>
 int launch(lbk_ctx* c, int kind, double vec_passes, int slot, F&& fn, int K = 1, bool exchange = true,
            const Geo* gv = nullptr) {
+    if (c->pend_slot >= 0 && !c->pend_taken) {
+        const int rc = flush_pending(c);
+        if (rc) return rc;
+    }
     const double bytes = vec_passes * 8.0 * (double)c->geo.n_loc;
     c->bytes_total += bytes;
     hipEvent_t a = nullptr, b = nullptr;
@@ -1933,14 +2008,23 @@ int launch(lbk_ctx* c, int kind, double vec_passes, int slot, F&& fn, int K = 1,
         HIPCHK(c, hipEventRecord(b, c->stream));
         c->pending.push_back({kind, a, b, bytes});
         a = b = nullptr;
-        if (slot >= 0 && !c->ticket) {
+        if (slot >= 0 && !c->ticket && !c->defer_now) {
             a = ev_get(c);
             b = ev_get(c);
             if (a) HIPCHK(c, hipEventRecord(a, c->stream));
             kind = LBK_K_GROUP_REDUCE;
         }
     }
-    if (slot >= 0 && !c->ticket) {
+    if (c->pend_taken) {  // the consumer's workgroup 0 stored the pending slot's group values
+        c->pend_slot = -1;
+        c->pend_taken = 0;
+    }
+    if (c->defer_now) {
+        c->pend_slot = slot;
+        c->pend_part = defer_part(c, c->defer_region);
+        c->defer_region ^= 1;
+        c->defer_now = 0;
+    } else if (slot >= 0 && !c->ticket) {
         const Geo g = gv ? *gv : kgeo(c);
         double* sl = slot_base(c, slot);
         double* hs = mirrored(c, slot, K) ? slot_dhost(c, slot) : nullptr;
@@ -2078,6 +2162,11 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
     // (tests/test_gpu_parity.py::test_cooperative_iteration_bit_exact). LBFGS_COOP=<segments>.
     c->coop_max = 256;
     if (const char* e = getenv("LBFGS_COOP")) c->coop_max = std::min(atoi(e), LBK_COOP_SEGMAX);  // max segments
+    c->pend_slot = -1;
+    // measured (profiles/r01/defer_ab.txt): +21..32 % at n = 3e5 (586 segments); -14 % at 1954
+    // segments and worse beyond, where every workgroup forms two or more group trees
+    c->defer_max = LBK_SEG_PER_GROUP;
+    if (const char* e = getenv("LBFGS_DEFER")) c->defer_max = atoi(e);  // max segments
     // measured +1 % at n = 1e7 (default and vector-free), +1 % vector-free and neutral default at
     // 1e8 (profiles/r01/rev_ab.txt); bit-identical either way (per-segment partials)
     c->rev_on = 1;
@@ -2252,7 +2341,7 @@ int lbk_copy(lbk_ctx* c, double* dst, const double* src) {
 
 int lbk_dot(lbk_ctx* c, const double* a, const double* b, int slot) {
     Geo g = kgeo(c);
-    Red r = kred(c, slot);
+    Red r = kred_deferrable(c, slot);
     return launch(c, LBK_K_DOT, 2, slot, [&] {
         NT_DISPATCH(c, hipLaunchKernelGGL(k_dot<NT_>, dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, a, b, g, r));
     });
@@ -2261,7 +2350,8 @@ int lbk_dot(lbk_ctx* c, const double* a, const double* b, int slot) {
 int lbk_axpy_dot(lbk_ctx* c, double* qout, const double* qin, const double* y, const double* s, double rho,
                  int ref_alpha, int slot) {
     Geo g = kgeo(c);
-    Red r = kred(c, slot);
+    g.ppart = take_pending(c, ref_alpha);
+    Red r = kred_deferrable(c, slot);
     const double* pa = sref(c, ref_alpha);
     return launch(c, LBK_K_AXPY_DOT, 4, slot, [&] {
         NT_DISPATCH(c, hipLaunchKernelGGL(k_axpy_dot<NT_>, dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, qout, qin, y, s, rho, pa, g, r));
@@ -2271,7 +2361,8 @@ int lbk_axpy_dot(lbk_ctx* c, double* qout, const double* qin, const double* y, c
 int lbk_mid(lbk_ctx* c, double* rout, const double* qin, const double* y0, double rho0, double gamma,
             int ref_alpha, int slot) {
     Geo g = kgeo(c);
-    Red r = kred(c, slot);
+    g.ppart = take_pending(c, ref_alpha);
+    Red r = kred_deferrable(c, slot);
     const double* pa = sref(c, ref_alpha);
     if (c->geo.world > 1) g.edge_slot = r.slot;
     return launch(c, LBK_K_MID, 3, slot, [&] {
@@ -2282,7 +2373,8 @@ int lbk_mid(lbk_ctx* c, double* rout, const double* qin, const double* y0, doubl
 int lbk_axpy2_dot(lbk_ctx* c, double* rr, const double* rin, const double* s, const double* ynext, double rho,
                   int ref_beta, int ref_alpha, int slot) {
     Geo g = kgeo(c);
-    Red r = kred(c, slot);
+    g.ppart = take_pending(c, ref_beta);
+    Red r = kred_deferrable(c, slot);
     const double* pb = sref(c, ref_beta);
     const double* pa = sref(c, ref_alpha);
     if (c->geo.world > 1) g.edge_slot = r.slot;
@@ -2294,6 +2386,7 @@ int lbk_axpy2_dot(lbk_ctx* c, double* rr, const double* rin, const double* s, co
 int lbk_last(lbk_ctx* c, double* dout, const double* rr, const double* s, const double* gg, double rho,
              int ref_beta, int ref_alpha, int slot) {
     Geo g = kgeo(c);
+    g.ppart = take_pending(c, ref_beta);
     Red r = kred(c, slot);
     const double* pb = sref(c, ref_beta);
     const double* pa = sref(c, ref_alpha);
@@ -2366,6 +2459,7 @@ int lbk_commit(lbk_ctx* c, int obj, int dmode, const double* x, const double* ds
     if (dmode == LBK_D_TWOLOOP) {
         da.pa = sref(c, ref_alpha);
         da.pb = sref(c, ref_beta);
+        g.ppart = take_pending(c, ref_beta);
     }
     double passes = 4.0 + (dmode == LBK_D_BUF ? 3.0 : dmode == LBK_D_NEG_G ? 2.0 : 4.0);
     return launch(c, LBK_K_COMMIT, passes, slot, [&] {
@@ -2680,6 +2774,8 @@ double lbk_total(const double* groups64, int comp) {
 }
 
 int lbk_fetch_groups(lbk_ctx* c, int slot, double* groups64) {
+    const int frc = flush_pending(c);
+    if (frc) return frc;
     double* h = slot_host(c, slot);
     const size_t bytes = sizeof(double) * LBK_GROUPS * slot_stride(slot);
     if (!c->slot_mirror[slot < LBK_NSLOTS ? slot : LBK_NSLOTS + slot - LBK_WSLOT0])

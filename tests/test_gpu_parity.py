@@ -345,3 +345,29 @@ def test_cooperative_iteration_bit_exact(monkeypatch, n, m, ls):
     assert np.array_equal(a["tr_c1"], b["tr_c1"]) and a["messages"] == b["messages"]
     o = O.lbfgs("rosenbrock", x0, ls, m, 60, 1e-5, mode=O.CANON)
     assert np.array_equal(bits(b["tr_f"]), bits(o["f"]))
+
+
+@pytest.mark.parametrize("n,m,ls,obj", [(300_000, 10, "backtracking", "rosenbrock"),
+                                        (1_000_001, 5, "wolfe", "rosenbrock"),
+                                        (2_000_000, 7, "interpolation", "quad_tridiag")])
+def test_deferred_stage2_bit_exact(monkeypatch, n, m, ls, obj):
+    """Deferred stage 2 (LBFGS_DEFER: every workgroup of the consuming pass forms the previous
+    pass's total from its partials; no reduce launch between two-loop passes) against the
+    reduce-kernel sequence and the oracle: identical bits."""
+    x0 = L.x0_uniform(n, 5, -2.0, 2.0)
+    out = []
+    for defer in ("0", "8192"):
+        monkeypatch.setenv("LBFGS_DEFER", defer)
+        with L.Context(n, m) as c:
+            c.prof_reset()
+            c.prof_enable(True)
+            r = c.minimize(obj, x0, ls, 14, trace=True)
+            r["reduce_launches"] = c.prof_get("group_reduce")["launches"]
+            out.append(r)
+    a, b = out
+    assert b["reduce_launches"] < a["reduce_launches"]  # the deferred path really ran
+    for key in ("tr_f", "tr_gnorm", "x"):
+        assert np.array_equal(bits(a[key]), bits(b[key])), key
+    assert np.array_equal(a["tr_c1"], b["tr_c1"]) and a["messages"] == b["messages"]
+    o = O.lbfgs(obj, x0, ls, m, 14, 1e-5, mode=O.CANON)
+    assert np.array_equal(bits(b["tr_f"]), bits(o["f"]))
