@@ -346,12 +346,14 @@ __device__ __forceinline__ double src_total(const double* slot, const Geo& geo) 
     __shared__ double gv[LBK_GROUPS];
     __shared__ double ldt[4][1];
     const int ng = (int)((geo.nseg + LBK_SEG_PER_GROUP - 1) / LBK_SEG_PER_GROUP);
-    for (int g = 0; g < LBK_GROUPS; ++g) {
-        if (g < ng)
-            group_tree<1, false>(geo.ppart, (int64_t)g * LBK_SEG_PER_GROUP, (int64_t)g * LBK_SEG_PER_GROUP, geo.nseg,
-                                 LBK_SEG_PER_GROUP, &gv[g], nullptr, ldt);
-        else if (threadIdx.x == 0)
-            gv[g] = 0.0;  // a group with no segment: the slot's 0.0
+    // one group tree per group with segments (group_tree's registers only: a form that loads every
+    // group at once raised the pass kernels from 68-70 to 74-80 VGPRs, one wave per SIMD fewer, and
+    // ran slower); groups without a segment are the slot's 0.0
+    if (threadIdx.x < LBK_GROUPS) gv[threadIdx.x] = 0.0;
+    __syncthreads();
+    for (int g = 0; g < ng; ++g) {
+        group_tree<1, false>(geo.ppart, (int64_t)g * LBK_SEG_PER_GROUP, (int64_t)g * LBK_SEG_PER_GROUP, geo.nseg,
+                             LBK_SEG_PER_GROUP, &gv[g], nullptr, ldt);
         __syncthreads();
     }
     if (blockIdx.x == 0 && threadIdx.x < ng) const_cast<double*>(slot)[threadIdx.x * LBK_KMAX] = gv[threadIdx.x];
