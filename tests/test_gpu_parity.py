@@ -371,3 +371,20 @@ def test_deferred_stage2_bit_exact(monkeypatch, n, m, ls, obj):
     assert np.array_equal(a["tr_c1"], b["tr_c1"]) and a["messages"] == b["messages"]
     o = O.lbfgs(obj, x0, ls, m, 14, 1e-5, mode=O.CANON)
     assert np.array_equal(bits(b["tr_f"]), bits(o["f"]))
+
+
+@pytest.mark.parametrize("vector_free", [False, True])
+def test_full_run_to_convergence_bit_exact(vector_free):
+    """BASELINE configs[0] to convergence (Rosenbrock n=1e4, m=5, backtracking, tol 1e-5: ~17k
+    iterations through the cooperative kernel, or the vector-free commit): every f, |g|, alpha,
+    the final x and the whole message stream bit-identical to the oracle's restatement."""
+    n, m = 10_000, 5
+    x0 = L.x0_uniform(n, 42, -2.0, 2.0)
+    with L.Context(n, m) as c:
+        r = c.minimize("rosenbrock", x0, "backtracking", 30_000, trace=True, vector_free=vector_free)
+    o = O.lbfgs("rosenbrock", x0, "backtracking", m, 30_000, 1e-5, mode=O.CANON, vector_free=vector_free)
+    assert r["status"] == o["status"] == "converged" and r["iterations"] == o["iters"] > 15_000
+    assert np.array_equal(bits(r["tr_f"]), bits(o["f"]))
+    assert np.array_equal(bits(r["tr_gnorm"]), bits(o["gnorm"]))
+    assert np.array_equal(bits(r["x"]), bits(o["x"]))
+    assert r["messages"] == o["messages"]
