@@ -1770,6 +1770,7 @@ struct lbk_ctx {
     lbk_group* grp;  // emulated ranks: host exchange group (tests; NULL with RCCL)
     lbk_xgmi* xg;    // sharded, one process per GPU: peer mailboxes over xGMI (lbfgs_xgmi.hip)
     int xg_on;       // 1: exchanges go through xg instead of RCCL
+    int xg_mirror;   // 1: xg exchanges of host-read slots also fill the host mirror
     uint64_t* d_ckslot;  // [LBK_GROUPS][2] checksum words for the peer exchange
     int small_seg_max;  // persistent single-workgroup iteration when nseg <= this (0: off)
     // LBFGS_REV=1: every other pass walks its segments last to first, so a pass starts on the
@@ -1915,7 +1916,7 @@ int prof_flush(lbk_ctx* c) {
 // Sharded runs: each rank owns groups [g_lo, g_hi) of every result slot; gather them so
 // every rank holds all 8 (one RCCL all-gather of (8/world) x KMAX doubles per reduction, in
 // place, on the solver stream), or through the host group for emulated ranks.
-int exchange_buf(lbk_ctx* c, double* base, int ks) {
+int exchange_buf(lbk_ctx* c, double* base, int ks, double* host_mirror = nullptr) {
     const int per = (c->geo.g_hi - c->geo.g_lo) * ks;
     if (c->grp) {
         lbk_group* G = c->grp;
@@ -1928,7 +1929,7 @@ int exchange_buf(lbk_ctx* c, double* base, int ks) {
         return 0;
     }
     if (c->xg_on) {
-        if (lbk_xgmi_exchange(c->xg, c->stream, base, ks, c->geo.g_lo, c->geo.g_hi) != 0) {
+        if (lbk_xgmi_exchange(c->xg, c->stream, base, ks, c->geo.g_lo, c->geo.g_hi, host_mirror) != 0) {
             snprintf(c->err, sizeof c->err, "xgmi exchange launch failed");
             return -3;
         }
@@ -1946,7 +1947,18 @@ int exchange_buf(lbk_ctx* c, double* base, int ks) {
     return 0;
 }
 
-int exchange_slot(lbk_ctx* c, int slot) { return exchange_buf(c, slot_base(c, slot), slot_stride(slot)); }
+// Over the peer mailboxes the exchange kernel also completes the host mirror of the slots the
+// host reads back (as the stage 2 does on one rank, see mirrored()): no device-to-host copy
+// before those reads
+int exchange_slot(lbk_ctx* c, int slot, int K = 1, bool host_read = true) {
+    double* hm = nullptr;
+    if (host_read && c->xg_on && c->xg_mirror && !c->grp && (K >= 2 || slot >= LBK_NSLOTS))
+        hm = slot < LBK_NSLOTS ? c->dh_slots + (int64_t)slot * LBK_SLOT
+                               : c->dh_wslots + (int64_t)(slot - LBK_WSLOT0) * LBK_WSLOT;
+    const int rc = exchange_buf(c, slot_base(c, slot), slot_stride(slot), hm);
+    c->slot_mirror[slot < LBK_NSLOTS ? slot : LBK_NSLOTS + slot - LBK_WSLOT0] = rc == 0 && hm != nullptr;
+    return rc;
+}
 
 // Deferred partials live in the two highest components of the partials array: a consuming launch
 // reads them while its own workgroups store their partials (components 0..K-1, K <= 87), and a
@@ -2047,7 +2059,7 @@ int launch(lbk_ctx* c, int kind, double vec_passes, int slot, F&& fn, int K = 1,
         HIPCHK(c, hipEventRecord(b, c->stream));
         c->pending.push_back({kind, a, b, 0.0});
     }
-    if (exchange && c->geo.world > 1 && slot >= 0) return exchange_slot(c, slot);
+    if (exchange && c->geo.world > 1 && slot >= 0) return exchange_slot(c, slot, K);
     return 0;
 }
 
@@ -2058,7 +2070,7 @@ int vf_exchange_ghosts(lbk_ctx* c, int wslot, double* x, double* g, double* s, d
     const lbk_geo& G = c->geo;
     hipLaunchKernelGGL(k_vf_edges, dim3(1), dim3(64), 0, c->stream, sl, x, g, s, y, G.n_loc, G.g_lo, G.g_hi);
     HIPCHK(c, hipGetLastError());
-    const int rc = exchange_slot(c, wslot);
+    const int rc = exchange_slot(c, wslot, 1, false);  // edges: read by k_vf_ghosts only
     if (rc) return rc;
     hipLaunchKernelGGL(k_vf_ghosts, dim3(1), dim3(64), 0, c->stream, sl, x, g, s, y, G.n_loc, G.g_lo, G.g_hi,
                        G.elem_lo > 0 ? 1 : 0, G.elem_lo + G.n_loc < G.n ? 1 : 0);
@@ -2176,6 +2188,10 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
     // sharded slots are completed by the exchange on the device: those fetch with a copy
     c->direct = world == 1 ? 1 : 0;
     if (const char* e = getenv("LBFGS_DIRECT")) c->direct = world == 1 && atoi(e) != 0;
+    // measured neutral in 4-rank rehearsals on one GPU (profiles/r01/xgmi_mirror_ab.txt), where
+    // the ranks share the card; the saved copy is ~1 % of an 8-GPU iteration at best: opt-in
+    c->xg_mirror = 0;
+    if (const char* e = getenv("LBFGS_XGMI_MIRROR")) c->xg_mirror = atoi(e) != 0;
     *out = c;
 #define CK(expr)                                                                             \
     do {                                                                                     \

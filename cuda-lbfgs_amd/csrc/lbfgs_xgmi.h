@@ -34,8 +34,10 @@ int lbk_xgmi_handle(const lbk_xgmi* x, void* out);
 int lbk_xgmi_connect(lbk_xgmi* x, const void* handles, hipStream_t stream, char* err, size_t cap);
 int lbk_xgmi_connected(const lbk_xgmi* x);
 // slot = [LBK_GROUPS][ks] doubles in device memory; this rank's groups [g_lo, g_hi) are final;
-// afterwards (in stream order) every group is
-int lbk_xgmi_exchange(lbk_xgmi* x, hipStream_t stream, double* slot, int ks, int g_lo, int g_hi);
+// afterwards (in stream order) every group is. host_mirror (a device-mapped host pointer to
+// the same layout, or NULL) receives all groups as well, so the host reads the slot with no copy
+int lbk_xgmi_exchange(lbk_xgmi* x, hipStream_t stream, double* slot, int ks, int g_lo, int g_hi,
+                      double* host_mirror);
 // raw 64-bit words of the same layout (integer sums such as the trace checksums)
 int lbk_xgmi_exchange_u64(lbk_xgmi* x, hipStream_t stream, uint64_t* slot, int ks, int g_lo, int g_hi);
 // nonzero once an exchange timed out waiting for a peer (the slot then holds NaN)

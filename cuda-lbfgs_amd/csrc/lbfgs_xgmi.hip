@@ -46,14 +46,18 @@ namespace {
 __global__ __launch_bounds__(256) void k_xgmi_exchange(unsigned long long* __restrict__ slot, int ks, int g_lo,
                                                         int g_hi, XPeers P, int rank, int world, int positions,
                                                         unsigned epoch, unsigned* err,
-                                                        unsigned long long timeout) {
+                                                        unsigned long long timeout,
+                                                        unsigned long long* __restrict__ hm) {
     const int lo = g_lo * ks, hi = g_hi * ks, own = hi - lo, npos = XG_GROUPS * ks;
     const size_t par = (size_t)(epoch & 1u) * (size_t)positions * 2;
     const unsigned long long tag = (unsigned long long)epoch << 32;
     for (int i = threadIdx.x; i < own * world; i += blockDim.x) {
         const int p = i / own, j = lo + i % own;
-        if (p == rank) continue;
         const unsigned long long v = slot[j];
+        if (p == rank) {
+            if (hm) hm[j] = v;
+            continue;
+        }
         unsigned long long* dst = P.mb[p] + par + 2 * (size_t)j;
         __hip_atomic_store(dst, tag | (v & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(dst + 1, tag | (v >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -75,7 +79,9 @@ __global__ __launch_bounds__(256) void k_xgmi_exchange(unsigned long long* __res
             }
             __builtin_amdgcn_s_sleep(1);
         }
-        slot[j] = (a & 0xffffffffull) | ((b & 0xffffffffull) << 32);
+        const unsigned long long v = (a & 0xffffffffull) | ((b & 0xffffffffull) << 32);
+        slot[j] = v;
+        if (hm) hm[j] = v;
     }
 }
 
@@ -84,12 +90,12 @@ unsigned long long ticks(const lbk_xgmi* x, double seconds) {
 }
 
 int launch(lbk_xgmi* x, hipStream_t s, unsigned long long* slot, int ks, int g_lo, int g_hi,
-           unsigned long long timeout) {
+           unsigned long long timeout, unsigned long long* hm = nullptr) {
     if (ks < 1 || XG_GROUPS * ks > x->positions || g_lo < 0 || g_hi > XG_GROUPS || g_lo >= g_hi) return -1;
     ++x->epoch;
     if (x->epoch == 0) ++x->epoch;  // 0 marks an empty mailbox word
     hipLaunchKernelGGL(k_xgmi_exchange, dim3(1), dim3(256), 0, s, slot, ks, g_lo, g_hi, x->peers, x->rank,
-                       x->world, x->positions, x->epoch, x->err_d, timeout);
+                       x->world, x->positions, x->epoch, x->err_d, timeout, hm);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
@@ -227,9 +233,11 @@ int lbk_xgmi_connect(lbk_xgmi* x, const void* handles, hipStream_t stream, char*
     return rc;
 }
 
-int lbk_xgmi_exchange(lbk_xgmi* x, hipStream_t stream, double* slot, int ks, int g_lo, int g_hi) {
+int lbk_xgmi_exchange(lbk_xgmi* x, hipStream_t stream, double* slot, int ks, int g_lo, int g_hi,
+                      double* host_mirror) {
     if (!x->connected) return -5;
-    return launch(x, stream, reinterpret_cast<unsigned long long*>(slot), ks, g_lo, g_hi, x->timeout_ticks);
+    return launch(x, stream, reinterpret_cast<unsigned long long*>(slot), ks, g_lo, g_hi, x->timeout_ticks,
+                  reinterpret_cast<unsigned long long*>(host_mirror));
 }
 
 int lbk_xgmi_exchange_u64(lbk_xgmi* x, hipStream_t stream, uint64_t* slot, int ks, int g_lo, int g_hi) {

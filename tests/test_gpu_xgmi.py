@@ -54,13 +54,14 @@ def run_ranks(tmp_path, world, n, m, obj, ls, iters, mode, env=None):
     (8, "rosenbrock", "backtracking", "default", "1"),
     (8, "quad_tridiag", "wolfe", "vf", "0"),
 ])
-def test_xgmi_sharded_bit_exact(tmp_path, world, obj, ls, mode, ticket):
+def test_xgmi_sharded_bit_exact(tmp_path, world, obj, ls, mode, ticket, mirror="0"):
     n = 4_000_003  # every one of up to 8 ranks owns segments
     m, iters = 5, 12
     x0 = L.x0_uniform(n, 42, -2.0, 2.0)
     with L.Context(n, m) as c:
         ref = c.minimize(obj, x0, ls, iters, trace=True, vector_free=(mode == "vf"))
-    outs = run_ranks(tmp_path, world, n, m, obj, ls, iters, mode, env={"LBFGS_TICKET": ticket})
+    outs = run_ranks(tmp_path, world, n, m, obj, ls, iters, mode,
+                     env={"LBFGS_TICKET": ticket, "LBFGS_XGMI_MIRROR": mirror})
     x = np.zeros(n)
     for r, o in enumerate(outs):
         for key in ("tr_f", "tr_gnorm", "tr_alpha"):
@@ -70,6 +71,13 @@ def test_xgmi_sharded_bit_exact(tmp_path, world, obj, ls, mode, ticket):
         x[lo:lo + len(o["x"])] = o["x"]
         assert str(o["messages"]) == ref["messages"]
     assert np.array_equal(bits(x), bits(ref["x"]))
+
+
+@pytest.mark.parametrize("mode,ls,ticket", [("default", "wolfe", "1"), ("vf", "interpolation", "0")])
+def test_xgmi_host_mirror_bit_exact(tmp_path, mode, ls, ticket):
+    """LBFGS_XGMI_MIRROR=1: the exchange kernel also fills the host mirror of the slots the host
+    reads (commit, trials, vector-free Gram rows), which the host then reads with no copy."""
+    test_xgmi_sharded_bit_exact(tmp_path, 4, "rosenbrock", ls, mode, ticket, mirror="1")
 
 
 def test_xgmi_silent_peer_times_out(tmp_path):
