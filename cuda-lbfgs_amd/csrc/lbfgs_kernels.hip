@@ -97,6 +97,23 @@ __device__ __forceinline__ void st2m(double* p, double2 v, bool v0, bool v1) {
     }
 }
 
+// Work vectors (q / r / d: rewritten pass after pass, read again by the next) may keep the
+// temporal policy under NT so that, at per-rank sizes a few times below the Infinity Cache, they
+// stay resident while the history streams past (A/B variant: LBK_WORK_TEMPORAL).
+#ifndef LBK_WORK_TEMPORAL
+#define LBK_WORK_TEMPORAL 1
+#endif
+template <bool NT>
+__device__ __forceinline__ double2 ldw(const double* p) {
+    return ldv<NT && !LBK_WORK_TEMPORAL>(p);
+}
+// level 2: the iterate and gradient (x, g; read by the trials, the last second-loop pass and
+// the commit) as well
+template <bool NT>
+__device__ __forceinline__ double2 ldx(const double* p) {
+    return ldv<NT && (LBK_WORK_TEMPORAL < 2)>(p);
+}
+
 // fixed-order total of the 8 group partials of one slot component
 __device__ __forceinline__ double slot_total(const double* p) {
     double t = p[0];
@@ -518,6 +535,21 @@ __device__ __forceinline__ void st2(double* p, double2 v, bool v0, bool v1) {
 }
 
 // acc = fma(a, b, acc) for the valid elements of a lane pair
+template <bool MASK, bool NT>
+__device__ __forceinline__ void st2w(double* p, double2 v, bool v0, bool v1) {
+    st2<MASK, NT && !LBK_WORK_TEMPORAL>(p, v, v0, v1);
+}
+
+template <bool MASK, bool NT>
+__device__ __forceinline__ void st2x(double* p, double2 v, bool v0, bool v1) {
+    st2<MASK, NT && (LBK_WORK_TEMPORAL < 2)>(p, v, v0, v1);
+}
+// level 3: the new history pair (s, y: the next two-loop's first reads)
+template <bool MASK, bool NT>
+__device__ __forceinline__ void st2h(double* p, double2 v, bool v0, bool v1) {
+    st2<MASK, NT && (LBK_WORK_TEMPORAL < 3)>(p, v, v0, v1);
+}
+
 template <bool MASK>
 __device__ __forceinline__ double fma2(double2 a, double2 b, double acc, bool v0, bool v1) {
     if (!MASK || v0) acc = fma(a.x, b.x, acc);
@@ -556,7 +588,7 @@ struct OpAxpyDot {  // q = qin - alpha y;  acc += s . q       (lbfgs.cpp:133-137
         double2 q, y, s;
     };
     __device__ void load(Row& r, int64_t i) const {
-        r.q = ldv<NT>(qin + i);
+        r.q = ldw<NT>(qin + i);
         r.y = ldv<NT>(y + i);
         r.s = ldv<NT>(s + i);
     }
@@ -565,7 +597,7 @@ struct OpAxpyDot {  // q = qin - alpha y;  acc += s . q       (lbfgs.cpp:133-137
         double2 qn;
         qn.x = r.q.x - alpha * r.y.x;
         qn.y = r.q.y - alpha * r.y.y;
-        st2<MASK, NT>(qout + i, qn, v0, v1);
+        st2w<MASK, NT>(qout + i, qn, v0, v1);
         acc[0] = fma2<MASK>(r.s, qn, acc[0], v0, v1);
     }
 };
@@ -595,7 +627,7 @@ struct OpMid {  // r = (qin - alpha0 y0) * gamma;  acc += y0 . r      (:134-137,
         double2 q, y;
     };
     __device__ void load(Row& r, int64_t i) const {
-        r.q = ldv<NT>(qin + i);
+        r.q = ldw<NT>(qin + i);
         r.y = ldv<NT>(y0 + i);
     }
     template <bool MASK>
@@ -603,7 +635,7 @@ struct OpMid {  // r = (qin - alpha0 y0) * gamma;  acc += y0 . r      (:134-137,
         double2 rr;
         rr.x = (r.q.x - alpha * r.y.x) * gamma;
         rr.y = (r.q.y - alpha * r.y.y) * gamma;
-        st2<MASK, NT>(rout + i, rr, v0, v1);
+        st2w<MASK, NT>(rout + i, rr, v0, v1);
         publish_edges(edge_slot, i, n_loc, g_lo, g_hi, rr, v0, v1);
         acc[0] = fma2<MASK>(r.y, rr, acc[0], v0, v1);
     }
@@ -623,7 +655,7 @@ struct OpAxpy2Dot {  // r += s (alpha - beta);  acc += ynext . r      (:159-164)
         double2 r, s, y;
     };
     __device__ void load(Row& w, int64_t i) const {
-        w.r = ldv<NT>(rin + i);
+        w.r = ldw<NT>(rin + i);
         w.s = ldv<NT>(s + i);
         w.y = ldv<NT>(yn + i);
     }
@@ -632,7 +664,7 @@ struct OpAxpy2Dot {  // r += s (alpha - beta);  acc += ynext . r      (:159-164)
         double2 rn;
         rn.x = w.r.x + w.s.x * coef;
         rn.y = w.r.y + w.s.y * coef;
-        st2<MASK, NT>(r + i, rn, v0, v1);
+        st2w<MASK, NT>(r + i, rn, v0, v1);
         publish_edges(edge_slot, i, n_loc, g_lo, g_hi, rn, v0, v1);
         acc[0] = fma2<MASK>(w.y, rn, acc[0], v0, v1);
     }
@@ -652,16 +684,16 @@ struct OpLast {  // d = -(r + s (alpha - beta));  acc += g . d        (:163-171)
         double2 r, s, g;
     };
     __device__ void load(Row& w, int64_t i) const {
-        w.r = ldv<NT>(r + i);
+        w.r = ldw<NT>(r + i);
         w.s = ldv<NT>(s + i);
-        w.g = ldv<NT>(g + i);
+        w.g = ldx<NT>(g + i);
     }
     template <bool MASK>
     __device__ void apply(Row& w, int64_t i, int64_t, bool v0, bool v1, double (&acc)[1]) const {
         double2 d;
         d.x = -(w.r.x + w.s.x * coef);
         d.y = -(w.r.y + w.s.y * coef);
-        st2<MASK, NT>(dout + i, d, v0, v1);
+        st2w<MASK, NT>(dout + i, d, v0, v1);
         publish_edges(edge_slot, i, n_loc, g_lo, g_hi, d, v0, v1);
         acc[0] = fma2<MASK>(w.g, d, acc[0], v0, v1);
     }
@@ -683,7 +715,7 @@ struct OpNegDot {  // d = -g;  acc += g . d                          (:90, :151-
         double2 d;
         d.x = -w.g.x;
         d.y = -w.g.y;
-        st2<MASK, NT>(dout + i, d, v0, v1);
+        st2w<MASK, NT>(dout + i, d, v0, v1);
         publish_edges(edge_slot, i, n_loc, g_lo, g_hi, d, v0, v1);
         acc[0] = fma2<MASK>(w.g, d, acc[0], v0, v1);
     }
@@ -773,12 +805,12 @@ template <int DMODE, bool NT>
 __device__ __forceinline__ double2 load_dir(const DirArgs& da, int64_t i, double2 gv) {
     double2 d;
     if (DMODE == LBK_D_BUF) {
-        d = ldv<NT>(da.dsrc + i);
+        d = ldw<NT>(da.dsrc + i);
     } else if (DMODE == LBK_D_NEG_G) {
         d.x = -gv.x;
         d.y = -gv.y;
     } else {
-        const double2 rv = ldv<NT>(da.dsrc + i);
+        const double2 rv = ldw<NT>(da.dsrc + i);
         const double2 sv = ldv<NT>(da.s + i);
         d.x = -(rv.x + sv.x * da.coef);
         d.y = -(rv.y + sv.y * da.coef);
@@ -871,11 +903,11 @@ struct OpObjective {
         double zh;
     };
     __device__ void load(Row& r, int64_t i) const {
-        const double2 xv = ldv<NT>(x + i);
+        const double2 xv = ldx<NT>(x + i);
         if (NO_DIR) {
             r.z = xv;
         } else {
-            r.d = ldv<NT>(da.dsrc + i);
+            r.d = ldw<NT>(da.dsrc + i);
             r.z.x = xv.x + alpha * r.d.x;
             r.z.y = xv.y + alpha * r.d.y;
         }
@@ -885,7 +917,7 @@ struct OpObjective {
     __device__ void apply(Row& r, int64_t i, int64_t e0, bool v0, bool v1, double (&acc)[2]) const {
         const double2 g = objective_pair<OBJ, MASK>(r.z, r.zh, e0, n, v0, v1, acc[0], WITH_G);
         if (WITH_G) {
-            if (gout) st2<MASK, NT>(gout + i, g, v0, v1);
+            if (gout) st2x<MASK, NT>(gout + i, g, v0, v1);
             acc[1] = NO_DIR ? fma2<MASK>(g, g, acc[1], v0, v1) : fma2<MASK>(g, r.d, acc[1], v0, v1);
         }
     }
@@ -916,8 +948,8 @@ struct OpCommit {
         double zh;
     };
     __device__ void load(Row& r, int64_t i) const {
-        r.x = ldv<NT>(x + i);
-        r.g = ldv<NT>(da.g + i);
+        r.x = ldx<NT>(x + i);
+        r.g = ldx<NT>(da.g + i);
         r.d = load_dir<DMODE, NT>(da, i, r.g);
         if (OBJ == LBK_OBJ_NONE) r.gx = ldv<NT>(gn + i);
         r.z.x = r.x.x + alpha * r.d.x;
@@ -931,16 +963,16 @@ struct OpCommit {
             g2 = r.gx;
         } else {
             g2 = objective_pair<OBJ, MASK>(r.z, r.zh, e0, n, v0, v1, acc[LBK_C_F], true);
-            st2<MASK, NT>(gn + i, g2, v0, v1);
+            st2x<MASK, NT>(gn + i, g2, v0, v1);
         }
-        st2<MASK, NT>(xn + i, r.z, v0, v1);
+        st2x<MASK, NT>(xn + i, r.z, v0, v1);
         double2 sv, yv;
         sv.x = r.z.x - r.x.x;
         sv.y = r.z.y - r.x.y;
         yv.x = g2.x - r.g.x;
         yv.y = g2.y - r.g.y;
-        st2<MASK, NT>(so + i, sv, v0, v1);
-        st2<MASK, NT>(yo + i, yv, v0, v1);
+        st2h<MASK, NT>(so + i, sv, v0, v1);
+        st2h<MASK, NT>(yo + i, yv, v0, v1);
         acc[LBK_C_GD] = fma2<MASK>(r.g, r.d, acc[LBK_C_GD], v0, v1);
         acc[LBK_C_SY] = fma2<MASK>(sv, yv, acc[LBK_C_SY], v0, v1);
         acc[LBK_C_YY] = fma2<MASK>(yv, yv, acc[LBK_C_YY], v0, v1);
@@ -1032,8 +1064,8 @@ struct OpVfCommit {
     };
     // x, g, the basis and z = x + alpha d (and x + ac[j] d) of local elements i, i+1
     __device__ void load(Row& r, int64_t i) const {
-        r.x = ldv<NT>(x + i);
-        r.g = ldv<NT>(g + i);
+        r.x = ldx<NT>(x + i);
+        r.g = ldx<NT>(g + i);
 #pragma unroll
         for (int l = 0; l < 2 * HB; ++l)
             if (l < 2 * B.h) r.b[l] = ldv<NT>(B.b[l] + i);
@@ -1110,15 +1142,15 @@ struct OpVfCommit {
     template <bool MASK>
     __device__ void apply(Row& r, int64_t i, int64_t e0, bool v0, bool v1, double (&acc)[K]) const {
         const double2 g2 = objective_pair<OBJ, MASK>(r.z, r.zh, e0, n, v0, v1, acc[LBK_VF_F], true);
-        st2<MASK, NT>(gn + i, g2, v0, v1);
-        st2<MASK, NT>(xn + i, r.z, v0, v1);
+        st2x<MASK, NT>(gn + i, g2, v0, v1);
+        st2x<MASK, NT>(xn + i, r.z, v0, v1);
         double2 sv, yv;
         sv.x = r.z.x - r.x.x;
         sv.y = r.z.y - r.x.y;
         yv.x = g2.x - r.g.x;
         yv.y = g2.y - r.g.y;
-        st2<MASK, NT>(so + i, sv, v0, v1);
-        st2<MASK, NT>(yo + i, yv, v0, v1);
+        st2h<MASK, NT>(so + i, sv, v0, v1);
+        st2h<MASK, NT>(yo + i, yv, v0, v1);
         acc[LBK_VF_SY] = fma2<MASK>(sv, yv, acc[LBK_VF_SY], v0, v1);
         acc[LBK_VF_YY] = fma2<MASK>(yv, yv, acc[LBK_VF_YY], v0, v1);
         acc[LBK_VF_GG] = fma2<MASK>(g2, g2, acc[LBK_VF_GG], v0, v1);
@@ -1769,6 +1801,7 @@ struct lbk_ctx {
     int ticket;      // reduction mode (see reduce_publish)
     lbk_group* grp;  // emulated ranks: host exchange group (tests; NULL with RCCL)
     lbk_xgmi* xg;    // sharded, one process per GPU: peer mailboxes over xGMI (lbfgs_xgmi.hip)
+    int nt_vf;       // the vector-free passes' NT policy (c->nt while they launch)
     int xg_on;       // 1: exchanges go through xg instead of RCCL
     int xg_mirror;   // 1: xg exchanges of host-read slots also fill the host mirror
     uint64_t* d_ckslot;  // [LBK_GROUPS][2] checksum words for the peer exchange
@@ -2152,10 +2185,14 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
     }
     // front pad 32 doubles: ghost at [-1] and element 0 on a 256-B boundary, so every 1-KiB
     // row load/store covers whole cache lines; back: whole rows + halo
-    // non-temporal streaming once a vector no longer fits comfortably in the 256 MiB Infinity
-    // Cache: +4 % at n=1e8, -1 % at n=1e7 (profiles/r01); override: LBFGS_NT=0/1
-    c->nt = (G.n_loc * 8 > (128ll << 20)) ? 1 : 0;
-    if (const char* e = getenv("LBFGS_NT")) c->nt = atoi(e) != 0;
+    // non-temporal streaming of the history (the work vectors q/r/d keep the temporal policy,
+    // LBK_WORK_TEMPORAL) once vectors no longer fit comfortably in the 256 MiB Infinity Cache.
+    // Two-loop passes: -2 % at n_loc = 1e7, +1.3 % at 1.25e7, +4 % at 1e8; vector-free passes
+    // (2m+6 vectors each): +1.5 % at 2e6, +5 % at 1e7 and above (profiles/r01/nt_threshold_ab.txt,
+    // work_temporal_ab.txt). Override for both: LBFGS_NT=0/1
+    c->nt = (G.n_loc * 8 > (88ll << 20)) ? 1 : 0;
+    c->nt_vf = (G.n_loc * 8 > (12ll << 20)) ? 1 : 0;
+    if (const char* e = getenv("LBFGS_NT")) c->nt = c->nt_vf = atoi(e) != 0;
     // stage-2 reduction: separate 8-workgroup kernel by default; in-launch tickets only for
     // tiny grids where the extra launch dominates (override: LBFGS_TICKET=0/1)
     // sharded runs with long segments too: one rank of an 8-GPU n = 1e8 run (1017 workgroups of
@@ -2539,10 +2576,19 @@ VfBasis<HB> vf_basis(int h, const double* const* S, const double* const* Y, cons
     return B;
 }
 
+// the vector-free passes run under their own NT threshold (c->nt_vf)
+struct NtScope {
+    lbk_ctx* c;
+    int saved;
+    NtScope(lbk_ctx* c_, int nt) : c(c_), saved(c_->nt) { c->nt = nt; }
+    ~NtScope() { c->nt = saved; }
+};
+
 template <int HB>
 int vf_commit_hb(lbk_ctx* c, int obj, int h, const double* x, const double* g, const double* const* S,
                  const double* const* Y, const double* cs, const double* cy, double cg, double alpha,
                  const double* cand, double* xn, double* gn, double* so, double* yo, int wslot) {
+    const NtScope nts(c, c->nt_vf);
     Geo geo = vgeo(c);
     Red r = kred(c, wslot);
     const VfBasis<HB> B = vf_basis<HB>(h, S, Y, cs, cy, cg);
@@ -2562,6 +2608,7 @@ int vf_commit_hb(lbk_ctx* c, int obj, int h, const double* x, const double* g, c
 template <int HB>
 int vf_dir_hb(lbk_ctx* c, int h, double* d, const double* g, const double* const* S, const double* const* Y,
               const double* cs, const double* cy, double cg) {
+    const NtScope nts(c, c->nt_vf);
     const VfBasis<HB> B = vf_basis<HB>(h, S, Y, cs, cy, cg);
     const int64_t npair = c->geo.n_loc / 2;
     const int nb = (int)std::max<int64_t>(1, std::min<int64_t>((npair + 255) / 256, 16384));
