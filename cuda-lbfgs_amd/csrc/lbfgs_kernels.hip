@@ -103,15 +103,20 @@ __device__ __forceinline__ void st2m(double* p, double2 v, bool v0, bool v1) {
 #ifndef LBK_WORK_TEMPORAL
 #define LBK_WORK_TEMPORAL 1
 #endif
+// A/B levels: 0 all NT; 1 q/r/d temporal; 2 + x, g; 3 + new s, y; 4 / 5 q/r/d loads / stores only
+#define LBK_WLD_T (LBK_WORK_TEMPORAL >= 1 && LBK_WORK_TEMPORAL <= 4)
+#define LBK_WST_T (LBK_WORK_TEMPORAL >= 1 && LBK_WORK_TEMPORAL != 4)
+#define LBK_XG_T (LBK_WORK_TEMPORAL == 2 || LBK_WORK_TEMPORAL == 3)
+#define LBK_SY_T (LBK_WORK_TEMPORAL == 3)
 template <bool NT>
 __device__ __forceinline__ double2 ldw(const double* p) {
-    return ldv<NT && !LBK_WORK_TEMPORAL>(p);
+    return ldv<NT && !LBK_WLD_T>(p);
 }
 // level 2: the iterate and gradient (x, g; read by the trials, the last second-loop pass and
 // the commit) as well
 template <bool NT>
 __device__ __forceinline__ double2 ldx(const double* p) {
-    return ldv<NT && (LBK_WORK_TEMPORAL < 2)>(p);
+    return ldv<NT && !LBK_XG_T>(p);
 }
 
 // fixed-order total of the 8 group partials of one slot component
@@ -537,17 +542,17 @@ __device__ __forceinline__ void st2(double* p, double2 v, bool v0, bool v1) {
 // acc = fma(a, b, acc) for the valid elements of a lane pair
 template <bool MASK, bool NT>
 __device__ __forceinline__ void st2w(double* p, double2 v, bool v0, bool v1) {
-    st2<MASK, NT && !LBK_WORK_TEMPORAL>(p, v, v0, v1);
+    st2<MASK, NT && !LBK_WST_T>(p, v, v0, v1);
 }
 
 template <bool MASK, bool NT>
 __device__ __forceinline__ void st2x(double* p, double2 v, bool v0, bool v1) {
-    st2<MASK, NT && (LBK_WORK_TEMPORAL < 2)>(p, v, v0, v1);
+    st2<MASK, NT && !LBK_XG_T>(p, v, v0, v1);
 }
 // level 3: the new history pair (s, y: the next two-loop's first reads)
 template <bool MASK, bool NT>
 __device__ __forceinline__ void st2h(double* p, double2 v, bool v0, bool v1) {
-    st2<MASK, NT && (LBK_WORK_TEMPORAL < 3)>(p, v, v0, v1);
+    st2<MASK, NT && !LBK_SY_T>(p, v, v0, v1);
 }
 
 template <bool MASK>
