@@ -356,6 +356,7 @@ def test_deferred_stage2_bit_exact(monkeypatch, n, m, ls, obj):
     reduce-kernel sequence and the oracle: identical bits."""
     x0 = L.x0_uniform(n, 5, -2.0, 2.0)
     out = []
+    monkeypatch.setenv("LBFGS_TICKET", "0")  # deferral replaces the reduce kernel, not tickets
     for defer in ("0", "8192"):
         monkeypatch.setenv("LBFGS_DEFER", defer)
         with L.Context(n, m) as c:
