@@ -57,9 +57,10 @@ def parse():
                    help="skip the vector-free measurement reported beside the default mode")
     p.add_argument("--no-config4", action="store_true",
                    help="8 ranks: skip the n=1e9 measurement (BASELINE configs[4]) after the headline")
-    p.add_argument("--exchange", choices=["xgmi", "rccl"], default="xgmi",
+    p.add_argument("--exchange", choices=["auto", "xgmi", "rccl"], default="auto",
                    help="sharded runs: reductions through the xGMI peer mailboxes (falls back to RCCL "
-                        "when any rank's self-test fails) or RCCL all-gathers")
+                        "when any rank's self-test fails) or RCCL all-gathers; auto: the mailboxes "
+                        "unless RCCL measures >10%% faster per exchange on this node")
     return p.parse_args()
 
 
@@ -176,12 +177,21 @@ def measure(a, D, n, x0, dev, rank, world, uid, unfused=False, vector_free=False
     """W warm-up steps, then EXACTLY K timed steps (barrier + device sync on both sides, no
     instrumentation), then a separate event-instrumented pass for per-kernel durations."""
     ctx = L.Context(n, a.history, device=dev, rank=rank, world=world, uid=uid)
-    if world > 1 and a.exchange == "xgmi":
+    if world > 1 and a.exchange in ("xgmi", "auto"):
         ok, msg = ctx.connect_peers(D.allgather_bytes, D.all_ok)
         if msg:
             print(f"rank {rank}: {msg}", file=sys.stderr, flush=True)
         if not ok and uid is None:
             raise L.LbfgsError("xGMI peer exchange unavailable and no RCCL communicator")
+        if ok and a.exchange == "auto" and uid is not None:
+            # collective calls in the same order on every rank; the slowest rank decides
+            tx = D.allreduce(ctx.exchange_latency("xgmi", 8, 100), "max")
+            tr = D.allreduce(ctx.exchange_latency("rccl", 8, 100), "max")
+            if tr < 0.9 * tx:
+                ctx.peer_enable(False)
+            if rank == 0:
+                print(f"exchange auto: xgmi {tx:.2f} us, rccl {tr:.2f} us -> {ctx.backend}", file=sys.stderr,
+                      flush=True)
     backend = ctx.backend
     ctx.init(a.objective, x0, a.line_search, tolerance=1e-5, unfused=unfused, vector_free=vector_free)
     ctx.step(a.warmup)

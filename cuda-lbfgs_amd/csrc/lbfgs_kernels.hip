@@ -2899,6 +2899,7 @@ int lbk_peer_connect(lbk_ctx* c, const void* handles) {
 
 int lbk_peer_enable(lbk_ctx* c, int on) {
     if (on && !lbk_xgmi_connected(c->xg)) return -5;
+    if (!on && !c->comm && !c->grp) return -5;  // nothing else to exchange through
     c->xg_on = on ? 1 : 0;
     return 0;
 }

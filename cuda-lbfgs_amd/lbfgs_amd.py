@@ -274,6 +274,13 @@ class Context:
                 self._err("lbfgs_peer_enable", rc2)
         return ok, msg
 
+    def peer_enable(self, on=True):
+        """Route this context's exchanges through the peer mailboxes (after connect_peers) or
+        back to its RCCL communicator. Every rank must make the same choice."""
+        rc = lib().lbfgs_peer_enable(self.h, 1 if on else 0)
+        if rc != 0:
+            self._err("lbfgs_peer_enable", rc)
+
     def exchange_latency(self, backend, components=8, iters=200):
         """Collective: microseconds per exchange through 'rccl' or 'xgmi' (every rank calls)."""
         us = C.c_double()

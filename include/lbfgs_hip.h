@@ -149,6 +149,9 @@ int lbfgs_device_count(void);
 #define LBFGS_PEER_HANDLE_BYTES 64
 int lbfgs_peer_handle(lbfgs_ctx* ctx, void* out /* LBFGS_PEER_HANDLE_BYTES */);
 int lbfgs_peer_connect(lbfgs_ctx* ctx, const void* handles /* world x LBFGS_PEER_HANDLE_BYTES */);
+/* on = 1: exchanges through the mailboxes (after a successful connect on every rank); on = 0: back
+ * to the RCCL communicator (LBFGS_ERR_STATE without one). Every rank must make the same choice;
+ * bench.py --exchange auto keeps the mailboxes unless RCCL measures >10 % faster. */
 int lbfgs_peer_enable(lbfgs_ctx* ctx, int on);
 /* 0: one rank, 1: RCCL all-gathers, 2: xGMI peer mailboxes, 3: host group (emulated ranks) */
 int lbfgs_exchange_backend(const lbfgs_ctx* ctx);
