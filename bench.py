@@ -185,9 +185,15 @@ def measure(a, D, n, x0, dev, rank, world, uid, unfused=False, vector_free=False
             raise L.LbfgsError("xGMI peer exchange unavailable and no RCCL communicator")
         if ok and a.exchange == "auto" and uid is not None:
             # collective calls in the same order on every rank; the slowest rank decides
-            tx = D.allreduce(ctx.exchange_latency("xgmi", 8, 100), "max")
-            tr = D.allreduce(ctx.exchange_latency("rccl", 8, 100), "max")
-            if tr < 0.9 * tx:
+            try:
+                lx, lr = ctx.exchange_latency("xgmi", 8, 100), ctx.exchange_latency("rccl", 8, 100)
+            except L.LbfgsError as e:
+                print(f"rank {rank}: exchange timing failed: {e}", file=sys.stderr, flush=True)
+                lx = lr = None
+            timed = D.all_ok(lx is not None)
+            tx = D.allreduce(lx if timed else 0.0, "max")
+            tr = D.allreduce(lr if timed else 0.0, "max")
+            if timed and tr < 0.9 * tx:
                 ctx.peer_enable(False)
             if rank == 0:
                 print(f"exchange auto: xgmi {tx:.2f} us, rccl {tr:.2f} us -> {ctx.backend}", file=sys.stderr,
