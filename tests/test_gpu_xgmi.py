@@ -80,6 +80,25 @@ def test_xgmi_host_mirror_bit_exact(tmp_path, mode, ls, ticket):
     test_xgmi_sharded_bit_exact(tmp_path, 4, "rosenbrock", ls, mode, ticket, mirror="1")
 
 
+def test_xgmi_soak_8_ranks_bit_exact(tmp_path):
+    """A long sharded solve (8 ranks, 1500 iterations, ~2e4 mailbox exchanges per rank through
+    both parities) stays bit-identical to one GPU: a protocol race (epoch reuse, a stale
+    mailbox word) would show as a wrong value or a timeout."""
+    n, m, iters = 4_000_003, 5, 1500
+    x0 = L.x0_uniform(n, 42, -2.0, 2.0)  # the worker's seed
+    with L.Context(n, m) as c:
+        ref = c.minimize("rosenbrock", x0, "backtracking", iters, trace=True)
+    outs = run_ranks(tmp_path, 8, n, m, "rosenbrock", "backtracking", iters, "default",
+                     env={"LBFGS_TICKET": "1"})
+    x = np.zeros(n)
+    for r, o in enumerate(outs):
+        for key in ("tr_f", "tr_gnorm", "tr_alpha"):
+            assert np.array_equal(bits(o[key]), bits(ref[key])), (r, key)
+        lo = int(o["lo"])
+        x[lo:lo + len(o["x"])] = o["x"]
+    assert np.array_equal(bits(x), bits(ref["x"]))
+
+
 def test_xgmi_silent_peer_times_out(tmp_path):
     """A peer that publishes its handle but never exchanges must not hang the others: rank 0's
     self-test gives up after its timeout (LBFGS_XGMI_SELFTEST_TIMEOUT) and no rank enables the
