@@ -2132,6 +2132,8 @@ int lbk_unique_id(void* out128) {
     return 0;
 }
 
+// The factor is chosen from the 512-minimum segment length L0 (not the canonical L, which is
+// longer for LBK_MIDL_LO <= n <= LBK_MIDL_HI); the vector-free segment length is F x canonical L.
 int lbk_vf_factor(int64_t n) {
     const int64_t per = (n + LBK_SEGS - 1) / LBK_SEGS;
     int64_t L = ((per + 127) / 128) * 128;
@@ -2154,7 +2156,14 @@ int lbk_geometry_plan(int64_t n, int rank, int world, lbk_geo* out) {
     // than 512-multiples keep all 8 groups populated for n >= 7.3e6 (sharding over 8 ranks)
     const int64_t per = (n + LBK_SEGS - 1) / LBK_SEGS;
     G.L = ((per + 127) / 128) * 128;
-    if (G.L < 512) G.L = 512;
+    // minimum segment length: 2048 elements where n cannot shard anyway (n <= 4 * 1024 * 512:
+    // two ranks would need more than 4096 segments of 512), from 2^18 up; 512 elsewhere. Fewer,
+    // longer segments bring mid n under the cooperative (<= 256 segments) and deferred
+    // (<= 1024) stage-2 forms: measured +6..21 % at n = 3e5..2e6, vector-free +16..60 %
+    // (profiles/r01/lmin_ab.txt). Below 2^18 the default mode would gain too (+29 % at 1e5) but
+    // the vector-free mode would lose (-25 %). The oracle's orc_canon_geometry states the rule.
+    const int64_t lmin = (n >= LBK_MIDL_LO && n <= LBK_MIDL_HI) ? LBK_MIDL : 512;
+    if (G.L < lmin) G.L = lmin;
 #ifdef LBK_DEBUG_SEGLEN  // timing experiments only (tools/gpu_ab_shardgeo.sh): breaks the canonical order
     G.L = LBK_DEBUG_SEGLEN;
 #endif

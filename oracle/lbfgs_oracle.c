@@ -78,7 +78,9 @@ void orc_checksum(const double* x, int64_t n, uint64_t* c1, uint64_t* c2) {
  * Reductions.
  * ORC_SEQ  : vector_utils.cpp:32-41 (dotProduct), :78-86 (vectorNorm) — left to right.
  * ORC_CANON: the device order:
- *   seg_len L = max(512, roundup(ceil(n/8192), 128)); segment s = [sL, min((s+1)L, n));
+ *   seg_len L = max(Lmin, roundup(ceil(n/8192), 128)), Lmin = 2048 for 262144 <= n <= 2097152
+ *   (lbfgs_kernels.hip lbk_geometry_plan: n that cannot shard), 512 otherwise;
+ *   segment s = [sL, min((s+1)L, n));
  *   thread t = 64w + lane (256 per segment); thread t visits, for u = 0.., row r = 4u + w,
  *   elements sL + 128r + 2 lane + v (v = 0,1) that are < segment end and < limit;
  *   dot: acc = fma(a, b, acc); sum: acc = acc + t.
@@ -94,17 +96,21 @@ void orc_checksum(const double* x, int64_t n, uint64_t* c1, uint64_t* c2) {
 void orc_canon_geometry(int64_t n, int64_t* seg_len, int64_t* nseg) {
     int64_t per = (n + CANON_SEGS - 1) / CANON_SEGS;
     int64_t L = ((per + 127) / 128) * 128;
-    if (L < 512) L = 512;
+    const int64_t lmin = (n >= 262144 && n <= 2097152) ? 2048 : 512;
+    if (L < lmin) L = lmin;
     *seg_len = L;
     *nseg = (n + L - 1) / L;
 }
 
 /* The vector-free commit's segments (lbfgs_kernels.hip vgeo / lbk_vf_factor): F canonical
- * segments each, F the largest of {1, 2, 4, 8} with F L <= 8192 and ceil(n / (F L)) >= 1024;
- * 1024 / F of them per group, placed first in the group's 1024-entry tree (0.0 behind). */
+ * segments each, F the largest of {1, 2, 4, 8} with 2 F L0 <= 8192 and
+ * ceil(n / (2 F L0)) >= 1024 while doubling, L0 = max(512, roundup(ceil(n/8192), 128)) (the
+ * canonical length without the mid-n minimum); 1024 / F of them per group, placed first in the
+ * group's 1024-entry tree (0.0 behind). */
 int orc_vf_factor(int64_t n) {
-    int64_t L, nseg;
-    orc_canon_geometry(n, &L, &nseg);
+    int64_t per = (n + CANON_SEGS - 1) / CANON_SEGS;
+    int64_t L = ((per + 127) / 128) * 128;
+    if (L < 512) L = 512;
     int F = 1;
     while (F < 8 && 2 * F * L <= 8192 && (n + 2 * F * L - 1) / (2 * F * L) >= 1024) F *= 2;
     return F;

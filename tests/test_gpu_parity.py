@@ -347,7 +347,7 @@ def test_cooperative_iteration_bit_exact(monkeypatch, n, m, ls):
     assert np.array_equal(bits(b["tr_f"]), bits(o["f"]))
 
 
-@pytest.mark.parametrize("n,m,ls,obj", [(300_000, 10, "backtracking", "rosenbrock"),
+@pytest.mark.parametrize("n,m,ls,obj", [(700_001, 10, "backtracking", "rosenbrock"),
                                         (1_000_001, 5, "wolfe", "rosenbrock"),
                                         (2_000_000, 7, "interpolation", "quad_tridiag")])
 def test_deferred_stage2_bit_exact(monkeypatch, n, m, ls, obj):
