@@ -2225,7 +2225,11 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
     // +22 % at 1e5 (196 segments); -22 % at 391 segments and -38 % at 508, where the barrier's
     // fan-in and every workgroup's read of all partials outweigh the saved launches. Bit-identical
     // (tests/test_gpu_parity.py::test_cooperative_iteration_bit_exact). LBFGS_COOP=<segments>.
-    c->coop_max = 256;
+    // with the mid-n 2048-element segments (4x the work per workgroup) the crossover to the
+    // deferred stage 2 comes earlier: at 245 segments (n = 5e5) deferred runs 6.8-7.0k it/s
+    // against 5.4-5.6k cooperative, at 196 they tie, at 147 cooperative leads 7.9-8.1k to
+    // 7.0-7.8k (profiles/r01/coop_long_ab.txt)
+    c->coop_max = G.L > 512 ? 192 : 256;
     if (const char* e = getenv("LBFGS_COOP")) c->coop_max = std::min(atoi(e), LBK_COOP_SEGMAX);  // max segments
     c->pend_slot = -1;
     // measured (profiles/r01/defer_ab.txt): +21..32 % at n = 3e5 (586 segments); -14 % at 1954
