@@ -22,9 +22,11 @@ extern "C" {
 #define LBK_NSLOTS 256
 #define LBK_SEGS 8192
 #define LBK_SEG_PER_GROUP 1024
-/* canonical minimum segment length LBK_MIDL for LBK_MIDL_LO <= n <= LBK_MIDL_HI, else 512 */
+/* canonical minimum segment length LBK_MIDL for LBK_MIDL_LO <= n <= LBK_MIDL_HI, else 512; the
+ * vector-free commit's base length is LBK_MIDL only from LBK_VFL_LO (shorter segments below) */
 #define LBK_MIDL 2048
-#define LBK_MIDL_LO 262144
+#define LBK_MIDL_LO 65536
+#define LBK_VFL_LO 262144
 #define LBK_MIDL_HI 2097152 /* 4 * 1024 * 512: sharding needs more elements at L = 512 */
 
 /* wide result slots (vector-free mode: 4h + 6 components): ids LBK_WSLOT0 + w */

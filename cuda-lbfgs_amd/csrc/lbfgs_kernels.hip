@@ -1807,6 +1807,7 @@ struct lbk_ctx {
     lbk_group* grp;  // emulated ranks: host exchange group (tests; NULL with RCCL)
     lbk_xgmi* xg;    // sharded, one process per GPU: peer mailboxes over xGMI (lbfgs_xgmi.hip)
     int nt_vf;       // the vector-free passes' NT policy (c->nt while they launch)
+    int ticket_env;  // LBFGS_TICKET override (-1: none)
     int xg_on;       // 1: exchanges go through xg instead of RCCL
     int xg_mirror;   // 1: xg exchanges of host-read slots also fill the host mirror
     uint64_t* d_ckslot;  // [LBK_GROUPS][2] checksum words for the peer exchange
@@ -1866,11 +1867,22 @@ Geo kgeo(const lbk_ctx* c) {
 // elements in both geometries. Short canonical segments (n <= ~1e7) leave each wave of the
 // vector-free commit only 1-3 rows, and its fixed costs per segment (the two wave-run edges,
 // a 4h+7-component reduction) dominate; F up to 8 restores runs of ~10 rows.
+// The base length is the canonical L except for LBK_MIDL_LO <= n < LBK_VFL_LO, where the
+// canonical segments are 2048 long but the vector-free commit keeps the 512-minimum length
+// (measured there: 2048-element segments cost the vector-free mode 25 %, profiles/r01/lmin_ab.txt).
+int64_t vf_base_len(int64_t n, int64_t canon_L) {
+    if (n < LBK_MIDL_LO || n >= LBK_VFL_LO) return canon_L;
+    const int64_t per = (n + LBK_SEGS - 1) / LBK_SEGS;
+    int64_t L = ((per + 127) / 128) * 128;
+    return L < 512 ? 512 : L;
+}
+
 Geo vgeo(const lbk_ctx* c) {
     Geo g = kgeo(c);
     const int F = c->geo.vf_f;
-    if (F <= 1) return g;
-    g.L = c->geo.L * F;
+    const int64_t base = vf_base_len(c->geo.n, c->geo.L);
+    if (F <= 1 && base == c->geo.L) return g;
+    g.L = base * F;
     g.nseg = (c->geo.n + g.L - 1) / g.L;
     g.spg = LBK_SEG_PER_GROUP / F;
     g.seg_lo = std::min<int64_t>((int64_t)c->geo.g_lo * g.spg, g.nseg);
@@ -2157,11 +2169,11 @@ int lbk_geometry_plan(int64_t n, int rank, int world, lbk_geo* out) {
     const int64_t per = (n + LBK_SEGS - 1) / LBK_SEGS;
     G.L = ((per + 127) / 128) * 128;
     // minimum segment length: 2048 elements where n cannot shard anyway (n <= 4 * 1024 * 512:
-    // two ranks would need more than 4096 segments of 512), from 2^18 up; 512 elsewhere. Fewer,
+    // two ranks would need more than 4096 segments of 512), from 2^16 up; 512 elsewhere. Fewer,
     // longer segments bring mid n under the cooperative (<= 256 segments) and deferred
-    // (<= 1024) stage-2 forms: measured +6..21 % at n = 3e5..2e6, vector-free +16..60 %
-    // (profiles/r01/lmin_ab.txt). Below 2^18 the default mode would gain too (+29 % at 1e5) but
-    // the vector-free mode would lose (-25 %). The oracle's orc_canon_geometry states the rule.
+    // (<= 1024) stage-2 forms: measured +6..29 % at n = 1e5..2e6, vector-free +16..60 % from
+    // 2^18 (profiles/r01/lmin_ab.txt; below 2^18 its commit keeps 512, see vf_base_len). The
+    // oracle's orc_canon_geometry states the rule.
     const int64_t lmin = (n >= LBK_MIDL_LO && n <= LBK_MIDL_HI) ? LBK_MIDL : 512;
     if (G.L < lmin) G.L = lmin;
 #ifdef LBK_DEBUG_SEGLEN  // timing experiments only (tools/gpu_ab_shardgeo.sh): breaks the canonical order
@@ -2213,7 +2225,8 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
     // L = 12288 per pass) measured 1 % faster with tickets on one GPU (tools/gpu_ab_shardgeo.sh),
     // and the stage-2 launch before each all-gather disappears
     c->ticket = ((G.seg_hi - G.seg_lo) <= 64 || (world > 1 && G.L >= 8192)) ? 1 : 0;
-    if (const char* e = getenv("LBFGS_TICKET")) c->ticket = atoi(e) != 0;
+    c->ticket_env = -1;
+    if (const char* e = getenv("LBFGS_TICKET")) c->ticket = c->ticket_env = atoi(e) != 0;
     c->vec_doubles = LBK_FRONT + ((G.n_loc + 511) / 512) * 512 + 512;
     // small n: the whole two-loop + commit in one single-workgroup launch (LBFGS_SMALL_SEGS=N
     // enables it for nseg <= N). Measured 1.8x slower at n=1e4 and 5x at 3e4 than the launch
@@ -2602,12 +2615,24 @@ struct NtScope {
     ~NtScope() { c->nt = saved; }
 };
 
+// ... and its stage-2 form by its own segment count (the canonical rule applied to the
+// vector-free geometry: tickets for <= 64 workgroups or sharded segments >= 8192)
+struct TicketScope {
+    lbk_ctx* c;
+    int saved;
+    TicketScope(lbk_ctx* c_, const Geo& g) : c(c_), saved(c_->ticket) {
+        if (c->ticket_env < 0) c->ticket = (geo_blocks(c, g) <= 64 || (c->geo.world > 1 && g.L >= 8192)) ? 1 : 0;
+    }
+    ~TicketScope() { c->ticket = saved; }
+};
+
 template <int HB>
 int vf_commit_hb(lbk_ctx* c, int obj, int h, const double* x, const double* g, const double* const* S,
                  const double* const* Y, const double* cs, const double* cy, double cg, double alpha,
                  const double* cand, double* xn, double* gn, double* so, double* yo, int wslot) {
     const NtScope nts(c, c->nt_vf);
     Geo geo = vgeo(c);
+    const TicketScope tks(c, geo);
     Red r = kred(c, wslot);
     const VfBasis<HB> B = vf_basis<HB>(h, S, Y, cs, cy, cg);
     constexpr int K = LBK_VF_YB + 4 * HB + LBK_VF_NA;

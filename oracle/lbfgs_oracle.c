@@ -78,7 +78,7 @@ void orc_checksum(const double* x, int64_t n, uint64_t* c1, uint64_t* c2) {
  * Reductions.
  * ORC_SEQ  : vector_utils.cpp:32-41 (dotProduct), :78-86 (vectorNorm) — left to right.
  * ORC_CANON: the device order:
- *   seg_len L = max(Lmin, roundup(ceil(n/8192), 128)), Lmin = 2048 for 262144 <= n <= 2097152
+ *   seg_len L = max(Lmin, roundup(ceil(n/8192), 128)), Lmin = 2048 for 65536 <= n <= 2097152
  *   (lbfgs_kernels.hip lbk_geometry_plan: n that cannot shard), 512 otherwise;
  *   segment s = [sL, min((s+1)L, n));
  *   thread t = 64w + lane (256 per segment); thread t visits, for u = 0.., row r = 4u + w,
@@ -96,7 +96,7 @@ void orc_checksum(const double* x, int64_t n, uint64_t* c1, uint64_t* c2) {
 void orc_canon_geometry(int64_t n, int64_t* seg_len, int64_t* nseg) {
     int64_t per = (n + CANON_SEGS - 1) / CANON_SEGS;
     int64_t L = ((per + 127) / 128) * 128;
-    const int64_t lmin = (n >= 262144 && n <= 2097152) ? 2048 : 512;
+    const int64_t lmin = (n >= 65536 && n <= 2097152) ? 2048 : 512;
     if (L < lmin) L = lmin;
     *seg_len = L;
     *nseg = (n + L - 1) / L;
@@ -133,7 +133,14 @@ static void canon_groups_mode(const double* a, const double* b, int64_t n, int64
     orc_canon_geometry(n, &L, &nseg);
     int64_t spg = CANON_SEG_PER_GROUP;
     if (contig) {
+        /* base length: the canonical L, except 65536 <= n < 262144 where the vector-free commit
+         * keeps the 512-minimum length (lbfgs_kernels.hip vf_base_len) */
         const int F = orc_vf_factor(n);
+        if (n >= 65536 && n < 262144) {
+            const int64_t per = (n + CANON_SEGS - 1) / CANON_SEGS;
+            L = ((per + 127) / 128) * 128;
+            if (L < 512) L = 512;
+        }
         L *= F;
         nseg = (n + L - 1) / L;
         spg /= F;
