@@ -7,7 +7,9 @@ series sharding the same n across ranks).
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 
 A step is one L-BFGS iteration of the whole n-vector problem (two-loop recursion, line search,
-commit). Warm-up iterations fill the m-pair history, so every timed step uses h = m pairs.
+commit). Before the W warm-up steps, m untimed iterations fill the m-pair history
+(`history_fill`), so every timed step uses h = m pairs whatever W is; the line reports the
+h range of the timed steps (`h_min`, `h_max`, `steady_state`).
 All vectors are resident in HBM before timing starts. One process per GPU; the solver's data
 path exchanges group partials with RCCL all-gathers inside liblbfgs_hip.so; torch.distributed
 (gloo) is only used for the rendezvous (unique id), barriers and the max-over-ranks time.
@@ -18,6 +20,7 @@ import argparse
 import json
 import os
 import platform
+import shutil
 import subprocess
 import sys
 import tempfile
@@ -47,7 +50,10 @@ def parse():
     p.add_argument("--objective", default="rosenbrock")
     p.add_argument("--line-search", default="backtracking")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-n", type=float, default=1e7, help="CPU baseline sample size")
+    p.add_argument("--cpu-n", type=float, default=None,
+                   help="CPU baseline size (default: the benchmark's n, measured directly)")
+    p.add_argument("--cpu-n2", type=float, default=1e7,
+                   help="secondary CPU baseline size reported beside it (0: none)")
     p.add_argument("--no-prof", action="store_true", help="no per-kernel HIP events")
     p.add_argument("--unfused", action="store_true",
                    help="one launch per BLAS-1 op (BASELINE configs[1] shape), same iterates")
@@ -110,30 +116,77 @@ class Dist:
             self.dist.destroy_process_group()
 
 
-def cpu_baseline(n_sample, m, steps_for_h):
+class CpuBaseline:
     """The reference itself (oracle/_ref/ref_lbfgs: the reference's sequential sources compiled
-    unmodified, -O2 -ffp-contract=off), single core, Rosenbrock n_sample, m, backtracking.
-    Per-iteration times come from the trace driver's grad() timestamps; the steady state uses
-    the iterations with h = m pairs, scaled linearly in n to the benchmark's n."""
-    ref = os.path.join(ROOT, "oracle", "_ref", "ref_lbfgs")
-    n_sample = int(n_sample)
-    iters = m + 2
-    if not os.path.exists(ref):
-        return None
-    with tempfile.TemporaryDirectory() as tmp:
-        pre = os.path.join(tmp, "cpu")
-        cmd = [ref, "rosenbrock", str(n_sample), str(m), "backtracking", str(iters), "1e-5", "42",
-               "-2", "2", pre, "0"]
+    unmodified, -O2 -ffp-contract=off), one core, Rosenbrock, m, backtracking, x0 ~ U(-2,2) from
+    std::mt19937(42), as BASELINE.md §3 prescribes: m + 2 iterations, the steady state is the mean
+    of the iterations with h = m pairs. Per-iteration times come from the trace driver's grad()
+    timestamps (each grad call also checksums x and takes |g|: 2 extra reads of ~8m + 11 vector
+    passes, i.e. the CPU figure is ~2 % pessimistic).
+
+    The runs start as child processes pinned (taskset) to host cores the benchmark process
+    leaves alone, before the GPU work, and are collected after it: the GPU timing does not
+    wait for them and they share no device or core with it. `pinned` records whether taskset
+    worked; an unpinned run is reported as such, never silently."""
+
+    def __init__(self, sizes, m):
+        self.runs = []
+        ref = os.path.join(ROOT, "oracle", "_ref", "ref_lbfgs")
+        if not os.path.exists(ref):
+            return
         try:
-            cmd = ["taskset", "-c", "0"] + cmd
-            subprocess.run(cmd, check=True, capture_output=True, timeout=600)
-        except (FileNotFoundError, subprocess.CalledProcessError):
-            subprocess.run(cmd[3:], check=True, capture_output=True, timeout=600)
-        g = np.fromfile(pre + ".g.bin", dtype=np.uint64).reshape(-1, 5)
-        t = g[:, 3].copy().view(np.float64)
-    dt = np.diff(t)  # dt[k] = time of iteration k (grad call k -> k+1)
-    steady = dt[m:]  # iterations with h = m
-    return dict(per_iter_s=float(np.mean(steady)), iters_timed=len(steady), total_s=float(t[-1]))
+            cores = sorted(os.sched_getaffinity(0))
+        except AttributeError:
+            cores = list(range(os.cpu_count() or 1))
+        self.tmp = tempfile.TemporaryDirectory()
+        for j, n in enumerate(sizes):
+            n = int(n)
+            pre = os.path.join(self.tmp.name, f"cpu{j}")
+            cmd = [ref, "rosenbrock", str(n), str(m), "backtracking", str(m + 2), "1e-5", "42", "-2", "2", pre, "0"]
+            core = cores[j % len(cores)] if len(cores) > len(sizes) else None
+            pinned = False
+            if core is not None and shutil.which("taskset"):
+                probe = subprocess.run(["taskset", "-c", str(core), "true"], capture_output=True)
+                pinned = probe.returncode == 0
+            full = (["taskset", "-c", str(core)] + cmd) if pinned else cmd
+            p = subprocess.Popen(full, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
+            self.runs.append(dict(n=n, m=m, pre=pre, proc=p, core=core if pinned else None, pinned=pinned,
+                                  t0=time.perf_counter()))
+        # keep the benchmark's own threads off the reference's cores
+        used = {r["core"] for r in self.runs if r["core"] is not None}
+        rest = [c for c in cores if c not in used]
+        if used and rest:
+            try:
+                os.sched_setaffinity(0, rest)
+            except OSError:
+                pass
+
+    def collect(self, timeout=900):
+        out = []
+        for r in self.runs:
+            p = r["proc"]
+            try:
+                p.wait(timeout=max(timeout - (time.perf_counter() - r["t0"]), 1))
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+                out.append(dict(n=r["n"], error="timed out"))
+                continue
+            if p.returncode != 0:
+                out.append(dict(n=r["n"], error=f"rc={p.returncode} {p.stderr.read().decode()[-200:]}"))
+                continue
+            g = np.fromfile(r["pre"] + ".g.bin", dtype=np.uint64).reshape(-1, 5)
+            t = g[:, 3].copy().view(np.float64)
+            dt = np.diff(t)  # dt[k] = time of iteration k (grad call k -> k+1)
+            steady = dt[r["m"]:]  # iterations with h = m
+            out.append(dict(n=r["n"], per_iter_s=float(np.mean(steady)), iters_timed=len(steady),
+                            total_s=float(t[-1]), pinned=r["pinned"], core=r["core"]))
+        for r in self.runs:
+            if r["proc"].stderr:
+                r["proc"].stderr.close()
+        if self.runs:
+            self.tmp.cleanup()
+        return out
 
 
 def ntag(n):
@@ -185,12 +238,19 @@ def measure(a, D, n, x0, dev, rank, world, uid, unfused=False, vector_free=False
             raise L.LbfgsError("xGMI peer exchange unavailable and no RCCL communicator")
         if ok and a.exchange == "auto" and uid is not None:
             # collective calls in the same order on every rank; the slowest rank decides
+            # vote after each collective timing, so that no rank enters the RCCL all-gather
+            # unless every rank got through the mailbox timing (RCCL has no timeout)
+            lx = lr = None
             try:
-                lx, lr = ctx.exchange_latency("xgmi", 8, 100), ctx.exchange_latency("rccl", 8, 100)
+                lx = ctx.exchange_latency("xgmi", 8, 100)
             except L.LbfgsError as e:
-                print(f"rank {rank}: exchange timing failed: {e}", file=sys.stderr, flush=True)
-                lx = lr = None
-            timed = D.all_ok(lx is not None)
+                print(f"rank {rank}: xgmi exchange timing failed: {e}", file=sys.stderr, flush=True)
+            if D.all_ok(lx is not None):
+                try:
+                    lr = ctx.exchange_latency("rccl", 8, 100)
+                except L.LbfgsError as e:
+                    print(f"rank {rank}: rccl exchange timing failed: {e}", file=sys.stderr, flush=True)
+            timed = D.all_ok(lx is not None and lr is not None)
             tx = D.allreduce(lx if timed else 0.0, "max")
             tr = D.allreduce(lr if timed else 0.0, "max")
             if timed and tr < 0.9 * tx:
@@ -200,6 +260,9 @@ def measure(a, D, n, x0, dev, rank, world, uid, unfused=False, vector_free=False
                       flush=True)
     backend = ctx.backend
     ctx.init(a.objective, x0, a.line_search, tolerance=1e-5, unfused=unfused, vector_free=vector_free)
+    # history fill (untimed, not counted as warm-up): m iterations store m pairs, so every later
+    # step uses h = m whatever --warmup is (B_iter grows with h)
+    fill = ctx.step(a.history)
     ctx.step(a.warmup)
     ctx.sync()
     D.barrier()
@@ -236,7 +299,8 @@ def measure(a, D, n, x0, dev, rank, world, uid, unfused=False, vector_free=False
             for k in (8, 96):
                 lat[f"{b}_{k * 8}doubles"] = round(ctx.exchange_latency(b, k, 200), 2)
     ctx.close()
-    done_steps = a.steps if res["status"] == "running" else max(res["iterations"] - a.warmup, 1)
+    res["history_fill"] = fill["iterations"]
+    done_steps = a.steps if res["status"] == "running" else max(res["iterations"] - a.warmup - fill["iterations"], 1)
     return T, res, prof, bytes_all, done_steps, (backend, lat)
 
 
@@ -328,6 +392,12 @@ def main():
     need_uid = world > 1 and not rehearsal
     uid = D.broadcast_bytes(L.unique_id() if (need_uid and rank == 0) else None) if need_uid else None
 
+    # the reference on host cores, started first and collected after the GPU work (rank 0, N=1)
+    cpu_runs = None
+    if world == 1 and rank == 0 and not a.no_cpu_baseline:
+        sizes = [int(a.cpu_n) if a.cpu_n else n] + ([int(a.cpu_n2)] if a.cpu_n2 else [])
+        cpu_runs = CpuBaseline(sizes, a.history)
+
     x0 = L.x0_uniform(n, 42, -2.0, 2.0)
     # BENCH_DEVICE_MOD=k maps rank -> device local_rank % k (rehearsing several ranks on fewer GPUs)
     # a launcher that exposes one device per process (HIP_VISIBLE_DEVICES) leaves local_rank >= count
@@ -365,26 +435,38 @@ def main():
         value = done_steps / T
         roof = roofline(prof, n, world)
         cpu = None
-        if world == 1 and not a.no_cpu_baseline:
-            cb = cpu_baseline(a.cpu_n, a.history, a.history)
-            if cb:
-                scale = n / int(a.cpu_n)
-                cpu = dict(value=round(1.0 / (cb["per_iter_s"] * scale), 6), unit="iters/s", cores=1,
-                           kind="reference",
-                           sample=(f"reference sequential LBFGS (oracle/_ref, sources compiled -O2 "
-                                   f"-ffp-contract=off), Rosenbrock n={int(a.cpu_n):.0e} m={a.history} "
-                                   f"backtracking, mean of {cb['iters_timed']} steady iterations "
-                                   f"(h=m) = {cb['per_iter_s']:.3f} s/iter, scaled x{scale:g} "
-                                   f"linearly in n to n={n:.0e}; 1 of {os.cpu_count()} cores "
-                                   f"({cpu_model()})"),
-                           per_iter_s_sample=cb["per_iter_s"], total_s=round(cb["total_s"], 2))
+        if cpu_runs is not None:
+            cbs = cpu_runs.collect()
+            main_cb = cbs[0] if cbs else None
+            if main_cb and "per_iter_s" in main_cb:
+                scale = n / main_cb["n"]
+                cpu = dict(value=round(1.0 / (main_cb["per_iter_s"] * scale), 6), unit="iters/s", cores=1,
+                           kind="reference", pinned=main_cb["pinned"],
+                           sample=(f"reference sequential LBFGS (oracle/_ref, its sources compiled -O2 "
+                                   f"-ffp-contract=off), Rosenbrock n={main_cb['n']:.0e} m={a.history} "
+                                   f"backtracking, {a.history + 2} iterations, mean of the "
+                                   f"{main_cb['iters_timed']} with h=m = {main_cb['per_iter_s']:.3f} s/iter"
+                                   + (f" (scaled x{scale:g} linearly in n to n={n:.0e})" if scale != 1 else
+                                      " (measured directly at the benchmark's n)")
+                                   + f"; {'pinned to core ' + str(main_cb['core']) if main_cb['pinned'] else 'NOT pinned'}"
+                                   f", 1 thread, of {os.cpu_count()} cores ({cpu_model()})"),
+                           per_iter_s=main_cb["per_iter_s"], total_s=round(main_cb["total_s"], 2),
+                           secondary=[dict(n=c["n"], per_iter_s=c.get("per_iter_s"), pinned=c.get("pinned"),
+                                           error=c.get("error")) for c in cbs[1:]])
+            elif cbs:
+                cpu = {"error": cbs[0].get("error", "no result")}
+        h_min, h_max = res.get("h_min", -1), res.get("h_max", -1)
         out = {
-            "metric": "L-BFGS iters/sec (n=1e8 Rosenbrock, m=10, fp64)",
+            "metric": f"L-BFGS iters/sec (n={ntag(n)} {a.objective.capitalize()}, m={a.history}, fp64)",
             "value": round(value, 4),
             "unit": "iters/s",
             "n_gpus": world,
             "steps": done_steps,
             "warmup": a.warmup,
+            "history_fill": res["history_fill"],
+            "h_min": h_min,
+            "h_max": h_max,
+            "steady_state": h_min == a.history,
             "ms_per_step": round(T / done_steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": "strong",

@@ -25,6 +25,11 @@
 using std::vector;
 
 // ---- benchmark objectives: the reference formulas, host-side (benchmark.cpp:16-81) ----------
+// Protected visibility: identify() below compares a caller's function pointer with THIS
+// library's definitions. A caller that defines its own function of the same name (the
+// reference's main.cpp defines quadratic / quadratic_grad, main.cpp:7-21) keeps its own address
+// and is run as a host callback, never silently replaced by a device kernel.
+#define LBFGS_OWN __attribute__((visibility("protected")))
 namespace lbfgs_amd {
 double QuadTridiagF::operator()(const vector<double>& x) const {
     double result = 0.0;
@@ -50,7 +55,7 @@ std::function<vector<double>(const vector<double>&)> generate_quadratic_gradient
     return lbfgs_amd::QuadTridiagG{n};
 }
 
-double rosenbrock(const vector<double>& X) {
+LBFGS_OWN double rosenbrock(const vector<double>& X) {
     double sum = 0.0;
     for (size_t i = 0; i + 1 < X.size(); i++) {
         double term1 = X[i + 1] - X[i] * X[i];
@@ -60,7 +65,7 @@ double rosenbrock(const vector<double>& X) {
     return sum;
 }
 
-vector<double> rosenbrock_grad(const vector<double>& X) {
+LBFGS_OWN vector<double> rosenbrock_grad(const vector<double>& X) {
     vector<double> grad(X.size(), 0.0);
     for (size_t i = 0; i + 1 < X.size(); i++) {
         double term1 = 2.0 * (X[i] - 1);
@@ -71,13 +76,13 @@ vector<double> rosenbrock_grad(const vector<double>& X) {
     return grad;
 }
 
-double quadratic(const vector<double>& X) {
+LBFGS_OWN double quadratic(const vector<double>& X) {
     double sum = 0.0;
     for (const double x : X) sum += (x - 1) * (x - 1);
     return sum;
 }
 
-vector<double> quadratic_grad(const vector<double>& X) {
+LBFGS_OWN vector<double> quadratic_grad(const vector<double>& X) {
     vector<double> g(X.size());
     for (size_t i = 0; i < X.size(); i++) g[i] = 2.0 * (X[i] - 1);
     return g;
@@ -143,6 +148,8 @@ void host_g(const double* x, int64_t n, double* out, void* user) {
         std::fill(out, out + n, std::numeric_limits<double>::quiet_NaN());
     }
 }
+
+thread_local int g_last_objective = -1;
 
 struct CtxDeleter {
     void operator()(lbfgs_ctx* c) const { lbfgs_ctx_destroy(c); }
@@ -224,6 +231,7 @@ vector<double> run(const FnF& f, const FnG& grad, const vector<double>& x0, int 
     const int64_t n = (int64_t)x0.size();
     if (n < 1) throw std::invalid_argument("x0 must not be empty");
     const int obj = identify(f, grad, (int)n);
+    g_last_objective = obj;
     lbfgs_ctx* c = context_for(n, m);
     HostFns hf{&f, &grad, {}};
     lbfgs_host_fn cb{host_f, host_g, &hf};
@@ -265,6 +273,22 @@ vector<double> LBFGS_CUDA(const FnF f, const FnG grad, const vector<double> x0, 
 vector<double> LBFGS_CUDA(const FnF f, const FnG grad, const vector<double> x0, const int max_iterations,
                           const int m, const double tolerance) {
     return LBFGS_CUDA(f, grad, x0, std::string("backtracking"), max_iterations, m, tolerance);
+}
+
+int lbfgs_amd::last_objective() { return g_last_objective; }
+
+// benchmark.cpp:83-105: the reference's timing harness over LBFGS (backtracking, not verbose)
+double benchmark(const std::string function_name, const FnF f, const FnG grad, const vector<double> x0,
+                 const int max_iterations, const int m, const double tolerance) {
+    auto start = std::chrono::high_resolution_clock::now();
+    vector<double> optimum = LBFGS(f, grad, x0, "backtracking", max_iterations, m, tolerance, false);
+    auto end = std::chrono::high_resolution_clock::now();
+    const std::chrono::duration<double> elapsed = end - start;
+    std::cout << "Function: " << function_name << std::endl;
+    std::cout << "Optimum value: " << f(optimum) << std::endl;
+    std::cout << "Elapsed time: " << elapsed.count() << " seconds" << std::endl;
+    std::cout << "---------------------------------------------" << std::endl;
+    return elapsed.count();
 }
 
 // ---- line_search.h (line_search.cpp:8-189) --------------------------------------------------

@@ -94,6 +94,7 @@ struct lbfgs_ctx {
     int vf_cand_valid;
     /* counters */
     int64_t trials_f, trials_fg, commits, passes;
+    int h_min, h_max; /* pairs stored at the top of the iterations of the current call */
     /* messages / trace */
     char* msg;
     int msg_len, msg_cap;
@@ -668,6 +669,11 @@ static int commit(lbfgs_ctx* c, int dmode, double alpha, int cslot, double* tot)
 /* ------------------------------------------------------------------------------------------
  * One iteration of lbfgs.cpp:72-199. Returns 0 to continue, 1 when finished, < 0 on error.
  * ---------------------------------------------------------------------------------------- */
+static void note_h(lbfgs_ctx* c) {
+    if (c->h_min < 0 || c->h < c->h_min) c->h_min = c->h;
+    if (c->h > c->h_max) c->h_max = c->h;
+}
+
 static int iterate(lbfgs_ctx* c) {
     const int k = c->k, m = c->m, h = c->h;
     const double gnorm = sqrt(c->gg);
@@ -682,6 +688,7 @@ static int iterate(lbfgs_ctx* c) {
         c->status = LBFGS_STATUS_CONVERGED;
         return 1;
     }
+    note_h(c);
 
     /* ---- search direction (:87-143) ---- */
     int dmode = LBK_D_NEG_G;
@@ -942,6 +949,7 @@ static int iterate_vf(lbfgs_ctx* c) {
         c->status = LBFGS_STATUS_CONVERGED;
         return 1;
     }
+    note_h(c);
 
     /* ---- direction in coefficient space (:87-143): d = -(r) with r over the basis ---- */
     c->vf_h = h;
@@ -1204,11 +1212,15 @@ static void fill_result(lbfgs_ctx* c, lbfgs_result* out, double t0, double b0) {
     out->passes = c->passes;
     out->bytes = lbk_bytes_moved(c->dev) - b0;
     out->seconds = now_s() - t0;
+    out->h_min = c->h_min;
+    out->h_max = c->h_min < 0 ? -1 : c->h_max;
 }
 
 int lbfgs_solver_step(lbfgs_ctx* c, int max_steps, lbfgs_result* out) {
     if (!c || !c->inited) return LBFGS_ERR_STATE;
     const double t0 = now_s(), b0 = lbk_bytes_moved(c->dev);
+    c->h_min = -1;
+    c->h_max = -1;
     if (!c->finished) {
         for (int s = 0; s < max_steps; ++s) {
             int rc = c->vf ? iterate_vf(c) : iterate(c);
@@ -1237,7 +1249,7 @@ int lbfgs_minimize(lbfgs_ctx* c, int objective, const lbfgs_host_fn* cb, int lin
     const double b0 = lbk_bytes_moved(c->dev);
     int rc = lbfgs_solver_init(c, objective, cb, line_search, k, x0_host, tolerance, flags);
     if (rc) return rc;
-    rc = lbfgs_solver_step(c, max_iterations, NULL);
+    rc = lbfgs_solver_step(c, max_iterations, NULL); /* sets h_min / h_max for the whole solve */
     if (rc < 0) return rc;
     if (!c->finished) { /* :201-202 */
         rc = trace_push(c, c->f_cur, sqrt(c->gg), 1);

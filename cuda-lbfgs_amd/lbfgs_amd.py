@@ -39,7 +39,7 @@ class Result(C.Structure):
     _fields_ = [("iterations", C.c_int), ("status", C.c_int), ("f", C.c_double),
                 ("gnorm", C.c_double), ("trials_f", C.c_int64), ("trials_fg", C.c_int64),
                 ("commits", C.c_int64), ("passes", C.c_int64), ("bytes", C.c_double),
-                ("seconds", C.c_double)]
+                ("seconds", C.c_double), ("h_min", C.c_int), ("h_max", C.c_int)]
 
     def as_dict(self):
         d = {k: getattr(self, k) for k, _ in self._fields_}

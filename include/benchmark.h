@@ -1,5 +1,6 @@
-/* benchmark.h — drop-in for the objective surface of sequential-implementation/benchmark.h:12-16
- * and main.cpp:7-21 (= parallel-implementation/functions.h:6-12).
+/* benchmark.h — drop-in for sequential-implementation/benchmark.h:12-26 (the objectives and the
+ * benchmark() timing harness that the reference's main.cpp:45-53 calls) and the separable
+ * quadratic of main.cpp:7-21 (= parallel-implementation/functions.h:6-12).
  *
  * These are ordinary host functions with the reference's exact formulas, so user code that
  * calls them directly gets the reference's values. When they are passed to LBFGS() /
@@ -8,7 +9,9 @@
  * the host-callback path (LBFGS_OBJ_HOST). */
 #ifndef LBFGS_AMD_BENCHMARK_H
 #define LBFGS_AMD_BENCHMARK_H
+#include <chrono>
 #include <functional>
+#include <iostream>
 #include <string>
 #include <vector>
 
@@ -35,7 +38,17 @@ std::function<std::vector<double>(const std::vector<double>&)> generate_quadrati
 double rosenbrock(const std::vector<double>& X);
 std::vector<double> rosenbrock_grad(const std::vector<double>& X);
 
+/* a caller may define its own quadratic / quadratic_grad (the reference's main.cpp:7-21 does);
+ * those are the caller's functions and run through the host-callback path */
 double quadratic(const std::vector<double>& X);
 std::vector<double> quadratic_grad(const std::vector<double>& X);
+
+/* benchmark.h:19-26 / benchmark.cpp:83-105: times LBFGS(f, grad, x0, "backtracking",
+ * max_iterations, m, tolerance, false) and prints
+ *   Function: <name> / Optimum value: <f(optimum)> / Elapsed time: <s> seconds / a rule,
+ * returning the elapsed seconds. */
+double benchmark(const std::string function_name, const std::function<double(std::vector<double>)> f,
+                 const std::function<std::vector<double>(std::vector<double>)> grad,
+                 const std::vector<double> x0, const int max_iterations, const int m, const double tolerance);
 
 #endif

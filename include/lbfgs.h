@@ -34,4 +34,11 @@ std::vector<double> LBFGS_CUDA(const std::function<double(std::vector<double>)> 
                                const std::vector<double> x0, const int max_iterations, const int m,
                                const double tolerance);
 
+namespace lbfgs_amd {
+/* which objective path the calling thread's last LBFGS / LBFGS_CUDA call took: 0 Rosenbrock,
+ * 1 tridiagonal quadratic, 2 separable quadratic (device kernels), 3 host callbacks
+ * (LBFGS_OBJ_* of lbfgs_hip.h); -1 before the first call. Diagnostic for tests. */
+int last_objective();
+}  // namespace lbfgs_amd
+
 #endif

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define LBFGS_HIP_ABI_VERSION 1
+#define LBFGS_HIP_ABI_VERSION 2
 
 typedef struct lbfgs_ctx lbfgs_ctx;
 
@@ -121,6 +121,8 @@ typedef struct {
     int64_t passes;      /* device kernel launches */
     double bytes;        /* algorithmic HBM bytes moved by all launches (this rank) */
     double seconds;      /* wall time of the solve / step call */
+    int h_min, h_max;    /* history pairs stored at the top of the iterations this call ran
+                          * (h of SURVEY.md 8(d)'s B_iter; -1 when the call ran none) */
 } lbfgs_result;
 
 /* ---- context ---------------------------------------------------------------------------- */

@@ -43,3 +43,19 @@ def test_pmc_traffic_from_committed_profile(bench):
     vf, _ = bench.pmc_traffic("vf_commit", 10 ** 8, 1)
     assert vf == pytest.approx(26 * 8e8, rel=0.02)
     assert bench.pmc_traffic("axpy_dot", 10 ** 8, 8) == (None, None)  # per-rank PMC not committed
+
+
+def test_cpu_baseline_runner(bench):
+    """The reference timed on host cores beside the GPU run: child processes, steady iterations
+    (h = m) averaged, pinning recorded (tiny sizes here; bench.py runs n = 1e8 and 1e7)."""
+    if not os.path.exists(os.path.join(ROOT, "oracle", "_ref", "ref_lbfgs")):
+        pytest.skip("oracle/_ref not built (needs /root/reference)")
+    aff = os.sched_getaffinity(0)
+    try:
+        cb = bench.CpuBaseline([3000, 1000], 3)
+        out = cb.collect(timeout=120)
+    finally:
+        os.sched_setaffinity(0, aff)
+    assert [o["n"] for o in out] == [3000, 1000]
+    for o in out:
+        assert o["per_iter_s"] > 0 and o["iters_timed"] == 2 and isinstance(o["pinned"], bool)
