@@ -2031,7 +2031,7 @@ int flush_pending(lbk_ctx* c) {
 // segment counts where every consumer workgroup reading all partials is cheaper than a launch.
 Red kred_deferrable(lbk_ctx* c, int slot) {
     Red r = kred(c, slot);
-    if (c->geo.world == 1 && !c->ticket && c->geo.nseg > c->coop_max && c->geo.nseg <= c->defer_max) {
+    if (c->geo.world == 1 && !c->comm && !c->ticket && c->geo.nseg > c->coop_max && c->geo.nseg <= c->defer_max) {
         r.partials = defer_part(c, c->defer_region);
         c->defer_now = 1;
     }
@@ -2109,7 +2109,7 @@ int launch(lbk_ctx* c, int kind, double vec_passes, int slot, F&& fn, int K = 1,
         HIPCHK(c, hipEventRecord(b, c->stream));
         c->pending.push_back({kind, a, b, 0.0});
     }
-    if (exchange && c->geo.world > 1 && slot >= 0) return exchange_slot(c, slot, K);
+    if (exchange && (c->geo.world > 1 || c->comm) && slot >= 0) return exchange_slot(c, slot, K);
     return 0;
 }
 
@@ -2313,7 +2313,17 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
         }
         if (hipMalloc(&c->d_ckslot, sizeof(uint64_t) * LBK_GROUPS * 2) != hipSuccess) return -2;
     }
-    if (world > 1 && !grp && nccl_id) {
+    // one rank with an RCCL id: a 1-rank communicator, and every reduction goes through the
+    // sharded path's in-place all-gather (diagnostic: the RCCL leg executed on a one-GPU box,
+    // bit-identical to the unsharded run; the one-rank shortcuts - cooperative / single-workgroup
+    // iteration, deferred stage 2, host-mirrored stage 2 - are off so the slot order is the
+    // sharded one)
+    if (world == 1 && !grp && nccl_id) {
+        c->direct = 0;
+        c->coop_max = 0;
+        c->small_seg_max = 0;
+    }
+    if (!grp && nccl_id) {
         ncclUniqueId id;
         memcpy(&id, nccl_id, sizeof id);
         ncclResult_t r = ncclCommInitRank(&c->comm, world, id, rank);
@@ -2644,7 +2654,7 @@ int vf_commit_hb(lbk_ctx* c, int obj, int h, const double* x, const double* g, c
         });
         return 0;
     }, K, false, &geo);
-    if (rc || c->geo.world == 1) return rc;
+    if (rc || (c->geo.world == 1 && !c->comm)) return rc;
     return vf_exchange_ghosts(c, wslot, xn, gn, so, yo);
 }
 
@@ -2777,7 +2787,7 @@ int lbk_small_iter(lbk_ctx* c, int obj, int h, const double* g, double* q, doubl
 }
 
 int lbk_small_ok(const lbk_ctx* c, int h) {
-    if (c->geo.world != 1 || h < 1 || h > LBK_SMALL_HMAX) return 0;
+    if (c->geo.world != 1 || c->comm || h < 1 || h > LBK_SMALL_HMAX) return 0;
     if (c->coop_max > 0 && c->geo.nseg <= c->coop_max) return 1;
     return c->small_seg_max > 0 && c->geo.nseg <= c->small_seg_max && c->geo.nseg <= LBK_SMALL_SEGMAX;
 }
@@ -2846,7 +2856,7 @@ int lbk_checksum(lbk_ctx* c, const double* x, uint64_t* c1, uint64_t* c2) {
         *c2 = b;
         return 0;
     }
-    if (c->geo.world > 1 && !c->grp) {
+    if ((c->geo.world > 1 || c->comm) && !c->grp) {
         if (!c->comm) {
             snprintf(c->err, sizeof c->err, "sharded context has no exchange backend");
             return -3;
@@ -2943,7 +2953,7 @@ int lbk_peer_enable(lbk_ctx* c, int on) {
 }
 
 int lbk_exchange_bench(lbk_ctx* c, int backend, int ks, int iters, double* us) {
-    if (c->geo.world <= 1 || c->grp || ks < 1 || ks > LBK_KW || iters < 1) return -1;
+    if ((c->geo.world <= 1 && !c->comm) || c->grp || ks < 1 || ks > LBK_KW || iters < 1) return -1;
     if (backend == 2 && !lbk_xgmi_connected(c->xg)) return -5;
     if (backend == 1 && !c->comm) return -5;
     if (backend != 1 && backend != 2) return -1;
@@ -2967,7 +2977,7 @@ int lbk_exchange_bench(lbk_ctx* c, int backend, int ks, int iters, double* us) {
 }
 
 int lbk_exchange_backend(const lbk_ctx* c) {
-    if (c->geo.world <= 1) return 0;
+    if (c->geo.world <= 1) return c->comm ? 1 : 0;
     if (c->grp) return 3;
     if (c->xg_on) return 2;
     return c->comm ? 1 : 0;

@@ -210,7 +210,7 @@ class Context:
         h = C.c_void_p()
         if group is not None:
             rc = lib().lbfgs_ctx_create_emulated(C.byref(h), self.n, self.m, device, rank, group.h)
-        elif world == 1:
+        elif world == 1 and uid is None:
             rc = lib().lbfgs_ctx_create(C.byref(h), self.n, self.m, device)
         else:
             rc = lib().lbfgs_ctx_create_sharded(C.byref(h), self.n, self.m, device, rank, world, uid)

@@ -130,7 +130,9 @@ typedef struct {
 int lbfgs_ctx_create(lbfgs_ctx** out, int64_t n, int m, int device);
 /* One process per GPU: shard the vectors across 'world' ranks (world | 8) with an RCCL
  * communicator created from 'unique_id' (128 bytes, from lbfgs_unique_id on rank 0), and/or
- * the xGMI peer exchange (lbfgs_peer_*). */
+ * the xGMI peer exchange (lbfgs_peer_*). world = 1 with a unique_id builds a one-rank
+ * communicator and routes every reduction through the sharded path's RCCL all-gather
+ * (diagnostic: the RCCL leg on a one-GPU box, bit-identical to lbfgs_ctx_create). */
 int lbfgs_ctx_create_sharded(lbfgs_ctx** out, int64_t n, int m, int device, int rank, int world,
                              const void* unique_id);
 int lbfgs_unique_id(void* out128);
