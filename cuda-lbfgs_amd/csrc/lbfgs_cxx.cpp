@@ -245,6 +245,10 @@ vector<double> run(const FnF& f, const FnG& grad, const vector<double>& x0, int 
         if (md == "vector_free" && obj != LBFGS_OBJ_HOST && m <= 20) flags |= LBFGS_FLAG_VECTOR_FREE;
         else if (md == "unfused" && obj != LBFGS_OBJ_HOST) flags |= LBFGS_FLAG_UNFUSED;
     }
+    // host callables: LBFGS_REFERENCE_CALLS=1 calls f / grad exactly as the reference does (its
+    // re-evaluations included); default one call per distinct point
+    if (const char* rcalls = std::getenv("LBFGS_REFERENCE_CALLS"))
+        if (std::atoi(rcalls) != 0) flags |= LBFGS_FLAG_REFERENCE_CALLS;
     int rc = lbfgs_minimize(c, obj, obj == LBFGS_OBJ_HOST ? &cb : nullptr, ls, &k, x0.data(), x.data(),
                             max_iterations, tolerance, flags, &res);
     if (!hf.error.empty()) throw std::runtime_error("objective callback failed: " + hf.error);

@@ -134,6 +134,11 @@ int lbk_download(lbk_ctx* c, double* host_global, const double* src);   /* local
 int lbk_copy(lbk_ctx* c, double* dst, const double* src);               /* incl. ghosts */
 int lbk_download_local(lbk_ctx* c, double* host_local, const double* src);
 int lbk_upload_local(lbk_ctx* c, double* dst, const double* host_local);
+/* asynchronous local-range transfers on the solver stream; lbk_xfer_wait(tag) blocks until the
+ * last transfer issued with that tag (0..3) has completed (host buffers must be pinned) */
+int lbk_download_local_async(lbk_ctx* c, double* host_local, const double* src, int tag);
+int lbk_upload_local_async(lbk_ctx* c, double* dst, const double* host_local, int tag);
+int lbk_xfer_wait(lbk_ctx* c, int tag);
 
 /* kernels (async on the context stream). 'slot' = result slot index; slot references
  * (prev, beta, alpha) are (slot index, component) pairs packed as slot*LBK_KMAX + comp. */

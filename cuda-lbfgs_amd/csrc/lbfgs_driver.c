@@ -68,7 +68,18 @@ struct lbfgs_ctx {
     double f_cur, gg;
     int sg_valid, sg_ref;
     lbfgs_host_fn cb;
-    double *hx, *hg; /* host buffers (callbacks) */
+    /* host-callback objective (LBFGS_OBJ_HOST), pinned buffers: hx the trial point z, hxx the
+     * iterate x (reference call order only), hg[2] the gradient double buffer (a callback fills
+     * one while the other's upload may still be in flight) */
+    double *hx, *hxx, *hg[2];
+    int hg_cur;
+    int hz_valid, hz_pending; /* hx holds (or is receiving) z = x + hz_alpha d of this iteration */
+    double hz_alpha;
+    int hxx_valid, hxx_pending;
+    int hf_valid; /* f(z) at hf_alpha, this iteration */
+    double hf_alpha, hf_val;
+    int refcalls; /* LBFGS_FLAG_REFERENCE_CALLS */
+    int64_t cb_f, cb_g;
     /* per-iteration working state */
     int dmode, d_ready;
     double rho_last, a0;
@@ -295,7 +306,9 @@ void lbfgs_ctx_destroy(lbfgs_ctx* c) {
     free_vectors(c);
     lbk_destroy(c->dev);
     lbk_host_free(c->hx);
-    lbk_host_free(c->hg);
+    lbk_host_free(c->hxx);
+    lbk_host_free(c->hg[0]);
+    lbk_host_free(c->hg[1]);
     free(c->msg);
     free(c->tr_f);
     free(c->tr_gn);
@@ -360,25 +373,132 @@ int lbfgs_exchange_latency(lbfgs_ctx* c, int backend, int components, int iters,
 }
 
 /* ------------------------------------------------------------------------------------------
- * Host-callback objective helpers (LBFGS_OBJ_HOST; single rank)
+ * Host-callback objective (LBFGS_OBJ_HOST; single rank). The device forms every point the
+ * objective is called at (z = x + alpha d, as the commit will form x_new) and the host calls
+ * f / grad on a pinned copy of it.
+ *   default: one f and at most one grad call per distinct point: z, f(z) and grad(z) are
+ *            cached for the iteration, so a Wolfe trial's gradient (line_search.cpp:160) reuses
+ *            its f call (:146), and the commit (lbfgs.cpp:160,171) reuses both;
+ *   LBFGS_FLAG_REFERENCE_CALLS: the reference's own call sequence, call for call, including its
+ *            re-evaluations of f(x) inside the line searches (line_search.cpp:24,42,65,133) and
+ *            of f, grad at x_new after them (lbfgs.cpp:160,171); values returned by those calls
+ *            are the ones used, as in the reference.
+ * Transfers are asynchronous on the solver stream: the gradient upload runs from one of two
+ * pinned buffers while the host goes on (e.g. into the f call that follows a grad call,
+ * line_search.cpp:39-42), and in the reference order z's download overlaps the f(x) call.
  * ---------------------------------------------------------------------------------------- */
+#define XF_Z 0
+#define XF_X 1
+#define XF_G0 2 /* + buffer */
+
 static int host_bufs(lbfgs_ctx* c) {
-    /* pinned: the per-trial x download and gradient upload are direct DMA, no staging copy */
-    if (!c->hx) c->hx = (double*)lbk_host_alloc(sizeof(double) * (size_t)c->n);
-    if (!c->hg) c->hg = (double*)lbk_host_alloc(sizeof(double) * (size_t)c->n);
-    return (c->hx && c->hg) ? 0 : LBFGS_ERR_NOMEM;
+    const size_t b = sizeof(double) * (size_t)c->n;
+    if (!c->hx) c->hx = (double*)lbk_host_alloc(b);
+    if (!c->hg[0]) c->hg[0] = (double*)lbk_host_alloc(b);
+    if (!c->hg[1]) c->hg[1] = (double*)lbk_host_alloc(b);
+    if (c->refcalls && !c->hxx) c->hxx = (double*)lbk_host_alloc(b);
+    return (c->hx && c->hg[0] && c->hg[1] && (!c->refcalls || c->hxx)) ? 0 : LBFGS_ERR_NOMEM;
 }
 
-/* f (and optionally grad -> device vector gdst) at z = x + alpha d on the host */
-static int host_eval_at(lbfgs_ctx* c, double alpha, double* f, double* gdst) {
+/* x or d changed: nothing cached refers to the current iteration */
+static void host_invalidate(lbfgs_ctx* c) {
+    c->hz_valid = 0;
+    c->hf_valid = 0;
+    c->gt_valid = 0;
+}
+
+/* issue z = x + alpha d and its download (no wait) */
+static int host_point_issue(lbfgs_ctx* c, double alpha) {
+    if (c->hz_valid && c->hz_alpha == alpha) return 0;
+    if (c->hz_pending) DEVNC(lbk_xfer_wait(c->dev, XF_Z)); /* hx is still being written */
     DEV(lbk_point(c->dev, c->xn, c->x, c->d, alpha));
-    DEVNC(lbk_download_local(c->dev, c->hx, c->xn));
-    *f = c->cb.f(c->hx, c->n, c->cb.user);
-    if (gdst) {
-        c->cb.grad(c->hx, c->n, c->hg, c->cb.user);
-        DEVNC(lbk_upload_local(c->dev, gdst, c->hg));
+    DEVNC(lbk_download_local_async(c->dev, c->hx, c->xn, XF_Z));
+    c->hz_valid = c->hz_pending = 1;
+    c->hz_alpha = alpha;
+    c->hf_valid = 0;
+    return 0;
+}
+
+static int host_point(lbfgs_ctx* c, double alpha) {
+    int rc = host_point_issue(c, alpha);
+    if (rc) return rc;
+    if (c->hz_pending) {
+        DEVNC(lbk_xfer_wait(c->dev, XF_Z));
+        c->hz_pending = 0;
     }
     return 0;
+}
+
+/* f(z(alpha)); fresh = 1 calls f even if it was evaluated at this point before */
+static int host_f_at(lbfgs_ctx* c, double alpha, int fresh, double* f) {
+    if (!fresh && c->hf_valid && c->hf_alpha == alpha && c->hz_valid && c->hz_alpha == alpha) {
+        *f = c->hf_val;
+        return 0;
+    }
+    int rc = host_point(c, alpha);
+    if (rc) return rc;
+    *f = c->cb.f(c->hx, c->n, c->cb.user);
+    c->cb_f++;
+    c->hf_valid = 1;
+    c->hf_alpha = alpha;
+    c->hf_val = *f;
+    return 0;
+}
+
+/* grad(z(alpha)) into the device vector dst (the upload is left in flight) */
+static int host_g_at(lbfgs_ctx* c, double alpha, int fresh, double* dst) {
+    if (!fresh && c->gt_valid && c->gt_alpha == alpha) {
+        if (dst != c->gt) DEVNC(lbk_copy(c->dev, dst, c->gt));
+        return 0;
+    }
+    int rc = host_point(c, alpha);
+    if (rc) return rc;
+    const int b = c->hg_cur;
+    c->hg_cur ^= 1;
+    DEVNC(lbk_xfer_wait(c->dev, XF_G0 + b)); /* the upload that last read this buffer */
+    c->cb.grad(c->hx, c->n, c->hg[b], c->cb.user);
+    c->cb_g++;
+    DEVNC(lbk_upload_local_async(c->dev, dst, c->hg[b], XF_G0 + b));
+    if (dst == c->gt) {
+        c->gt_valid = 1;
+        c->gt_alpha = alpha;
+    } else if (c->gt_valid && c->gt_alpha == alpha) {
+        c->gt_valid = 0;
+    }
+    return 0;
+}
+
+/* reference call order: f at the iterate x itself (line_search.cpp:24,42,65,133) */
+static int host_fx_issue(lbfgs_ctx* c) {
+    if (c->hxx_valid) return 0;
+    DEVNC(lbk_download_local_async(c->dev, c->hxx, c->x, XF_X));
+    c->hxx_valid = c->hxx_pending = 1;
+    return 0;
+}
+
+static int host_fx(lbfgs_ctx* c, double* f) {
+    int rc = host_fx_issue(c);
+    if (rc) return rc;
+    if (c->hxx_pending) {
+        DEVNC(lbk_xfer_wait(c->dev, XF_X));
+        c->hxx_pending = 0;
+    }
+    *f = c->cb.f(c->hxx, c->n, c->cb.user);
+    c->cb_f++;
+    return 0;
+}
+
+/* f(x) as a line search sees it: the reference's fresh call in its order (the next trial
+ * point's download issued first, so it overlaps the call), else the iteration's f_current */
+static int ls_fx(lbfgs_ctx* c, double next_alpha, double* fx) {
+    if (!(c->obj == LBFGS_OBJ_HOST && c->refcalls)) {
+        *fx = c->f_cur;
+        return 0;
+    }
+    int rc = host_fx_issue(c);
+    if (!rc && next_alpha > 0) rc = host_point_issue(c, next_alpha);
+    if (!rc) rc = host_fx(c, fx);
+    return rc;
 }
 
 /* ------------------------------------------------------------------------------------------
@@ -434,15 +554,23 @@ static int trial(lbfgs_ctx* c, double alpha, int need_g, double* f, double* dphi
             if (dphi) *dphi = t[1];
         }
     } else if (c->obj == LBFGS_OBJ_HOST) {
-        rc = host_eval_at(c, alpha, f, need_g ? c->gt : NULL);
+        /* reference order: the backtracking-Wolfe search takes grad(x_new) before f(x_new)
+         * (line_search.cpp:39-42); the Wolfe search's gradient follows its own f call at the
+         * same point (:146,160), never a second f */
+        const int rf = c->refcalls && !(need_g && c->ls == LBFGS_LS_WOLFE);
+        if (need_g && c->ls == LBFGS_LS_BACKTRACKING_WOLFE) {
+            rc = host_g_at(c, alpha, c->refcalls, c->gt);
+            if (!rc) rc = host_f_at(c, alpha, rf, f);
+        } else {
+            rc = host_f_at(c, alpha, rf, f);
+            if (!rc && need_g) rc = host_g_at(c, alpha, c->refcalls, c->gt);
+        }
         if (rc) return rc;
         if (need_g) {
             double t;
             DEV(lbk_dot(c->dev, c->gt, c->d, SLOT_TRIAL(c->m)));
             DEVNC(lbk_fetch(c->dev, SLOT_TRIAL(c->m), 1, &t));
-            *dphi = t;
-            c->gt_valid = 1;
-            c->gt_alpha = alpha;
+            if (dphi) *dphi = t;
         }
     } else {
         double t[2];
@@ -473,10 +601,11 @@ static int ls_backtracking(lbfgs_ctx* c, double gd, double* out) {
     const lbfgs_constants* K = &c->K;
     double alpha = K->initial_step;
     for (;;) {
-        double ft;
-        int rc = trial(c, alpha, 0, &ft, NULL);
+        double fx, ft;
+        int rc = ls_fx(c, alpha, &fx); /* f(x) - f(x + alpha d), left operand first */
+        if (!rc) rc = trial(c, alpha, 0, &ft, NULL);
         if (rc) return rc;
-        if (!(c->f_cur - ft < K->c1 * alpha * gd)) break;
+        if (!(fx - ft < K->c1 * alpha * gd)) break;
         alpha *= K->backtracking_alpha;
         if (alpha < K->backtracking_tol) break;
     }
@@ -489,10 +618,11 @@ static int ls_backtracking_wolfe(lbfgs_ctx* c, double gd, double* out) {
     const lbfgs_constants* K = &c->K;
     double alpha = K->initial_step;
     for (;;) {
-        double fn, dphi;
+        double fn, dphi, fx;
         int rc = trial(c, alpha, 1, &fn, &dphi);
+        if (!rc) rc = ls_fx(c, 0.0, &fx);
         if (rc) return rc;
-        if (fn > c->f_cur + K->c1 * alpha * gd) {
+        if (fn > fx + K->c1 * alpha * gd) {
             alpha *= K->backtracking_alpha;
         } else if (dphi < K->c2 * gd) {
             alpha *= 1.1;
@@ -508,7 +638,9 @@ static int ls_backtracking_wolfe(lbfgs_ctx* c, double gd, double* out) {
 /* line_search.cpp:57-121 */
 static int ls_interpolation(lbfgs_ctx* c, double gd, double* out) {
     const lbfgs_constants* K = &c->K;
-    const double f_x = c->f_cur;
+    double f_x;
+    int rc0 = ls_fx(c, K->initial_step, &f_x);
+    if (rc0) return rc0;
     double alpha = K->initial_step, alpha_prev = 0.0, f_prev = f_x;
     int it = 0;
     while (it++ < 20) {
@@ -547,7 +679,9 @@ static int ls_interpolation(lbfgs_ctx* c, double gd, double* out) {
 /* line_search.cpp:125-189 */
 static int ls_wolfe(lbfgs_ctx* c, double gd, double* out) {
     const lbfgs_constants* K = &c->K;
-    const double f_x = c->f_cur;
+    double f_x;
+    int rc0 = ls_fx(c, K->initial_step, &f_x);
+    if (rc0) return rc0;
     double alpha = K->initial_step;
     double alpha_lo = 0.0, alpha_hi = INFINITY, f_lo = f_x, dphi_lo = gd;
     for (int iter = 0; iter < 20; ++iter) {
@@ -641,17 +775,18 @@ static int commit(lbfgs_ctx* c, int dmode, double alpha, int cslot, double* tot)
     const double* s_last = dmode == LBK_D_TWOLOOP ? c->S[c->s_last_pair] : NULL;
     int obj = c->obj;
     if (c->obj == LBFGS_OBJ_HOST) {
-        /* host objective: g_new on the device first (reuse the trial gradient if it is the
-         * gradient at exactly this step), f on the host */
+        /* f(x_new) (lbfgs.cpp:160), then - unless the step failed (:164-168) - grad(x_new)
+         * (:171) onto the device for the commit kernel; both from the line search's cache
+         * unless the reference call order asks for the reference's fresh calls */
         double f;
-        if (c->gt_valid && c->gt_alpha == alpha) {
-            int rc = host_eval_at(c, alpha, &f, NULL);
-            if (rc) return rc;
-            DEVNC(lbk_copy(c->dev, c->gn, c->gt));
-        } else {
-            int rc = host_eval_at(c, alpha, &f, c->gn);
-            if (rc) return rc;
+        int rc = host_f_at(c, alpha, c->refcalls, &f);
+        if (rc) return rc;
+        if (alpha < 1e-10) { /* the caller stops here; nothing else of tot is read */
+            tot[LBK_C_F] = f;
+            return 0;
         }
+        rc = host_g_at(c, alpha, c->refcalls, c->gn);
+        if (rc) return rc;
         obj = LBK_OBJ_NONE;
         DEV(lbk_commit(c->dev, obj, dmode, c->x, dsrc, s_last, c->g, c->rho_last, c->ref_b_last,
                        c->ref_a_last, alpha, c->xn, c->gn, c->S[pair], c->Y[pair], cslot));
@@ -696,7 +831,8 @@ static int iterate(lbfgs_ctx* c) {
     const int small = c->obj != LBFGS_OBJ_HOST && !c->unfused && c->geo->world == 1 && lbk_small_ok(c->dev, h);
     c->d_ready = 0;
     c->spec_valid = 0;
-    c->gt_valid = 0;
+    host_invalidate(c);
+    c->hxx_valid = 0;
     if (!(k == 0 || h == 0)) {
         int bad_rho = 0;
         for (int i = h - 1; i >= 0; --i)
@@ -836,6 +972,7 @@ static int iterate(lbfgs_ctx* c) {
             say(c, "Warning: Not a descent direction, using gradient\n");
             c->dmode = LBK_D_NEG_G;
             c->d_ready = 0;
+            host_invalidate(c);
             rc = materialize_d(c);
             if (rc) return rc;
             DEVNC(lbk_fetch(c->dev, SLOT_LAST(m), 1, &gd));
@@ -1130,11 +1267,15 @@ int lbfgs_solver_init(lbfgs_ctx* c, int objective, const lbfgs_host_fn* cb, int 
     if (!c || !x0_host) return LBFGS_ERR_BAD_ARG;
     if (objective < 0 || objective > LBFGS_OBJ_HOST) return LBFGS_ERR_BAD_ARG;
     if (line_search < 0 || line_search > LBFGS_LS_BACKTRACKING_WOLFE) return LBFGS_ERR_BAD_ARG;
+    c->refcalls = (flags & LBFGS_FLAG_REFERENCE_CALLS) != 0;
     if (objective == LBFGS_OBJ_HOST) {
         if (!cb || !cb->f || !cb->grad || c->geo->world != 1) return LBFGS_ERR_BAD_ARG;
         c->cb = *cb;
         if (host_bufs(c)) return LBFGS_ERR_NOMEM;
     }
+    host_invalidate(c);
+    c->hxx_valid = 0;
+    c->cb_f = c->cb_g = 0;
     c->unfused = (flags & LBFGS_FLAG_UNFUSED) != 0;
     if (c->unfused && (objective == LBFGS_OBJ_HOST || c->geo->world != 1)) return LBFGS_ERR_BAD_ARG;
     /* ping-pong q/r (LBFGS_PINGPONG=1): measured neutral at n=1e8 and -8 % at n=1e7 (the
@@ -1184,8 +1325,13 @@ int lbfgs_solver_init(lbfgs_ctx* c, int objective, const lbfgs_host_fn* cb, int 
     DEVNC(lbk_upload(c->dev, c->x, x0_host)); /* x = x0 */
     if (objective == LBFGS_OBJ_HOST) {         /* :29-30 */
         c->f_cur = c->cb.f(x0_host, c->n, c->cb.user);
-        c->cb.grad(x0_host, c->n, c->hg, c->cb.user);
-        DEVNC(lbk_upload_local(c->dev, c->g, c->hg));
+        const int b = c->hg_cur;
+        c->hg_cur ^= 1;
+        DEVNC(lbk_xfer_wait(c->dev, XF_G0 + b));
+        c->cb.grad(x0_host, c->n, c->hg[b], c->cb.user);
+        c->cb_f++;
+        c->cb_g++;
+        DEVNC(lbk_upload_local(c->dev, c->g, c->hg[b]));
         DEV(lbk_dot(c->dev, c->g, c->g, SLOT_INIT));
         DEVNC(lbk_fetch(c->dev, SLOT_INIT, 1, &c->gg));
     } else {
@@ -1214,6 +1360,8 @@ static void fill_result(lbfgs_ctx* c, lbfgs_result* out, double t0, double b0) {
     out->seconds = now_s() - t0;
     out->h_min = c->h_min;
     out->h_max = c->h_min < 0 ? -1 : c->h_max;
+    out->f_calls = c->cb_f;
+    out->grad_calls = c->cb_g;
 }
 
 int lbfgs_solver_step(lbfgs_ctx* c, int max_steps, lbfgs_result* out) {
@@ -1391,12 +1539,14 @@ int lbfgs_line_search(lbfgs_ctx* c, int objective, const lbfgs_host_fn* cb, int 
     if (!c || !x || !d || !g || !alpha_out || c->geo->world != 1) return LBFGS_ERR_BAD_ARG;
     if (objective < 0 || objective > LBFGS_OBJ_HOST) return LBFGS_ERR_BAD_ARG;
     if (line_search < 0 || line_search > LBFGS_LS_BACKTRACKING_WOLFE) return LBFGS_ERR_BAD_ARG;
+    c->refcalls = 0; /* the standalone search evaluates f(x) once (see above) */
     if (objective == LBFGS_OBJ_HOST) {
         if (!cb || !cb->f || (!cb->grad && (line_search == LBFGS_LS_WOLFE || line_search == LBFGS_LS_BACKTRACKING_WOLFE)))
             return LBFGS_ERR_BAD_ARG;
         c->cb = *cb;
         if (host_bufs(c)) return LBFGS_ERR_NOMEM;
     }
+    c->cb_f = c->cb_g = 0;
     c->inited = 0;
     c->unfused = 0;
     c->obj = objective;
@@ -1411,6 +1561,7 @@ int lbfgs_line_search(lbfgs_ctx* c, int objective, const lbfgs_host_fn* cb, int 
     DEVNC(lbk_upload(c->dev, c->g, g));
     if (objective == LBFGS_OBJ_HOST) {
         c->f_cur = c->cb.f(x, c->n, c->cb.user);
+        c->cb_f++;
     } else {
         double t[2];
         DEV(lbk_eval(c->dev, objective, c->x, NULL, SLOT_MISC(m)));
@@ -1423,7 +1574,8 @@ int lbfgs_line_search(lbfgs_ctx* c, int objective, const lbfgs_host_fn* cb, int 
     c->dmode = LBK_D_BUF;
     c->d_ready = 1;
     c->spec_valid = 0;
-    c->gt_valid = 0;
+    host_invalidate(c);
+    c->hxx_valid = 0;
     double alpha = 0.0;
     int rc;
     switch (line_search) {

@@ -1831,6 +1831,7 @@ struct lbk_ctx {
     unsigned* coop_err_d;
     double* coop_redge;            // 2 per segment
     double wall_khz;
+    hipEvent_t xfer_ev[4];  // lbk_*_local_async completion (host-callback transfers)
 };
 
 namespace {
@@ -2341,6 +2342,8 @@ void lbk_destroy(lbk_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     prof_flush(c);
     for (auto e : c->ev_free) (void)hipEventDestroy(e);
+    for (auto e : c->xfer_ev)
+        if (e) (void)hipEventDestroy(e);
     if (c->comm) ncclCommDestroy(c->comm);
     lbk_xgmi_destroy(c->xg);
     if (c->d_ckslot) (void)hipFree(c->d_ckslot);
@@ -2404,6 +2407,32 @@ int lbk_upload_local(lbk_ctx* c, double* dst, const double* host_local) {
     if (c->geo.n_loc == 0) return 0;
     HIPCHK(c, hipMemcpyAsync(dst, host_local, sizeof(double) * c->geo.n_loc, hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+// asynchronous transfers of the local range on the solver stream; event `tag` (0..3) marks the
+// copy's completion for lbk_xfer_wait (host-callback objectives: double-buffered pinned buffers)
+int lbk_download_local_async(lbk_ctx* c, double* host_local, const double* src, int tag) {
+    if (tag < 0 || tag >= 4) return -1;
+    if (!c->xfer_ev[tag]) HIPCHK(c, hipEventCreateWithFlags(&c->xfer_ev[tag], hipEventDisableTiming));
+    if (c->geo.n_loc > 0)
+        HIPCHK(c, hipMemcpyAsync(host_local, src, sizeof(double) * c->geo.n_loc, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipEventRecord(c->xfer_ev[tag], c->stream));
+    return 0;
+}
+
+int lbk_upload_local_async(lbk_ctx* c, double* dst, const double* host_local, int tag) {
+    if (tag < 0 || tag >= 4) return -1;
+    if (!c->xfer_ev[tag]) HIPCHK(c, hipEventCreateWithFlags(&c->xfer_ev[tag], hipEventDisableTiming));
+    if (c->geo.n_loc > 0)
+        HIPCHK(c, hipMemcpyAsync(dst, host_local, sizeof(double) * c->geo.n_loc, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipEventRecord(c->xfer_ev[tag], c->stream));
+    return 0;
+}
+
+int lbk_xfer_wait(lbk_ctx* c, int tag) {
+    if (tag < 0 || tag >= 4) return -1;
+    if (c->xfer_ev[tag]) HIPCHK(c, hipEventSynchronize(c->xfer_ev[tag]));
     return 0;
 }
 

@@ -20,6 +20,7 @@ OBJECTIVES = {"rosenbrock": 0, "quad_tridiag": 1, "quad_sep": 2, "host": 3}
 LINE_SEARCHES = {"backtracking": 0, "interpolation": 1, "wolfe": 2, "backtracking_wolfe": 3}
 STATUS = {0: "converged", 1: "max_iter", 2: "ls_failed", 3: "running"}
 FLAG_VERBOSE, FLAG_QUIET, FLAG_TRACE, FLAG_UNFUSED, FLAG_VECTOR_FREE = 1, 2, 4, 8, 16
+FLAG_REFERENCE_CALLS = 32
 KERNELS = ["dot", "axpy_dot", "mid", "axpy2_dot", "last", "negdot", "eval", "trial_f",
            "trial_fg", "commit", "point", "checksum", "update", "vf_commit", "vf_dir", "small_iter",
            "group_reduce"]
@@ -39,7 +40,8 @@ class Result(C.Structure):
     _fields_ = [("iterations", C.c_int), ("status", C.c_int), ("f", C.c_double),
                 ("gnorm", C.c_double), ("trials_f", C.c_int64), ("trials_fg", C.c_int64),
                 ("commits", C.c_int64), ("passes", C.c_int64), ("bytes", C.c_double),
-                ("seconds", C.c_double), ("h_min", C.c_int), ("h_max", C.c_int)]
+                ("seconds", C.c_double), ("h_min", C.c_int), ("h_max", C.c_int),
+                ("f_calls", C.c_int64), ("grad_calls", C.c_int64)]
 
     def as_dict(self):
         d = {k: getattr(self, k) for k, _ in self._fields_}
@@ -311,7 +313,7 @@ class Context:
 
     def minimize(self, objective, x0, line_search="backtracking", max_iterations=1000, m=None,
                  tolerance=1e-5, verbose=False, quiet=True, trace=False, consts=None,
-                 f=None, grad=None, unfused=False, vector_free=False):
+                 f=None, grad=None, unfused=False, vector_free=False, reference_calls=False):
         assert m is None or m == self.m
         x0 = np.ascontiguousarray(x0, dtype=np.float64)
         assert x0.shape == (self.n,)
@@ -319,7 +321,7 @@ class Context:
         res = Result()
         flags = (FLAG_VERBOSE if verbose else 0) | (FLAG_QUIET if quiet else 0) | \
                 (FLAG_TRACE if trace else 0) | (FLAG_UNFUSED if unfused else 0) | \
-                (FLAG_VECTOR_FREE if vector_free else 0)
+                (FLAG_VECTOR_FREE if vector_free else 0) | (FLAG_REFERENCE_CALLS if reference_calls else 0)
         cb = self._host_fn(f, grad) if objective == "host" else None
         k = consts if consts is not None else constants()
         rc = lib().lbfgs_minimize(self.h, OBJECTIVES[objective], C.byref(cb) if cb else None,

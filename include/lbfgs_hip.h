@@ -87,6 +87,12 @@ enum {
  * (f within 1e-10 over horizons comparable to the canonical order's). Single rank,
  * device objectives, m <= 20. */
 #define LBFGS_FLAG_VECTOR_FREE 16u
+/* host-callback objectives: call f and grad exactly as the reference does, call for call
+ * (its re-evaluations of f(x) in every line search, line_search.cpp:24,42,65,133, and of f and
+ * grad at x_new after it, lbfgs.cpp:160,171), for callables with side effects or counters.
+ * Default: one f and at most one grad call per distinct point (same iterates either way for a
+ * deterministic objective). */
+#define LBFGS_FLAG_REFERENCE_CALLS 32u
 
 typedef struct {
     double c1;                 /* C1 = 1e-4                  config.h:5 */
@@ -123,6 +129,8 @@ typedef struct {
     double seconds;      /* wall time of the solve / step call */
     int h_min, h_max;    /* history pairs stored at the top of the iterations this call ran
                           * (h of SURVEY.md 8(d)'s B_iter; -1 when the call ran none) */
+    int64_t f_calls;     /* host-callback objective: f / grad callbacks since solver init */
+    int64_t grad_calls;
 } lbfgs_result;
 
 /* ---- context ---------------------------------------------------------------------------- */
