@@ -70,6 +70,10 @@ extern "C" {
 #define LBK_C_GG 4   /* g_new . g_new    */
 #define LBK_C_SG 5   /* s . g_new  (alpha of the next first pass) */
 #define LBK_C_DPHI 6 /* g_new . d        */
+#define LBK_C_FC 7   /* f(x + cand d): the line search's next step, computed alongside */
+
+/* batched trials: steps per f-only pass (backtracking / interpolation halving chains) */
+#define LBK_TRIALS_NC 4
 
 /* kernel kinds, for profiling / byte accounting */
 enum {
@@ -159,7 +163,14 @@ int lbk_trial(lbk_ctx* c, int obj, const double* x, const double* d, double alph
  * For obj == NONE the new gradient is read from gn (host-supplied). */
 int lbk_commit(lbk_ctx* c, int obj, int dmode, const double* x, const double* dsrc,
                const double* s_last, const double* g, double rho, int ref_beta, int ref_alpha,
-               double alpha, double* xn, double* gn, double* s_out, double* y_out, int slot);
+               double alpha, double* xn, double* gn, double* s_out, double* y_out, int slot, double cand);
+/* batched line-search trials along d (dmode as the commit's: a buffer, -g, or the last two-loop
+ * update formed on the fly): f at alphas[0..nc-1] (components 0..nc-1) and, with dphi,
+ * g(x + alphas[0] d) . d (component nc; nc = 1 only). nc is 1 or LBK_TRIALS_NC. Device
+ * objectives only. */
+int lbk_trials(lbk_ctx* c, int obj, int dmode, const double* x, const double* dsrc, const double* s_last,
+               const double* g, double rho, int ref_beta, int ref_alpha, const double* alphas, int nc, int dphi,
+               int slot);
 /* z = x + alpha * d (host-callback objectives) */
 int lbk_point(lbk_ctx* c, double* z, const double* x, const double* d, double alpha);
 /* elementwise primitives (op: 0 alpha*a, 1 a+b, 2 -a, 3 a+alpha*b) over the local range */

@@ -89,6 +89,16 @@ struct lbfgs_ctx {
     int gt_valid;
     double gt_alpha;
     int unfused; /* LBFGS_FLAG_UNFUSED */
+    /* batched line-search trials (LBFGS_BATCH, default on): the first commit also reduces f at
+     * the backtracking search's next step; a trial pass evaluates the next LBK_TRIALS_NC steps of
+     * a halving chain, or f and g.d together for the Wolfe searches; d stays unmaterialised for
+     * the first two trial passes and the commit */
+    int batch;
+    int cand_valid;
+    double cand_alpha, cand_f;
+    int tc_n, tc_dphi_ok;
+    double tc_a[LBK_TRIALS_NC], tc_f[LBK_TRIALS_NC], tc_dphi;
+    int trial_passes;
     /* vector-free mode (LBFGS_FLAG_VECTOR_FREE): Gram matrix over the pair pool, indexed by
      * pool slot (P = m + 1): Gss[p][q] = s_p.s_q, Gsy[p][q] = s_p.y_q, Gyy[p][q] = y_p.y_q,
      * Gsg[p] = s_p.g, Gyg[p] = y_p.g (g = current gradient; |g|^2 is gg) */
@@ -526,6 +536,70 @@ static int materialize_d(lbfgs_ctx* c) {
     return 0;
 }
 
+/* Device objectives, batched (c->batch). The steps a search tries after a rejection are known in
+ * advance on its halving chains - backtracking alpha * beta (line_search.cpp:26), interpolation
+ * alpha * 0.5 once alpha_prev == alpha (:92-97, the reference's alpha_prev quirk) - so one pass
+ * evaluates LBK_TRIALS_NC of them, formed by the same repeated multiplication as the search. The
+ * Wolfe searches' next step depends on the f just computed, so their pass takes one step, with
+ * g.d (:160) in the same read (the gradient is recomputed by the commit, never stored). Results
+ * are those of separate single-step passes, bit for bit. */
+static int trial_batched(lbfgs_ctx* c, double alpha, int need_g, double* f, double* dphi) {
+    if (!need_g && c->cand_valid && alpha == c->cand_alpha) { /* reduced by the first commit */
+        *f = c->cand_f;
+        return 0;
+    }
+    for (int j = 0; j < c->tc_n; ++j)
+        if (alpha == c->tc_a[j] && (!need_g || (j == 0 && c->tc_dphi_ok))) {
+            *f = c->tc_f[j];
+            if (need_g && dphi) *dphi = c->tc_dphi;
+            return 0;
+        }
+    const int want_dphi = need_g || c->ls == LBFGS_LS_WOLFE || c->ls == LBFGS_LS_BACKTRACKING_WOLFE;
+    double a[LBK_TRIALS_NC];
+    int nc = 1;
+    a[0] = alpha;
+    if (!want_dphi) {
+        const double ratio = c->ls == LBFGS_LS_BACKTRACKING ? c->K.backtracking_alpha : 0.5;
+        nc = LBK_TRIALS_NC;
+        for (int j = 1; j < nc; ++j) a[j] = a[j - 1] * ratio;
+    }
+    /* d: the buffer once materialised; -g formed on the fly (one rank); the last second-loop
+     * update formed on the fly for this iteration's first two trial passes, then materialised
+     * (3 vector reads per pass against 4 once for k_last + 2 per pass) */
+    int dm = LBK_D_BUF;
+    if (!c->d_ready) {
+        if (c->dmode == LBK_D_NEG_G && c->geo->world == 1) {
+            dm = LBK_D_NEG_G;
+        } else if (c->dmode == LBK_D_TWOLOOP && c->trial_passes < 2) {
+            dm = LBK_D_TWOLOOP;
+        } else {
+            int rc = materialize_d(c);
+            if (rc) return rc;
+        }
+    }
+    const double* dsrc = dm == LBK_D_BUF ? c->d : dm == LBK_D_TWOLOOP ? c->rc : NULL;
+    const double* s_last = dm == LBK_D_TWOLOOP ? c->S[c->s_last_pair] : NULL;
+    DEV(lbk_trials(c->dev, c->obj, dm, c->x, dsrc, s_last, c->g, c->rho_last, c->ref_b_last, c->ref_a_last, a, nc,
+                   want_dphi, SLOT_TRIAL(c->m)));
+    double t[LBK_TRIALS_NC + 1];
+    DEVNC(lbk_fetch(c->dev, SLOT_TRIAL(c->m), nc + (want_dphi ? 1 : 0), t));
+    c->trial_passes++;
+    c->tc_n = nc;
+    for (int j = 0; j < nc; ++j) {
+        c->tc_a[j] = a[j];
+        c->tc_f[j] = t[j];
+    }
+    c->tc_dphi_ok = want_dphi;
+    c->tc_dphi = want_dphi ? t[nc] : 0.0;
+    *f = t[0];
+    if (need_g && dphi) *dphi = c->tc_dphi;
+    if (want_dphi)
+        c->trials_fg++;
+    else
+        c->trials_f++;
+    return 0;
+}
+
 static int trial(lbfgs_ctx* c, double alpha, int need_g, double* f, double* dphi) {
     if (c->spec_valid && alpha == c->a0) {
         *f = c->spec_f;
@@ -539,6 +613,7 @@ static int trial(lbfgs_ctx* c, double alpha, int need_g, double* f, double* dphi
                 return 0;
             }
     }
+    if (c->batch && !c->unfused && c->obj != LBFGS_OBJ_HOST) return trial_batched(c, alpha, need_g, f, dphi);
     int rc = materialize_d(c);
     if (rc) return rc;
     if (c->unfused) {
@@ -768,7 +843,7 @@ static int twoloop_unfused(lbfgs_ctx* c, const double* rho, double gamma) {
     return 0;
 }
 
-static int commit(lbfgs_ctx* c, int dmode, double alpha, int cslot, double* tot) {
+static int commit(lbfgs_ctx* c, int dmode, double alpha, int cslot, double* tot, double cand) {
     if (c->unfused) return commit_unfused(c, alpha, tot);
     const int pair = c->free_pair;
     const double* dsrc = dmode == LBK_D_BUF ? c->d : c->rc;
@@ -789,13 +864,19 @@ static int commit(lbfgs_ctx* c, int dmode, double alpha, int cslot, double* tot)
         if (rc) return rc;
         obj = LBK_OBJ_NONE;
         DEV(lbk_commit(c->dev, obj, dmode, c->x, dsrc, s_last, c->g, c->rho_last, c->ref_b_last,
-                       c->ref_a_last, alpha, c->xn, c->gn, c->S[pair], c->Y[pair], cslot));
+                       c->ref_a_last, alpha, c->xn, c->gn, c->S[pair], c->Y[pair], cslot, 0.0));
         DEVNC(lbk_fetch(c->dev, cslot, 7, tot));
         tot[LBK_C_F] = f;
     } else {
+        const int with_cand = cand > 0.0 && dmode != LBK_D_BUF;
         DEV(lbk_commit(c->dev, obj, dmode, c->x, dsrc, s_last, c->g, c->rho_last, c->ref_b_last,
-                       c->ref_a_last, alpha, c->xn, c->gn, c->S[pair], c->Y[pair], cslot));
-        DEVNC(lbk_fetch(c->dev, cslot, 7, tot));
+                       c->ref_a_last, alpha, c->xn, c->gn, c->S[pair], c->Y[pair], cslot, with_cand ? cand : 0.0));
+        DEVNC(lbk_fetch(c->dev, cslot, with_cand ? 8 : 7, tot));
+        if (with_cand) {
+            c->cand_valid = 1;
+            c->cand_alpha = cand;
+            c->cand_f = tot[LBK_C_FC];
+        }
     }
     c->commits++;
     return 0;
@@ -831,6 +912,9 @@ static int iterate(lbfgs_ctx* c) {
     const int small = c->obj != LBFGS_OBJ_HOST && !c->unfused && c->geo->world == 1 && lbk_small_ok(c->dev, h);
     c->d_ready = 0;
     c->spec_valid = 0;
+    c->cand_valid = 0;
+    c->tc_n = 0;
+    c->trial_passes = 0;
     host_invalidate(c);
     c->hxx_valid = 0;
     if (!(k == 0 || h == 0)) {
@@ -940,11 +1024,13 @@ static int iterate(lbfgs_ctx* c) {
             rc = materialize_d(c);
             if (rc) return rc;
         }
+        /* the backtracking search's second step, f reduced by the same pass (line_search.cpp:26) */
+        const double cand = (c->batch && c->ls == LBFGS_LS_BACKTRACKING) ? c->a0 * c->K.backtracking_alpha : 0.0;
         if (small_done) { /* the commit at a0 ran inside lbk_small_iter */
             DEVNC(lbk_fetch(c->dev, cslot, 7, tot));
             c->commits++;
         } else {
-            rc = commit(c, c->dmode, c->a0, cslot, tot);
+            rc = commit(c, c->dmode, c->a0, cslot, tot, cand);
             if (rc) return rc;
         }
         gd = tot[LBK_C_GD];
@@ -956,7 +1042,7 @@ static int iterate(lbfgs_ctx* c) {
                 rc = materialize_d(c);
                 if (rc) return rc;
             }
-            rc = commit(c, c->dmode, c->a0, cslot, tot);
+            rc = commit(c, c->dmode, c->a0, cslot, tot, cand);
             if (rc) return rc;
             gd = tot[LBK_C_GD];
         }
@@ -991,9 +1077,13 @@ static int iterate(lbfgs_ctx* c) {
 
     /* ---- commit (:159-198) ---- */
     if (!(c->spec_valid && alpha == c->a0)) {
-        rc = materialize_d(c);
-        if (rc) return rc;
-        rc = commit(c, LBK_D_BUF, alpha, cslot, tot);
+        /* batched: d may still be unmaterialised (formed on the fly again, same bits) */
+        if (!(c->batch && !c->unfused && c->obj != LBFGS_OBJ_HOST && !c->d_ready &&
+              (c->dmode == LBK_D_TWOLOOP || (c->dmode == LBK_D_NEG_G && c->geo->world == 1)))) {
+            rc = materialize_d(c);
+            if (rc) return rc;
+        }
+        rc = commit(c, c->d_ready ? LBK_D_BUF : c->dmode, alpha, cslot, tot, 0.0);
         if (rc) return rc;
     }
     c->f_cur = tot[LBK_C_F];
@@ -1149,6 +1239,9 @@ static int iterate_vf(lbfgs_ctx* c) {
     }
     c->dmode = D_VF;
     c->d_ready = 0;
+    c->cand_valid = 0;
+    c->tc_n = 0;
+    c->trial_passes = 0;
     c->gt_valid = 0;
 
     /* ---- fused first trial + commit at a0, then the line search (:156) ---- */
@@ -1277,6 +1370,11 @@ int lbfgs_solver_init(lbfgs_ctx* c, int objective, const lbfgs_host_fn* cb, int 
     c->hxx_valid = 0;
     c->cb_f = c->cb_g = 0;
     c->unfused = (flags & LBFGS_FLAG_UNFUSED) != 0;
+    c->batch = 1;
+    {
+        const char* e = getenv("LBFGS_BATCH");
+        if (e) c->batch = atoi(e) != 0;
+    }
     if (c->unfused && (objective == LBFGS_OBJ_HOST || c->geo->world != 1)) return LBFGS_ERR_BAD_ARG;
     /* ping-pong q/r (LBFGS_PINGPONG=1): measured neutral at n=1e8 and -8 % at n=1e7 (the
      * in-place passes keep q/r in the Infinity Cache), so in-place is the default */
@@ -1549,6 +1647,14 @@ int lbfgs_line_search(lbfgs_ctx* c, int objective, const lbfgs_host_fn* cb, int 
     c->cb_f = c->cb_g = 0;
     c->inited = 0;
     c->unfused = 0;
+    c->batch = 1;
+    {
+        const char* e = getenv("LBFGS_BATCH");
+        if (e) c->batch = atoi(e) != 0;
+    }
+    c->cand_valid = 0;
+    c->tc_n = 0;
+    c->trial_passes = 0;
     c->obj = objective;
     c->ls = line_search;
     if (k)

@@ -877,6 +877,43 @@ __device__ __forceinline__ double halo_z(const double* __restrict__ x, const Dir
     return zh;
 }
 
+// (x, d) at the halo element of lane 0 (i-1) / lane 63 (i+2), or zeros: every step's halo
+// z = x + a d from one read (the batched trials and the commit's candidate step); the same
+// operands and operations as halo_z
+template <int OBJ, int DMODE>
+__device__ __forceinline__ double2 halo_xd(const double* __restrict__ x, const DirArgs& da, int64_t i, int64_t n_loc) {
+    double2 xd = make_double2(0.0, 0.0);
+    if (needs_halo<OBJ>()) {
+        const int lane = threadIdx.x & 63;
+        if (lane == 0 || lane == 63) {
+            const int64_t hi = (lane == 0) ? i - 1 : i + 2;
+            if (hi >= -1 && hi <= n_loc) {
+                double dh;
+                if (DMODE == LBK_D_BUF && da.ghost && (hi == -1 || hi == n_loc))
+                    dh = ghost_d(da, hi, n_loc);
+                else if (DMODE == LBK_D_TWOLOOP && da.ghost && (hi == -1 || hi == n_loc))
+                    dh = -(ghost_d(da, hi, n_loc) + da.s[hi] * da.coef);
+                else
+                    dh = load_dir1<DMODE>(da, hi);
+                xd = make_double2(x[hi], dh);
+            }
+        }
+    }
+    return xd;
+}
+
+// f terms of the two elements of a lane at z (right neighbour from the row, lane 63's from zh)
+template <int OBJ, bool MASK>
+__device__ __forceinline__ void objective_f_pair(double2 z, double zh, int64_t e0, int64_t n, bool v0, bool v1,
+                                                 double& facc) {
+    const int lane = threadIdx.x & 63;
+    const double dn = __shfl_down(z.x, 1, 64);
+    const double zr = (lane == 63) ? zh : dn;
+    const bool p0 = e0 + 1 < n, p1 = e0 + 2 < n;
+    if ((!MASK || v0) && obj_has_term<OBJ>(p0)) facc = facc + obj_term<OBJ>(z.x, z.y, p0);
+    if ((!MASK || v1) && obj_has_term<OBJ>(p1)) facc = facc + obj_term<OBJ>(z.y, zr, p1);
+}
+
 // f terms and gradient of the two elements of a lane at z (neighbours from the row)
 template <int OBJ, bool MASK>
 __device__ __forceinline__ double2 objective_pair(double2 z, double zh, int64_t e0, int64_t n, bool v0, bool v1,
@@ -938,8 +975,11 @@ __global__ __launch_bounds__(LB_BLOCK) void k_objective(const double* __restrict
 // The commit: d per DMODE, x_new = x + alpha d, f(x_new), g_new = grad f(x_new) (or read
 // from gn for OBJ == NONE), s = x_new - x, y = g_new - g, and the dots
 //   [GD] g.d  [F] f  [SY] s.y  [YY] y.y  [GG] g_new.g_new  [SG] s.g_new  [DPHI] g_new.d
-template <int OBJ, int DMODE, bool NT>
+// CAND: also f(x + cand d) at the line search's next backtracking step [FC] (no extra bytes:
+// x and d are in registers), so a rejected first step needs no trial pass for the second.
+template <int OBJ, int DMODE, bool NT, bool CAND = false>
 struct OpCommit {
+    static constexpr int K = CAND ? 8 : 7;
     const double* __restrict__ x;
     DirArgs da;
     double alpha;
@@ -948,9 +988,10 @@ struct OpCommit {
     double* __restrict__ so;
     double* __restrict__ yo;
     int64_t n, n_loc;
+    double cand;
     struct Row {
         double2 x, g, d, z, gx;
-        double zh;
+        double zh, zch;
     };
     __device__ void load(Row& r, int64_t i) const {
         r.x = ldx<NT>(x + i);
@@ -959,10 +1000,22 @@ struct OpCommit {
         if (OBJ == LBK_OBJ_NONE) r.gx = ldv<NT>(gn + i);
         r.z.x = r.x.x + alpha * r.d.x;
         r.z.y = r.x.y + alpha * r.d.y;
-        r.zh = (OBJ == LBK_OBJ_NONE) ? 0.0 : halo_z<OBJ, false, DMODE>(x, da, alpha, i, n_loc);
+        if (CAND) {
+            const double2 xd = halo_xd<OBJ, DMODE>(x, da, i, n_loc);
+            r.zh = xd.x + alpha * xd.y;
+            r.zch = xd.x + cand * xd.y;
+        } else {
+            r.zh = (OBJ == LBK_OBJ_NONE) ? 0.0 : halo_z<OBJ, false, DMODE>(x, da, alpha, i, n_loc);
+        }
     }
     template <bool MASK>
-    __device__ void apply(Row& r, int64_t i, int64_t e0, bool v0, bool v1, double (&acc)[7]) const {
+    __device__ void apply(Row& r, int64_t i, int64_t e0, bool v0, bool v1, double (&acc)[K]) const {
+        if (CAND) {
+            double2 zc;
+            zc.x = r.x.x + cand * r.d.x;
+            zc.y = r.x.y + cand * r.d.y;
+            objective_f_pair<OBJ, MASK>(zc, r.zch, e0, n, v0, v1, acc[LBK_C_FC]);
+        }
         double2 g2;
         if (OBJ == LBK_OBJ_NONE) {
             g2 = r.gx;
@@ -987,11 +1040,11 @@ struct OpCommit {
     }
 };
 
-template <int OBJ, int DMODE, bool NT>
+template <int OBJ, int DMODE, bool NT, bool CAND = false>
 __global__ __launch_bounds__(LB_BLOCK) void k_commit(const double* __restrict__ x, DirArgs da, double alpha,
                                                      double* __restrict__ xn, double* __restrict__ gn,
                                                      double* __restrict__ so, double* __restrict__ yo,
-                                                     Geo geo, Red red) {
+                                                     Geo geo, Red red, double cand = 0.0) {
     if (DMODE == LBK_D_TWOLOOP) {
         const double beta = da.rho * src_total(da.pb, geo);
         const double alph = da.rho * slot_total(da.pa);
@@ -1017,7 +1070,64 @@ __global__ __launch_bounds__(LB_BLOCK) void k_commit(const double* __restrict__ 
             so[e] = z - x[e];
         }
     }
-    run_pass<OpCommit<OBJ, DMODE, NT>, 7>(OpCommit<OBJ, DMODE, NT>{x, da, alpha, xn, gn, so, yo, geo.n, geo.n_loc}, geo, red);
+    using Op = OpCommit<OBJ, DMODE, NT, CAND>;
+    run_pass<Op, Op::K>(Op{x, da, alpha, xn, gn, so, yo, geo.n, geo.n_loc, cand}, geo, red);
+}
+
+// Batched line-search trials: f at NC steps a[0..NC-1] along d (d per DMODE: a buffer, -g, or the
+// last second-loop update -(r + s (alpha - beta)) formed on the fly, so a rejected first step
+// needs no materialised d) in one read of x and d; DPHI: also g(x + a[0] d) . d (the Wolfe
+// curvature term) from the same pass, the gradient never stored. Components: f_0..f_{NC-1}
+// [, dphi_0]. Every f is summed in the order of a single-step evaluation (same bits).
+template <int OBJ, int DMODE, int NC, bool DPHI, bool NT>
+struct OpTrials {
+    static constexpr int K = NC + (DPHI ? 1 : 0);
+    const double* __restrict__ x;
+    DirArgs da;
+    double a[NC];
+    int64_t n, n_loc;
+    struct Row {
+        double2 x, d;
+        double xh, dh;
+    };
+    __device__ void load(Row& r, int64_t i) const {
+        r.x = ldx<NT>(x + i);
+        double2 gv = make_double2(0.0, 0.0);
+        if (DMODE == LBK_D_NEG_G) gv = ldx<NT>(da.g + i);
+        r.d = load_dir<DMODE, NT>(da, i, gv);
+        const double2 xd = halo_xd<OBJ, DMODE>(x, da, i, n_loc);
+        r.xh = xd.x;
+        r.dh = xd.y;
+    }
+    template <bool MASK>
+    __device__ void apply(Row& r, int64_t, int64_t e0, bool v0, bool v1, double (&acc)[K]) const {
+#pragma unroll
+        for (int j = 0; j < NC; ++j) {
+            double2 z;
+            z.x = r.x.x + a[j] * r.d.x;
+            z.y = r.x.y + a[j] * r.d.y;
+            const double zh = r.xh + a[j] * r.dh;
+            if (DPHI && j == 0) {
+                const double2 g = objective_pair<OBJ, MASK>(z, zh, e0, n, v0, v1, acc[0], true);
+                acc[NC] = fma2<MASK>(g, r.d, acc[NC], v0, v1);
+            } else {
+                objective_f_pair<OBJ, MASK>(z, zh, e0, n, v0, v1, acc[j]);
+            }
+        }
+    }
+};
+
+template <int OBJ, int DMODE, int NC, bool DPHI, bool NT>
+__global__ __launch_bounds__(LB_BLOCK) void k_trials(const double* __restrict__ x, DirArgs da, Geo geo, Red red,
+                                                     OpTrials<OBJ, DMODE, NC, DPHI, NT> op) {
+    if (DMODE == LBK_D_TWOLOOP) {
+        const double beta = da.rho * src_total(da.pb, geo);
+        const double alph = da.rho * slot_total(da.pa);
+        op.da.coef = alph - beta;
+    }
+    run_pass<OpTrials<OBJ, DMODE, NC, DPHI, NT>, OpTrials<OBJ, DMODE, NC, DPHI, NT>::K>(op, geo, red);
+    (void)x;
+    (void)da;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -2099,6 +2209,7 @@ int launch(lbk_ctx* c, int kind, double vec_passes, int slot, F&& fn, int K = 1,
             case 1: hipLaunchKernelGGL(k_group_reduce<1>, grid, blk, 0, c->stream, c->partials, g, sl, hs, ks); break;
             case 2: hipLaunchKernelGGL(k_group_reduce<2>, grid, blk, 0, c->stream, c->partials, g, sl, hs, ks); break;
             case 7: hipLaunchKernelGGL(k_group_reduce<7>, grid, blk, 0, c->stream, c->partials, g, sl, hs, ks); break;
+            case 8: hipLaunchKernelGGL(k_group_reduce<8>, grid, blk, 0, c->stream, c->partials, g, sl, hs, ks); break;
             default:
                 hipLaunchKernelGGL(k_group_reduce_wide, dim3(c->geo.g_hi - c->geo.g_lo, (K + 7) / 8), blk, 0, c->stream,
                                    c->partials, g, sl, hs, K, ks);
@@ -2576,9 +2687,12 @@ int lbk_trial(lbk_ctx* c, int obj, const double* x, const double* d, double alph
 
 int lbk_commit(lbk_ctx* c, int obj, int dmode, const double* x, const double* dsrc, const double* s_last,
                const double* gg, double rho, int ref_beta, int ref_alpha, double alpha, double* xn, double* gn,
-               double* s_out, double* y_out, int slot) {
+               double* s_out, double* y_out, int slot, double cand) {
     Geo g = kgeo(c);
-    Red r = kred(c, slot, 7);
+    // the candidate step rides the first (speculative) commit of the direction modes
+    const bool with_cand = cand > 0.0 && obj != LBK_OBJ_NONE && dmode != LBK_D_BUF;
+    const int K = with_cand ? 8 : 7;
+    Red r = kred(c, slot, K);
     DirArgs da = {dsrc, s_last, gg, 0.0, nullptr, nullptr, rho,
                   (dmode == LBK_D_BUF || dmode == LBK_D_TWOLOOP) ? ghost_ptr(c) : nullptr, c->geo.g_lo, c->geo.g_hi};
     if (dmode == LBK_D_TWOLOOP) {
@@ -2587,6 +2701,16 @@ int lbk_commit(lbk_ctx* c, int obj, int dmode, const double* x, const double* ds
         g.ppart = take_pending(c, ref_beta);
     }
     double passes = 4.0 + (dmode == LBK_D_BUF ? 3.0 : dmode == LBK_D_NEG_G ? 2.0 : 4.0);
+    if (with_cand) {
+        return launch(c, LBK_K_COMMIT, passes, slot, [&] {
+            if (dmode == LBK_D_NEG_G) {
+                OBJ_DISPATCH(obj, hipLaunchKernelGGL((k_commit<O_, LBK_D_NEG_G, NT_, true>), dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, x, da, alpha, xn, gn, s_out, y_out, g, r, cand));
+            } else {
+                OBJ_DISPATCH(obj, hipLaunchKernelGGL((k_commit<O_, LBK_D_TWOLOOP, NT_, true>), dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, x, da, alpha, xn, gn, s_out, y_out, g, r, cand));
+            }
+            return 0;
+        }, 8);
+    }
     return launch(c, LBK_K_COMMIT, passes, slot, [&] {
         if (obj == LBK_OBJ_NONE) {
             NT_DISPATCH(c, switch (dmode) {
@@ -2609,6 +2733,52 @@ int lbk_commit(lbk_ctx* c, int obj, int dmode, const double* x, const double* ds
         }
         return 0;
     }, 7);
+}
+
+int lbk_trials(lbk_ctx* c, int obj, int dmode, const double* x, const double* dsrc, const double* s_last,
+               const double* gg, double rho, int ref_beta, int ref_alpha, const double* alphas, int nc, int dphi,
+               int slot) {
+    if (!((nc == 1 && dphi) || (nc == LBK_TRIALS_NC && !dphi) || (nc == 1 && !dphi)) || obj == LBK_OBJ_NONE) {
+        snprintf(c->err, sizeof c->err, "lbk_trials: nc=%d dphi=%d obj=%d", nc, dphi, obj);
+        return -1;
+    }
+    Geo g = kgeo(c);
+    const int K = nc + (dphi ? 1 : 0);
+    Red r = kred(c, slot, K);
+    DirArgs da = {dsrc, s_last, gg, 0.0, nullptr, nullptr, rho,
+                  (dmode == LBK_D_BUF || dmode == LBK_D_TWOLOOP) ? ghost_ptr(c) : nullptr, c->geo.g_lo, c->geo.g_hi};
+    if (dmode == LBK_D_TWOLOOP) {
+        da.pa = sref(c, ref_alpha);
+        da.pb = sref(c, ref_beta);
+        g.ppart = take_pending(c, ref_beta);
+    }
+    const double passes = dmode == LBK_D_TWOLOOP ? 3.0 : 2.0;
+    const int kind = dphi ? LBK_K_TRIAL_FG : LBK_K_TRIAL_F;
+#define TRIALS_LAUNCH(DM, NCC, DP)                                                                             \
+    OBJ_DISPATCH(obj, {                                                                                    \
+        OpTrials<O_, DM, NCC, DP, NT_> op{x, da, {}, c->geo.n, c->geo.n_loc};                               \
+        for (int j = 0; j < NCC; ++j) op.a[j] = alphas[j];                                                   \
+        hipLaunchKernelGGL((k_trials<O_, DM, NCC, DP, NT_>), dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, x, \
+                           da, g, r, op);                                                                  \
+    })
+#define TRIALS_DM(DM)                                                   \
+    if (nc == 1 && dphi) {                                              \
+        TRIALS_LAUNCH(DM, 1, true);                                     \
+    } else if (nc == 1) {                                               \
+        TRIALS_LAUNCH(DM, 1, false);                                    \
+    } else {                                                            \
+        TRIALS_LAUNCH(DM, LBK_TRIALS_NC, false);                        \
+    }
+    return launch(c, kind, passes, slot, [&] {
+        switch (dmode) {
+            case LBK_D_BUF: TRIALS_DM(LBK_D_BUF) break;
+            case LBK_D_NEG_G: TRIALS_DM(LBK_D_NEG_G) break;
+            default: TRIALS_DM(LBK_D_TWOLOOP) break;
+        }
+        return 0;
+    }, K);
+#undef TRIALS_DM
+#undef TRIALS_LAUNCH
 }
 
 int lbk_point(lbk_ctx* c, double* z, const double* x, const double* d, double alpha) {
