@@ -1,0 +1,82 @@
+#!/usr/bin/env python3
+"""BASELINE configs[3] in detail: tridiagonal quadratic (generate_quadratic_*) n = 1e8, m = 20,
+Wolfe line search, solved from x0 ~ U(-2, 2) (seed 42) to |g| < 1e-5 on one GPU, with the
+batched line-search trials on (default) and off (LBFGS_BATCH=0).
+
+Per mode: time to solution with x0 already resident (the context is initialised - x0 uploaded,
+f and g evaluated - before the clock starts), iterations, device passes and passes per
+iteration, trial passes, algorithmic bytes, and from a second (event-timed) solve the per-kernel
+time and the roofline of the dominant kernel (algorithmic bytes per launch / mean launch time).
+
+usage: python tools/config3.py [out.json] [--n N]
+"""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "cuda-lbfgs_amd"))
+import lbfgs_amd as L  # noqa: E402
+
+L.lib()
+HBM_PEAK_GBPS = 8000.0
+
+
+def solve(n, m, batch, prof):
+    os.environ["LBFGS_BATCH"] = "1" if batch else "0"
+    x0 = L.x0_uniform(n, 42, -2.0, 2.0)
+    with L.Context(n, m) as c:
+        c.init("quad_tridiag", x0, "wolfe", tolerance=1e-5)
+        c.sync()
+        if prof:
+            c.prof_reset()
+            c.prof_enable(True)
+        t0 = time.perf_counter()
+        r = c.step(1000)
+        c.sync()
+        dt = time.perf_counter() - t0
+        kern = {}
+        if prof:
+            for k in L.KERNELS:
+                p = c.prof_get(k)
+                if p["launches"]:
+                    kern[k] = p
+    out = dict(seconds=dt, iterations=r["iterations"], status=r["status"], f=r["f"], gnorm=r["gnorm"],
+               passes=r["passes"], passes_per_iter=r["passes"] / max(r["iterations"], 1),
+               trials_f=r["trials_f"], trials_fg=r["trials_fg"], commits=r["commits"], bytes=r["bytes"],
+               gbps=r["bytes"] / dt / 1e9, h_max=r["h_max"])
+    if prof:
+        tot = sum(v["ms"] for v in kern.values())
+        dom = max(kern, key=lambda k: kern[k]["ms"])
+        v = kern[dom]
+        bpl = v["bytes"] / v["launches"]
+        us = 1e3 * v["ms"] / v["launches"]
+        out["kernels"] = {k: dict(ms=round(v["ms"], 4), launches=v["launches"],
+                                  share=round(v["ms"] / tot, 4)) for k, v in kern.items()}
+        out["roofline"] = dict(bound="hbm", kernel=dom, achieved=round(bpl / us / 1e3, 1), peak=HBM_PEAK_GBPS,
+                               unit="GB/s", frac=round(bpl / us / 1e3 / HBM_PEAK_GBPS, 4),
+                               bytes_per_launch=bpl, avg_launch_us=round(us, 2), launches=v["launches"])
+    return out
+
+
+def main():
+    n = int(float(sys.argv[sys.argv.index("--n") + 1])) if "--n" in sys.argv else 10**8
+    outp = sys.argv[1] if len(sys.argv) > 1 and not sys.argv[1].startswith("--") else None
+    res = dict(config="configs[3]: quad_tridiag n=%d m=20 wolfe, tol 1e-5, x0 ~ U(-2,2) seed 42" % n)
+    for batch in (1, 0):
+        key = "batched" if batch else "one_pass_per_step"
+        solve(n, 20, batch, False)  # warm-up (first-touch, code objects)
+        res[key] = solve(n, 20, batch, False)
+        res[key]["profiled"] = solve(n, 20, batch, True)
+        print(key, json.dumps(res[key]), flush=True)
+    b, u = res["batched"], res["one_pass_per_step"]
+    res["speedup_batched"] = u["seconds"] / b["seconds"]
+    print(json.dumps(dict(speedup=res["speedup_batched"])))
+    if outp:
+        with open(outp, "w") as fp:
+            json.dump(res, fp, indent=1)
+
+
+if __name__ == "__main__":
+    main()
