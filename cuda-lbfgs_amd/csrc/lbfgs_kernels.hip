@@ -531,6 +531,79 @@ __device__ __forceinline__ void stream(const Op& op, const Seg& s, const Geo& ge
     }
 }
 
+// Stencil passes (the commit and the trials of the Rosenbrock / tridiagonal objectives need z
+// at each row's outer neighbours): over a full segment the waves step through 16 rows at a time
+// - wave w takes rows 16k + 4j + w, j = 0..3, which is the canonical visiting order (u = 4k + j)
+// - and publish the (x, d) of their rows' first and last elements in LDS, so a row's halo comes
+// from the neighbouring wave's registers instead of a second read of x and d (4.23 -> ~4.0
+// vector reads per commit launch at n = 1e8). Only the segment's first row's left halo and each
+// step's last row's right halo are read from memory. One barrier per step; the LDS edge table is
+// double-buffered and the previous step's carry is read before the barrier, so a wave running a
+// step ahead never overwrites what a slower one still reads.
+template <int K, class Op>
+__device__ __forceinline__ void stream_stencil(const Op& op, const Seg& s, double (&acc)[K]) {
+    __shared__ double2 E[2][16][2];
+    const int nrow = (int)(s.len >> 7);  // full segment: a whole number of rows
+    const int nsteps = (nrow + 15) >> 4;
+    const bool l0 = s.lane == 0, l63 = s.lane == 63;
+    for (int k = 0; k < nsteps; ++k) {
+        const int buf = k & 1;
+        typename Op::Row r[4];
+        double2 hmem[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int row = 16 * k + 4 * j + s.w;
+            if (row < nrow) {
+                const int64_t i = s.lb + (int64_t)row * 128 + 2 * s.lane;
+                op.load_core(r[j], i);
+                // memory halos: the segment's first row (left), a step's last row (right)
+                hmem[j] = make_double2(0.0, 0.0);
+                if (l0 && row == 0) hmem[j] = op.halo_mem(i - 1);
+                if (l63 && (4 * j + s.w == 15 || row + 1 == nrow)) hmem[j] = op.halo_mem(i + 2);
+            }
+        }
+        double2 carry = make_double2(0.0, 0.0);
+        if (k > 0 && s.w == 0 && l0) carry = E[buf ^ 1][15][1];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int row = 16 * k + 4 * j + s.w;
+            if (row < nrow) {
+                if (l0) E[buf][4 * j + s.w][0] = op.edge_first(r[j]);
+                if (l63) E[buf][4 * j + s.w][1] = op.edge_last(r[j]);
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int rr = 4 * j + s.w, row = 16 * k + rr;
+            if (row < nrow) {
+                double2 h = hmem[j];
+                if (l0 && row > 0) h = rr > 0 ? E[buf][rr - 1][1] : carry;
+                if (l63 && rr < 15 && row + 1 < nrow) h = E[buf][rr + 1][0];
+                op.set_halo(r[j], h);
+                const int64_t o = (int64_t)row * 128 + 2 * s.lane;
+                op.template apply<false>(r[j], s.lb + o, s.sbeg + o, true, true, acc);
+            }
+        }
+    }
+}
+
+#ifndef LBK_LDS_HALO
+#define LBK_LDS_HALO 1
+#endif
+
+// stencil ops over full segments exchange row halos through LDS; everything else streams
+template <int K, class Op>
+__device__ __forceinline__ void stream_halo(const Op& op, const Seg& s, const Geo& geo, double (&acc)[K]) {
+    if constexpr (LBK_LDS_HALO && Op::kStencil) {
+        if (s.len == geo.L) {
+            stream_stencil(op, s, acc);
+            return;
+        }
+    }
+    stream(op, s, geo, acc);
+}
+
 template <bool MASK, bool NT>
 __device__ __forceinline__ void st2(double* p, double2 v, bool v0, bool v1) {
     if (!MASK || (v0 && v1))
@@ -736,6 +809,16 @@ __device__ __forceinline__ void run_pass(const Op& op, const Geo& geo, const Red
     reduce_publish<K>(acc, geo, red);
 }
 
+template <class Op, int K>
+__device__ __forceinline__ void run_pass_halo(const Op& op, const Geo& geo, const Red& red) {
+    const Seg s = seg_setup(geo);
+    double acc[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) acc[k] = 0.0;
+    stream_halo(op, s, geo, acc);
+    reduce_publish<K>(acc, geo, red);
+}
+
 template <bool NT>
 __global__ __launch_bounds__(LB_BLOCK) void k_dot(const double* __restrict__ a, const double* __restrict__ b,
                                                   Geo geo, Red red) {
@@ -877,6 +960,20 @@ __device__ __forceinline__ double halo_z(const double* __restrict__ x, const Dir
     return zh;
 }
 
+// (x, d) at local element hi (-1 <= hi <= n_loc; zeros outside), d per DMODE: halo operands
+template <int DMODE>
+__device__ __forceinline__ double2 xd_at(const double* __restrict__ x, const DirArgs& da, int64_t hi, int64_t n_loc) {
+    if (hi < -1 || hi > n_loc) return make_double2(0.0, 0.0);
+    double dh;
+    if (DMODE == LBK_D_BUF && da.ghost && (hi == -1 || hi == n_loc))
+        dh = ghost_d(da, hi, n_loc);
+    else if (DMODE == LBK_D_TWOLOOP && da.ghost && (hi == -1 || hi == n_loc))
+        dh = -(ghost_d(da, hi, n_loc) + da.s[hi] * da.coef);
+    else
+        dh = load_dir1<DMODE>(da, hi);
+    return make_double2(x[hi], dh);
+}
+
 // (x, d) at the halo element of lane 0 (i-1) / lane 63 (i+2), or zeros: every step's halo
 // z = x + a d from one read (the batched trials and the commit's candidate step); the same
 // operands and operations as halo_z
@@ -993,6 +1090,22 @@ struct OpCommit {
         double2 x, g, d, z, gx;
         double zh, zch;
     };
+    static constexpr bool kStencil = OBJ != LBK_OBJ_NONE && (OBJ == LBK_OBJ_ROSENBROCK || OBJ == LBK_OBJ_QUAD_TRIDIAG);
+    __device__ void load_core(Row& r, int64_t i) const {
+        r.x = ldx<NT>(x + i);
+        r.g = ldx<NT>(da.g + i);
+        r.d = load_dir<DMODE, NT>(da, i, r.g);
+        if (OBJ == LBK_OBJ_NONE) r.gx = ldv<NT>(gn + i);
+        r.z.x = r.x.x + alpha * r.d.x;
+        r.z.y = r.x.y + alpha * r.d.y;
+    }
+    __device__ double2 halo_mem(int64_t hi) const { return xd_at<DMODE>(x, da, hi, n_loc); }
+    __device__ double2 edge_first(const Row& r) const { return make_double2(r.x.x, r.d.x); }
+    __device__ double2 edge_last(const Row& r) const { return make_double2(r.x.y, r.d.y); }
+    __device__ void set_halo(Row& r, double2 xd) const {
+        r.zh = xd.x + alpha * xd.y;
+        if (CAND) r.zch = xd.x + cand * xd.y;
+    }
     __device__ void load(Row& r, int64_t i) const {
         r.x = ldx<NT>(x + i);
         r.g = ldx<NT>(da.g + i);
@@ -1071,7 +1184,7 @@ __global__ __launch_bounds__(LB_BLOCK) void k_commit(const double* __restrict__ 
         }
     }
     using Op = OpCommit<OBJ, DMODE, NT, CAND>;
-    run_pass<Op, Op::K>(Op{x, da, alpha, xn, gn, so, yo, geo.n, geo.n_loc, cand}, geo, red);
+    run_pass_halo<Op, Op::K>(Op{x, da, alpha, xn, gn, so, yo, geo.n, geo.n_loc, cand}, geo, red);
 }
 
 // Batched line-search trials: f at NC steps a[0..NC-1] along d (d per DMODE: a buffer, -g, or the
@@ -1090,11 +1203,22 @@ struct OpTrials {
         double2 x, d;
         double xh, dh;
     };
-    __device__ void load(Row& r, int64_t i) const {
+    static constexpr bool kStencil = OBJ == LBK_OBJ_ROSENBROCK || OBJ == LBK_OBJ_QUAD_TRIDIAG;
+    __device__ void load_core(Row& r, int64_t i) const {
         r.x = ldx<NT>(x + i);
         double2 gv = make_double2(0.0, 0.0);
         if (DMODE == LBK_D_NEG_G) gv = ldx<NT>(da.g + i);
         r.d = load_dir<DMODE, NT>(da, i, gv);
+    }
+    __device__ double2 halo_mem(int64_t hi) const { return xd_at<DMODE>(x, da, hi, n_loc); }
+    __device__ double2 edge_first(const Row& r) const { return make_double2(r.x.x, r.d.x); }
+    __device__ double2 edge_last(const Row& r) const { return make_double2(r.x.y, r.d.y); }
+    __device__ void set_halo(Row& r, double2 xd) const {
+        r.xh = xd.x;
+        r.dh = xd.y;
+    }
+    __device__ void load(Row& r, int64_t i) const {
+        load_core(r, i);
         const double2 xd = halo_xd<OBJ, DMODE>(x, da, i, n_loc);
         r.xh = xd.x;
         r.dh = xd.y;
@@ -1125,7 +1249,7 @@ __global__ __launch_bounds__(LB_BLOCK) void k_trials(const double* __restrict__ 
         const double alph = da.rho * slot_total(da.pa);
         op.da.coef = alph - beta;
     }
-    run_pass<OpTrials<OBJ, DMODE, NC, DPHI, NT>, OpTrials<OBJ, DMODE, NC, DPHI, NT>::K>(op, geo, red);
+    run_pass_halo<OpTrials<OBJ, DMODE, NC, DPHI, NT>, OpTrials<OBJ, DMODE, NC, DPHI, NT>::K>(op, geo, red);
     (void)x;
     (void)da;
 }

@@ -9,9 +9,22 @@ read bytes are 2 * FETCH_SIZE * 1024; WRITE_SIZE is exact for 16-B streaming sto
 """
 import collections
 import csv
+import glob
 import json
+import os
 import re
 import sys
+
+
+def find(d, name):
+    """d/name, or the one file of that name below d (rocprofv3 adds host / pid levels)"""
+    p = os.path.join(d, name)
+    if os.path.exists(p):
+        return p
+    hits = sorted(glob.glob(os.path.join(d, "**", name), recursive=True))
+    if not hits:
+        raise FileNotFoundError(p)
+    return hits[-1]
 
 
 def short(name):
@@ -23,14 +36,14 @@ def short(name):
 
 def main(trace_dir, fetch_dir, write_dir, out, n=None):
     res = collections.OrderedDict()
-    for r in csv.DictReader(open(f"{trace_dir}/run_kernel_stats.csv")):
+    for r in csv.DictReader(open(find(trace_dir, "run_kernel_stats.csv"))):
         k = short(r["Name"])
         res.setdefault(k, {})
         res[k].update(calls=int(r["Calls"]), avg_us=float(r["AverageNs"]) / 1e3,
                       total_pct=float(r["Percentage"]))
     for tag, d in [("FETCH_SIZE", fetch_dir), ("WRITE_SIZE", write_dir)]:
         agg = collections.defaultdict(list)
-        for r in csv.DictReader(open(f"{d}/run_counter_collection.csv")):
+        for r in csv.DictReader(open(find(d, "run_counter_collection.csv"))):
             agg[short(r["Kernel_Name"])].append(float(r["Counter_Value"]))
         for k, v in agg.items():
             res.setdefault(k, {})[tag + "_KiB"] = sum(v) / len(v)
