@@ -192,7 +192,36 @@ void orc_canon_dot_groups(const double* a, const double* b, int64_t n, double* q
     canon_groups(a, b, n, n, 0, q8);
 }
 
+/* ORC_PAIR / ORC_REV / ORC_FMA: other legitimate summation orders of the same products / terms
+ * (recursive pairwise halving with 8-term sequential leaves; strictly right to left; left to
+ * right with the products fused into the additions, as an FMA-contracting build). Not a
+ * device order: they measure how long the reference agrees with ITSELF when only the order of
+ * its sums changes (tests/test_oracle_horizons.py), the yardstick for the canonical order's
+ * horizon against the reference. */
+static double pair_sum(const double* a, const double* b, int64_t lo, int64_t hi) {
+    if (hi - lo <= 8) {
+        double s = 0.0;
+        for (int64_t i = lo; i < hi; ++i) s += b ? a[i] * b[i] : a[i];
+        return s;
+    }
+    const int64_t mid = lo + (hi - lo) / 2;
+    return pair_sum(a, b, lo, mid) + pair_sum(a, b, mid, hi);
+}
+
+static double alt_sum(const double* a, const double* b, int64_t limit, int mode) {
+    if (mode == ORC_PAIR) return pair_sum(a, b, 0, limit);
+    if (mode == ORC_FMA) { /* left to right, products contracted (the reference built with FMA) */
+        double s = 0.0;
+        for (int64_t i = 0; i < limit; ++i) s = b ? fma(a[i], b[i], s) : s + a[i];
+        return s;
+    }
+    double s = 0.0;
+    for (int64_t i = limit - 1; i >= 0; --i) s += b ? a[i] * b[i] : a[i];
+    return s;
+}
+
 double orc_dot(const double* a, const double* b, int64_t n, int mode) {
+    if (mode == ORC_PAIR || mode == ORC_REV || mode == ORC_FMA) return alt_sum(a, b, n, mode);
     if (mode == ORC_CANON || mode == ORC_CANON_VF) {
         double q8[CANON_GROUPS];
         canon_groups_mode(a, b, n, n, 0, mode == ORC_CANON_VF, q8);
@@ -204,6 +233,7 @@ double orc_dot(const double* a, const double* b, int64_t n, int mode) {
 }
 
 double orc_sum(const double* t, int64_t n, int64_t limit, int mode) {
+    if (mode == ORC_PAIR || mode == ORC_REV || mode == ORC_FMA) return alt_sum(t, NULL, limit, mode);
     if (mode == ORC_CANON || mode == ORC_CANON_VF) {
         double q8[CANON_GROUPS];
         canon_groups_mode(t, NULL, n, limit, 1, mode == ORC_CANON_VF, q8);
@@ -215,7 +245,7 @@ double orc_sum(const double* t, int64_t n, int64_t limit, int mode) {
 }
 
 static double orc_norm(const double* v, int64_t n, int mode) {
-    if (mode == ORC_CANON) return sqrt(orc_dot(v, v, n, mode));
+    if (mode == ORC_CANON || mode == ORC_PAIR || mode == ORC_REV || mode == ORC_FMA) return sqrt(orc_dot(v, v, n, mode));
     double r = 0.; /* vector_utils.cpp:80-85 */
     for (int64_t i = 0; i < n; ++i) r += v[i] * v[i];
     return sqrt(r);

@@ -24,7 +24,9 @@ extern "C" {
  * std::function objective, lbfgs.h:9-10); used with the dense quadratics of matrices.h */
 enum { ORC_OBJ_ROSENBROCK = 0, ORC_OBJ_QUAD_TRIDIAG = 1, ORC_OBJ_QUAD_SEPARABLE = 2, ORC_OBJ_HOST = 3 };
 enum { ORC_LS_BACKTRACKING = 0, ORC_LS_INTERPOLATION = 1, ORC_LS_WOLFE = 2, ORC_LS_BACKTRACKING_WOLFE = 3 };
-enum { ORC_SEQ = 0, ORC_CANON = 1, ORC_CANON_VF = 2 /* contiguous rows per wave */ };
+enum { ORC_SEQ = 0, ORC_CANON = 1, ORC_CANON_VF = 2 /* contiguous rows per wave */,
+       ORC_PAIR = 3 /* pairwise sums */, ORC_REV = 4 /* right-to-left sums */,
+       ORC_FMA = 5 /* left-to-right, products fused */ };
 enum { ORC_CONVERGED = 0, ORC_MAX_ITER = 1, ORC_LS_FAILED = 2 };
 
 typedef struct {

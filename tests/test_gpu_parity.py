@@ -10,6 +10,7 @@ Contract:
     order (no parallel reduction order can reproduce a left-to-right sum), and ends in the
     same outcome.
 """
+import json
 import os
 import sys
 
@@ -174,6 +175,16 @@ HORIZON = {"qsep_main": (2, 2), "qtri_n1e4_m10_bt": (10, 10), "qtri_n1e4_m20_wol
            "rosen_n4097_m7_interp": (61, 38)}
 
 
+HORIZONS = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "horizons.json")))
+
+
+def _horizon(a, b, tol=1e-10):
+    k = min(len(a), len(b))
+    r = np.abs(a[:k] - b[:k]) / np.maximum(np.abs(b[:k]), 1e-300)
+    bad = np.nonzero(r > tol)[0]
+    return int(bad[0]) if len(bad) else int(k)
+
+
 @pytest.mark.parametrize("name", O.golden_cases())
 def test_trajectory_vs_reference_golden(name):
     meta, g = O.load_golden(name)
@@ -196,6 +207,10 @@ def test_trajectory_vs_reference_golden(name):
     rel_g = np.abs(r["tr_gnorm"][:Kg] - ref_g[:Kg]) / np.maximum(np.abs(ref_g[:Kg]), 1e-300)
     assert np.all(rel_f <= 1e-10), (int(np.argmax(rel_f)), float(rel_f.max()))
     assert np.all(rel_g <= 1e-10), (int(np.argmax(rel_g)), float(rel_g.max()))
+    # the device run's own horizon is at least the reference's against itself under another
+    # summation order (K_ref, tests/golden/horizons.json, tests/test_oracle_horizons.py)
+    kf, kg = HORIZONS[name]["ref"]
+    assert _horizon(r["tr_f"], ref_f) >= kf and _horizon(r["tr_gnorm"], ref_g) >= kg
     # same outcome as the reference run
     final = meta["stdout"].strip().splitlines()[-1]
     assert r["messages"].strip().splitlines()[-1] == final
