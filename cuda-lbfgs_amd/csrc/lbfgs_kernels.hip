@@ -2105,6 +2105,9 @@ Geo kgeo(const lbk_ctx* c) {
 // The base length is the canonical L except for LBK_MIDL_LO <= n < LBK_VFL_LO, where the
 // canonical segments are 2048 long but the vector-free commit keeps the 512-minimum length
 // (measured there: 2048-element segments cost the vector-free mode 25 %, profiles/r01/lmin_ab.txt).
+// Invariant: for every n that shards (world > 1) the base length equals the canonical L, so a
+// rank's vector-free segments cover exactly its canonical elements (vgeo inherits elem_lo /
+// n_loc from kgeo). Today n < LBK_VFL_LO never shards (lbk_geometry_plan); lbk_create checks it.
 int64_t vf_base_len(int64_t n, int64_t canon_L) {
     if (n < LBK_MIDL_LO || n >= LBK_VFL_LO) return canon_L;
     const int64_t per = (n + LBK_SEGS - 1) / LBK_SEGS;
@@ -2445,6 +2448,12 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
         *out = c;
         return -1;
     }
+    if (world > 1 && vf_base_len(n, G.L) != G.L) {  // see vf_base_len: ranks must own whole vf segments
+        snprintf(c->err, sizeof c->err, "n=%lld: vector-free base length differs from the canonical one under sharding",
+                 (long long)n);
+        *out = c;
+        return -1;
+    }
     // front pad 32 doubles: ghost at [-1] and element 0 on a 256-B boundary, so every 1-KiB
     // row load/store covers whole cache lines; back: whole rows + halo
     // non-temporal streaming of the history (the work vectors q/r/d keep the temporal policy,
@@ -2534,6 +2543,20 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
         int khz = 0;
         CK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device));
         c->wall_khz = khz > 0 ? khz : 100000.0;
+    }
+    {
+        // the cooperative iteration's grid barrier needs every workgroup resident at once: cap its
+        // segment count by what this device holds (fewer CUs, or a kernel grown past 2 per CU)
+        int cus = 0, occ = 1 << 30;
+        CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+        int o = 0;
+        CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, k_coop_iter<LBK_OBJ_ROSENBROCK>, LB_BLOCK, 0));
+        occ = std::min(occ, o);
+        CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, k_coop_iter<LBK_OBJ_QUAD_TRIDIAG>, LB_BLOCK, 0));
+        occ = std::min(occ, o);
+        CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, k_coop_iter<LBK_OBJ_QUAD_SEPARABLE>, LB_BLOCK, 0));
+        occ = std::min(occ, o);
+        c->coop_max = (int)std::min<int64_t>(c->coop_max, (int64_t)occ * cus);
     }
     CK(hipDeviceSynchronize());
 #undef CK

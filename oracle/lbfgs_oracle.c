@@ -96,7 +96,7 @@ void orc_checksum(const double* x, int64_t n, uint64_t* c1, uint64_t* c2) {
 void orc_canon_geometry(int64_t n, int64_t* seg_len, int64_t* nseg) {
     int64_t per = (n + CANON_SEGS - 1) / CANON_SEGS;
     int64_t L = ((per + 127) / 128) * 128;
-    const int64_t lmin = (n >= 65536 && n <= 2097152) ? 2048 : 512;
+    const int64_t lmin = (n >= ORC_MIDL_LO && n <= ORC_MIDL_HI) ? ORC_MIDL : 512;
     if (L < lmin) L = lmin;
     *seg_len = L;
     *nseg = (n + L - 1) / L;
@@ -133,10 +133,10 @@ static void canon_groups_mode(const double* a, const double* b, int64_t n, int64
     orc_canon_geometry(n, &L, &nseg);
     int64_t spg = CANON_SEG_PER_GROUP;
     if (contig) {
-        /* base length: the canonical L, except 65536 <= n < 262144 where the vector-free commit
-         * keeps the 512-minimum length (lbfgs_kernels.hip vf_base_len) */
+        /* base length: the canonical L, except ORC_MIDL_LO <= n < ORC_VFL_LO where the
+         * vector-free commit keeps the 512-minimum length (lbfgs_kernels.hip vf_base_len) */
         const int F = orc_vf_factor(n);
-        if (n >= 65536 && n < 262144) {
+        if (n >= ORC_MIDL_LO && n < ORC_VFL_LO) {
             const int64_t per = (n + CANON_SEGS - 1) / CANON_SEGS;
             L = ((per + 127) / 128) * 128;
             if (L < 512) L = 512;

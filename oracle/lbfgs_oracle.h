@@ -29,6 +29,14 @@ enum { ORC_SEQ = 0, ORC_CANON = 1, ORC_CANON_VF = 2 /* contiguous rows per wave 
        ORC_FMA = 5 /* left-to-right, products fused */ };
 enum { ORC_CONVERGED = 0, ORC_MAX_ITER = 1, ORC_LS_FAILED = 2 };
 
+/* the canonical geometry's size bounds (restating lbfgs_device.h LBK_MIDL*, LBK_VFL_LO): segments
+ * are at least ORC_MIDL long for ORC_MIDL_LO <= n <= ORC_MIDL_HI (512 elsewhere); the vector-free
+ * commit keeps the 512-minimum base length below ORC_VFL_LO */
+#define ORC_MIDL 2048
+#define ORC_MIDL_LO 65536
+#define ORC_MIDL_HI 2097152
+#define ORC_VFL_LO 262144
+
 typedef struct {
     int obj, ls, mode, verbose;
     int64_t n;

@@ -12,7 +12,8 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_DIR = os.path.join(ROOT, "oracle")
-ORACLE_SO = os.path.join(ORACLE_DIR, "_build", "liboracle.so")
+# ORACLE_LIB: an instrumented build of the same source (tests/test_sanitize.py, ASan + UBSan)
+ORACLE_SO = os.environ.get("ORACLE_LIB") or os.path.join(ORACLE_DIR, "_build", "liboracle.so")
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 OBJ = {"rosenbrock": 0, "quad_tridiag": 1, "quad_sep": 2, "host": 3}

@@ -1,0 +1,447 @@
+/* host_device_double.c — TEST DOUBLE, sanitizer job only (tests/sanitize/Makefile).
+ *
+ * A host-memory implementation of the device-layer interface the C driver programs against
+ * (cuda-lbfgs_amd/csrc/lbfgs_device.h), so that the driver's host logic - the line searches,
+ * the history ring, the slot references, the batched-trial caches, the host-callback call
+ * sequencing and the C++ drop-in shim - can run under AddressSanitizer / UBSan on the CPU
+ * (GPU sanitizers are not available on the MI355X pool). Every reduction is formed with the
+ * oracle's canonical-order routines (oracle/lbfgs_oracle.c, compiled into this file), so a solve
+ * through this double must reproduce the oracle's ORC_CANON trajectory bit for bit, which
+ * tests/sanitize/san_main.c checks.
+ *
+ * It is never linked into liblbfgs_hip.so, never loaded by the product, bench.py or smoke();
+ * the product path has no CPU fallback. One rank only; vector-free mode, sharding, the peer
+ * exchange and RCCL report "unsupported".
+ */
+#include "../../oracle/lbfgs_oracle.c"
+
+#include "lbfgs_device.h"
+
+#define DBL_FRONT 8
+
+struct lbk_ctx {
+    lbk_geo geo;
+    double slots[LBK_NSLOTS][LBK_GROUPS][LBK_KMAX];
+    double bytes;
+    char err[256];
+    double* scratch[6];
+};
+
+struct lbk_group {
+    int world;
+};
+
+/* ---- geometry ---- */
+int lbk_geometry_plan(int64_t n, int rank, int world, lbk_geo* out) {
+    if (n < 1 || world != 1 || rank != 0) return -1;
+    memset(out, 0, sizeof *out);
+    int64_t L, nseg;
+    orc_canon_geometry(n, &L, &nseg);
+    out->n = n;
+    out->L = L;
+    out->nseg = nseg;
+    out->seg_lo = 0;
+    out->seg_hi = nseg;
+    out->elem_lo = 0;
+    out->n_loc = n;
+    out->g_lo = 0;
+    out->g_hi = LBK_GROUPS;
+    out->rank = 0;
+    out->world = 1;
+    out->vf_f = orc_vf_factor(n);
+    return 0;
+}
+int lbk_vf_factor(int64_t n) { return orc_vf_factor(n); }
+
+int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const void* nccl_id, lbk_group* grp) {
+    (void)device;
+    *out = NULL;
+    if (world != 1 || grp || nccl_id) return -1;
+    lbk_ctx* c = (lbk_ctx*)calloc(1, sizeof *c);
+    if (!c) return -4;
+    if (lbk_geometry_plan(n, rank, world, &c->geo) != 0) {
+        free(c);
+        return -1;
+    }
+    for (int i = 0; i < 6; ++i) {
+        c->scratch[i] = (double*)calloc((size_t)n + 2, sizeof(double));
+        if (!c->scratch[i]) return -4;
+    }
+    *out = c;
+    return 0;
+}
+void lbk_destroy(lbk_ctx* c) {
+    if (!c) return;
+    for (int i = 0; i < 6; ++i) free(c->scratch[i]);
+    free(c);
+}
+const lbk_geo* lbk_geometry(const lbk_ctx* c) { return &c->geo; }
+const char* lbk_last_error(const lbk_ctx* c) { return c ? c->err : "no context"; }
+int lbk_unique_id(void* out128) {
+    (void)out128;
+    return -3;
+}
+int lbk_device_count(void) { return 0; }
+lbk_group* lbk_group_create(int world) {
+    (void)world;
+    return NULL;
+}
+void lbk_group_destroy(lbk_group* g) { free(g); }
+void lbk_set_ghost_slot(lbk_ctx* c, int slot) {
+    (void)c;
+    (void)slot;
+}
+int lbk_peer_handle(lbk_ctx* c, void* out) {
+    (void)c;
+    (void)out;
+    return -1;
+}
+int lbk_peer_connect(lbk_ctx* c, const void* h) {
+    (void)c;
+    (void)h;
+    return -1;
+}
+int lbk_peer_enable(lbk_ctx* c, int on) {
+    (void)c;
+    (void)on;
+    return -5;
+}
+int lbk_exchange_backend(const lbk_ctx* c) {
+    (void)c;
+    return 0;
+}
+int lbk_exchange_bench(lbk_ctx* c, int b, int ks, int it, double* us) {
+    (void)c, (void)b, (void)ks, (void)it, (void)us;
+    return -1;
+}
+
+/* ---- memory: ghost cells at [-1] and [n] (zero), as lbk_vec_alloc's layout ---- */
+double* lbk_vec_alloc(lbk_ctx* c) {
+    double* p = (double*)calloc((size_t)c->geo.n_loc + DBL_FRONT + 8, sizeof(double));
+    return p ? p + DBL_FRONT : NULL;
+}
+void lbk_vec_free(lbk_ctx* c, double* v) {
+    (void)c;
+    if (v) free(v - DBL_FRONT);
+}
+void* lbk_host_alloc(size_t bytes) { return malloc(bytes); }
+void lbk_host_free(void* p) { free(p); }
+int lbk_upload(lbk_ctx* c, double* dst, const double* h) {
+    memcpy(dst, h, sizeof(double) * (size_t)c->geo.n_loc);
+    return 0;
+}
+int lbk_download(lbk_ctx* c, double* h, const double* src) {
+    memcpy(h, src, sizeof(double) * (size_t)c->geo.n_loc);
+    return 0;
+}
+int lbk_copy(lbk_ctx* c, double* dst, const double* src) {
+    memcpy(dst - 1, src - 1, sizeof(double) * (size_t)(c->geo.n_loc + 2));
+    return 0;
+}
+int lbk_download_local(lbk_ctx* c, double* h, const double* src) { return lbk_download(c, h, src); }
+int lbk_upload_local(lbk_ctx* c, double* dst, const double* h) { return lbk_upload(c, dst, h); }
+int lbk_download_local_async(lbk_ctx* c, double* h, const double* src, int tag) {
+    if (tag < 0 || tag >= 4) return -1;
+    return lbk_download(c, h, src);
+}
+int lbk_upload_local_async(lbk_ctx* c, double* dst, const double* h, int tag) {
+    if (tag < 0 || tag >= 4) return -1;
+    return lbk_upload(c, dst, h);
+}
+int lbk_xfer_wait(lbk_ctx* c, int tag) {
+    (void)c;
+    return (tag < 0 || tag >= 4) ? -1 : 0;
+}
+int lbk_sync(lbk_ctx* c) {
+    (void)c;
+    return 0;
+}
+
+/* ---- slots ---- */
+static int slot_ok(lbk_ctx* c, int slot) {
+    if (slot < 0 || slot >= LBK_NSLOTS) {
+        snprintf(c->err, sizeof c->err, "double: slot %d unsupported", slot);
+        return 0;
+    }
+    return 1;
+}
+static double ref_total(lbk_ctx* c, int ref) {
+    const int s = ref / LBK_KMAX, k = ref % LBK_KMAX;
+    double t = c->slots[s][0][k];
+    for (int g = 1; g < LBK_GROUPS; ++g) t = t + c->slots[s][g][k];
+    return t;
+}
+/* component k of `slot` := canonical groups of a.b (kind 0) or of sum a[0..limit) (kind 1) */
+static void put(lbk_ctx* c, int slot, int k, const double* a, const double* b, int64_t limit, int kind) {
+    double q8[LBK_GROUPS];
+    canon_groups(a, b, c->geo.n, limit, kind, q8);
+    for (int g = 0; g < LBK_GROUPS; ++g) c->slots[slot][g][k] = q8[g];
+}
+int lbk_fetch_groups(lbk_ctx* c, int slot, double* g64) {
+    if (!slot_ok(c, slot)) return -1;
+    memcpy(g64, c->slots[slot], sizeof c->slots[slot]);
+    return 0;
+}
+int lbk_fetch(lbk_ctx* c, int slot, int ncomp, double* totals) {
+    if (!slot_ok(c, slot) || ncomp > LBK_KMAX) return -1;
+    for (int k = 0; k < ncomp; ++k) totals[k] = ref_total(c, slot * LBK_KMAX + k);
+    return 0;
+}
+double lbk_total(const double* g64, int comp) {
+    double t = g64[comp];
+    for (int g = 1; g < LBK_GROUPS; ++g) t = t + g64[g * LBK_KMAX + comp];
+    return t;
+}
+
+/* f terms of z (per element, the canonical restatement of orc_f) into t; returns the sum limit */
+static int64_t f_terms(int obj, const double* z, int64_t n, double* t) {
+    if (obj == LBK_OBJ_ROSENBROCK) {
+        for (int64_t i = 0; i + 1 < n; i++) {
+            const double term1 = z[i + 1] - z[i] * z[i];
+            const double term2 = 1 - z[i];
+            t[i] = 100.0 * term1 * term1 + term2 * term2;
+        }
+        return n - 1;
+    }
+    if (obj == LBK_OBJ_QUAD_TRIDIAG) {
+        for (int64_t i = 0; i < n; i++) {
+            const double dterm = 1000.0 * z[i] * z[i];
+            t[i] = (i + 1 < n) ? dterm + 100.0 * z[i] * z[i + 1] : dterm;
+        }
+        return n;
+    }
+    for (int64_t i = 0; i < n; i++) t[i] = (z[i] - 1) * (z[i] - 1);
+    return n;
+}
+
+#define CHECK_SLOT(slot) \
+    if (!slot_ok(c, slot)) return -1
+#define ACCOUNT(vecs) c->bytes += (vecs) * 8.0 * (double)c->geo.n_loc
+
+/* ---- the passes ---- */
+int lbk_dot(lbk_ctx* c, const double* a, const double* b, int slot) {
+    CHECK_SLOT(slot);
+    put(c, slot, 0, a, b, c->geo.n, 0);
+    ACCOUNT(2);
+    return 0;
+}
+int lbk_axpy_dot(lbk_ctx* c, double* qout, const double* qin, const double* y, const double* s, double rho,
+                 int ref_alpha, int slot) {
+    CHECK_SLOT(slot);
+    const double alpha = rho * ref_total(c, ref_alpha);
+    for (int64_t i = 0; i < c->geo.n; ++i) qout[i] = qin[i] - alpha * y[i];
+    put(c, slot, 0, s, qout, c->geo.n, 0);
+    ACCOUNT(4);
+    return 0;
+}
+int lbk_mid(lbk_ctx* c, double* rout, const double* qin, const double* y0, double rho0, double gamma,
+            int ref_alpha, int slot) {
+    CHECK_SLOT(slot);
+    const double alpha = rho0 * ref_total(c, ref_alpha);
+    for (int64_t i = 0; i < c->geo.n; ++i) rout[i] = (qin[i] - alpha * y0[i]) * gamma;
+    put(c, slot, 0, y0, rout, c->geo.n, 0);
+    ACCOUNT(3);
+    return 0;
+}
+static double coef_ab(lbk_ctx* c, double rho, int ref_beta, int ref_alpha) {
+    const double beta = rho * ref_total(c, ref_beta);
+    const double alpha = rho * ref_total(c, ref_alpha);
+    return alpha - beta;
+}
+int lbk_axpy2_dot(lbk_ctx* c, double* r, const double* rin, const double* s, const double* ynext, double rho,
+                  int ref_beta, int ref_alpha, int slot) {
+    CHECK_SLOT(slot);
+    const double coef = coef_ab(c, rho, ref_beta, ref_alpha);
+    for (int64_t i = 0; i < c->geo.n; ++i) r[i] = rin[i] + s[i] * coef;
+    put(c, slot, 0, ynext, r, c->geo.n, 0);
+    ACCOUNT(4);
+    return 0;
+}
+int lbk_last(lbk_ctx* c, double* dout, const double* r, const double* s, const double* g, double rho, int ref_beta,
+             int ref_alpha, int slot) {
+    CHECK_SLOT(slot);
+    const double coef = coef_ab(c, rho, ref_beta, ref_alpha);
+    for (int64_t i = 0; i < c->geo.n; ++i) dout[i] = -(r[i] + s[i] * coef);
+    put(c, slot, 0, g, dout, c->geo.n, 0);
+    ACCOUNT(4);
+    return 0;
+}
+int lbk_negdot(lbk_ctx* c, double* dout, const double* g, int slot) {
+    CHECK_SLOT(slot);
+    for (int64_t i = 0; i < c->geo.n; ++i) dout[i] = -g[i];
+    put(c, slot, 0, g, dout, c->geo.n, 0);
+    ACCOUNT(2);
+    return 0;
+}
+int lbk_eval(lbk_ctx* c, int obj, const double* x, double* gout, int slot) {
+    CHECK_SLOT(slot);
+    if (obj < 0 || obj > LBK_OBJ_QUAD_SEPARABLE) return -1;
+    const int64_t n = c->geo.n;
+    double* t = c->scratch[0];
+    double* g = gout ? gout : c->scratch[1];
+    put(c, slot, 0, t, NULL, f_terms(obj, x, n, t), 1);
+    orc_grad(obj, x, n, g);
+    put(c, slot, 1, g, g, n, 0);
+    ACCOUNT(gout ? 2 : 1);
+    return 0;
+}
+/* d per dmode into dd */
+static void form_dir(lbk_ctx* c, int dmode, const double* dsrc, const double* s_last, const double* g, double rho,
+                     int ref_beta, int ref_alpha, double* dd) {
+    const int64_t n = c->geo.n;
+    if (dmode == LBK_D_BUF) {
+        memcpy(dd, dsrc, sizeof(double) * (size_t)n);
+    } else if (dmode == LBK_D_NEG_G) {
+        for (int64_t i = 0; i < n; ++i) dd[i] = -g[i];
+    } else {
+        const double coef = coef_ab(c, rho, ref_beta, ref_alpha);
+        for (int64_t i = 0; i < n; ++i) dd[i] = -(dsrc[i] + s_last[i] * coef);
+    }
+}
+int lbk_trial(lbk_ctx* c, int obj, const double* x, const double* d, double alpha, double* gout, int slot) {
+    CHECK_SLOT(slot);
+    if (obj < 0 || obj > LBK_OBJ_QUAD_SEPARABLE) return -1;
+    const int64_t n = c->geo.n;
+    double *z = c->scratch[0], *t = c->scratch[1], *g = gout ? gout : c->scratch[2];
+    for (int64_t i = 0; i < n; ++i) z[i] = x[i] + alpha * d[i];
+    put(c, slot, 0, t, NULL, f_terms(obj, z, n, t), 1);
+    orc_grad(obj, z, n, g);
+    put(c, slot, 1, g, d, n, 0);
+    ACCOUNT(gout ? 3 : 2);
+    return 0;
+}
+int lbk_trials(lbk_ctx* c, int obj, int dmode, const double* x, const double* dsrc, const double* s_last,
+               const double* gg, double rho, int ref_beta, int ref_alpha, const double* alphas, int nc, int dphi,
+               int slot) {
+    CHECK_SLOT(slot);
+    if (obj < 0 || obj > LBK_OBJ_QUAD_SEPARABLE || nc < 1 || nc > LBK_TRIALS_NC || (dphi && nc != 1)) return -1;
+    const int64_t n = c->geo.n;
+    double *dd = c->scratch[3], *z = c->scratch[0], *t = c->scratch[1], *g = c->scratch[2];
+    form_dir(c, dmode, dsrc, s_last, gg, rho, ref_beta, ref_alpha, dd);
+    for (int j = 0; j < nc; ++j) {
+        for (int64_t i = 0; i < n; ++i) z[i] = x[i] + alphas[j] * dd[i];
+        put(c, slot, j, t, NULL, f_terms(obj, z, n, t), 1);
+        if (dphi && j == 0) {
+            orc_grad(obj, z, n, g);
+            put(c, slot, nc, g, dd, n, 0);
+        }
+    }
+    ACCOUNT(dmode == LBK_D_TWOLOOP ? 3 : 2);
+    return 0;
+}
+int lbk_commit(lbk_ctx* c, int obj, int dmode, const double* x, const double* dsrc, const double* s_last,
+               const double* g, double rho, int ref_beta, int ref_alpha, double alpha, double* xn, double* gn,
+               double* s_out, double* y_out, int slot, double cand) {
+    CHECK_SLOT(slot);
+    const int64_t n = c->geo.n;
+    double *dd = c->scratch[3], *t = c->scratch[1], *z = c->scratch[0];
+    form_dir(c, dmode, dsrc, s_last, g, rho, ref_beta, ref_alpha, dd);
+    for (int64_t i = 0; i < n; ++i) xn[i] = x[i] + alpha * dd[i];
+    if (obj != LBK_OBJ_NONE) {
+        put(c, slot, LBK_C_F, t, NULL, f_terms(obj, xn, n, t), 1);
+        orc_grad(obj, xn, n, gn);
+    }
+    for (int64_t i = 0; i < n; ++i) {
+        s_out[i] = xn[i] - x[i];
+        y_out[i] = gn[i] - g[i];
+    }
+    put(c, slot, LBK_C_GD, g, dd, n, 0);
+    put(c, slot, LBK_C_SY, s_out, y_out, n, 0);
+    put(c, slot, LBK_C_YY, y_out, y_out, n, 0);
+    put(c, slot, LBK_C_GG, gn, gn, n, 0);
+    put(c, slot, LBK_C_SG, s_out, gn, n, 0);
+    put(c, slot, LBK_C_DPHI, gn, dd, n, 0);
+    if (cand > 0.0 && obj != LBK_OBJ_NONE && dmode != LBK_D_BUF) {
+        for (int64_t i = 0; i < n; ++i) z[i] = x[i] + cand * dd[i];
+        put(c, slot, LBK_C_FC, t, NULL, f_terms(obj, z, n, t), 1);
+    }
+    ACCOUNT(4.0 + (dmode == LBK_D_BUF ? 3.0 : dmode == LBK_D_NEG_G ? 2.0 : 4.0));
+    return 0;
+}
+int lbk_point(lbk_ctx* c, double* z, const double* x, const double* d, double alpha) {
+    for (int64_t i = -1; i <= c->geo.n; ++i) z[i] = x[i] + alpha * d[i];
+    ACCOUNT(3);
+    return 0;
+}
+int lbk_elementwise(lbk_ctx* c, int op, double* out, const double* a, const double* b, double alpha) {
+    for (int64_t i = 0; i < c->geo.n; ++i) {
+        switch (op) {
+            case 0: out[i] = alpha * a[i]; break;
+            case 1: out[i] = a[i] + b[i]; break;
+            case 2: out[i] = -a[i]; break;
+            default: out[i] = a[i] + alpha * b[i]; break;
+        }
+    }
+    ACCOUNT(op == 1 || op == 3 ? 3 : 2);
+    return 0;
+}
+int lbk_update(lbk_ctx* c, int op, double* out, const double* a, const double* b, double rho, int slot_a, int slot_b,
+               double scal) {
+    double coef = 0.0;
+    if (op == LBK_U_AXPY_Q) coef = rho * ref_total(c, slot_a * LBK_KMAX);
+    if (op == LBK_U_AXPY_R) coef = (rho * ref_total(c, slot_a * LBK_KMAX)) - (rho * ref_total(c, slot_b * LBK_KMAX));
+    for (int64_t i = 0; i < c->geo.n; ++i) {
+        switch (op) {
+            case LBK_U_AXPY_Q: out[i] = a[i] - coef * b[i]; break;
+            case LBK_U_AXPY_R: out[i] = a[i] + b[i] * coef; break;
+            case LBK_U_SCALE: out[i] = a[i] * scal; break;
+            case LBK_U_NEG: out[i] = -a[i]; break;
+            case LBK_U_SUB: out[i] = a[i] - b[i]; break;
+            default: out[i] = a[i] + scal * b[i]; break;
+        }
+    }
+    ACCOUNT(3);
+    return 0;
+}
+int lbk_checksum(lbk_ctx* c, const double* x, uint64_t* c1, uint64_t* c2) {
+    orc_checksum(x, c->geo.n, c1, c2);
+    return 0;
+}
+
+/* ---- not modelled: vector-free mode, the small-n single-launch forms ---- */
+int lbk_vf_commit(lbk_ctx* c, int obj, int h, const double* x, const double* g, const double* const* S,
+                  const double* const* Y, const double* cs, const double* cy, double cg, double alpha,
+                  const double* cand, double* xn, double* gn, double* so, double* yo, int wslot, int* hb_out) {
+    (void)obj, (void)h, (void)x, (void)g, (void)S, (void)Y, (void)cs, (void)cy, (void)cg, (void)alpha, (void)cand;
+    (void)xn, (void)gn, (void)so, (void)yo, (void)wslot, (void)hb_out;
+    snprintf(c->err, sizeof c->err, "double: vector-free mode unsupported");
+    return -1;
+}
+int lbk_vf_dir(lbk_ctx* c, int h, double* d, const double* g, const double* const* S, const double* const* Y,
+               const double* cs, const double* cy, double cg) {
+    (void)c, (void)h, (void)d, (void)g, (void)S, (void)Y, (void)cs, (void)cy, (void)cg;
+    return -1;
+}
+int lbk_vf_bucket(int h) { return h <= LBK_VF_HMAX ? h : -1; }
+int lbk_vf_ghost_init(lbk_ctx* c, double* x, double* g, int wslot) {
+    (void)c, (void)x, (void)g, (void)wslot;
+    return 0;
+}
+int lbk_small_ok(const lbk_ctx* c, int h) {
+    (void)c, (void)h;
+    return 0;
+}
+int lbk_small_iter(lbk_ctx* c, int obj, int h, const double* g, double* q, double* r, const double* const* S,
+                   const double* const* Y, const double* rho, double gamma, int p0_ref, double a0, const double* x,
+                   double* xn, double* gn, double* so, double* yo, int slot_p0, int slot_a0, int slot_b0, int slot_c) {
+    (void)c, (void)obj, (void)h, (void)g, (void)q, (void)r, (void)S, (void)Y, (void)rho, (void)gamma, (void)p0_ref;
+    (void)a0, (void)x, (void)xn, (void)gn, (void)so, (void)yo, (void)slot_p0, (void)slot_a0, (void)slot_b0,
+        (void)slot_c;
+    return -1;
+}
+
+/* ---- profiling ---- */
+void lbk_prof_enable(lbk_ctx* c, int on) {
+    (void)c;
+    (void)on;
+}
+int lbk_prof_get(lbk_ctx* c, int kind, double* ms, int64_t* launches, double* bytes) {
+    (void)c;
+    if (kind < 0 || kind >= LBK_K_COUNT) return -1;
+    *ms = 0.0;
+    *launches = 0;
+    *bytes = 0.0;
+    return 0;
+}
+void lbk_prof_reset(lbk_ctx* c) { (void)c; }
+double lbk_bytes_moved(const lbk_ctx* c) { return c->bytes; }

@@ -173,3 +173,23 @@ def test_vector_free_large_history_buckets(m, ls):
     assert np.array_equal(bits(r["tr_f"]), bits(o["f"]))
     assert np.array_equal(bits(r["x"]), bits(o["x"]))
     assert "Skipping" not in o["messages"]  # the history really reaches h = m
+
+
+@pytest.mark.parametrize("ticket", [None, "0", "1"])
+@pytest.mark.parametrize("n", [65_535, 65_536, 131_073, 262_143, 262_144])
+def test_vector_free_geometry_edges_bit_exact(monkeypatch, n, ticket):
+    """The edges of the mid-n segment rules (ORC_MIDL_LO = 65536: canonical segments grow to 2048
+    while the vector-free commit keeps 512; ORC_VFL_LO = 262144: the vector-free base length
+    follows the canonical one; just over 131072 the canonical grid drops under the ticket
+    threshold and the vector-free grid does not), under both stage-2 forms and the default
+    choice: bit-exact against the oracle's ORC_CANON_VF restatement."""
+    if ticket is not None:
+        monkeypatch.setenv("LBFGS_TICKET", ticket)
+    x0 = L.x0_uniform(n, 9, -2.0, 2.0)
+    with L.Context(n, 8) as c:
+        r = c.minimize("rosenbrock", x0, "backtracking", 25, trace=True, vector_free=True)
+    o = O.lbfgs("rosenbrock", x0, "backtracking", 8, 25, 1e-5, mode=O.CANON, vector_free=True)
+    assert np.array_equal(bits(r["tr_f"]), bits(o["f"]))
+    assert np.array_equal(bits(r["tr_gnorm"]), bits(o["gnorm"]))
+    assert np.array_equal(r["tr_c1"], o["c1"]) and np.array_equal(r["tr_c2"], o["c2"])
+    assert np.array_equal(bits(r["x"]), bits(o["x"]))
