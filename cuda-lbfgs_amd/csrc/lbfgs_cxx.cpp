@@ -46,6 +46,47 @@ vector<double> QuadTridiagG::operator()(const vector<double>& x) const {
     }
     return g;
 }
+// dense quadratic: row i of A x as the device forms it (k_dense_rows: 64 lane sums over
+// j = l, l+64, ..., then the butterfly), so host and device values agree bit for bit
+static double dense_row(const double* a, const double* x, size_t n) {
+    double v[64], w[64];
+    for (size_t l = 0; l < 64; ++l) {
+        v[l] = 0.0;
+        for (size_t j = l; j < n; j += 64) v[l] = __builtin_fma(a[j], x[j], v[l]);
+    }
+    for (size_t m = 1; m < 64; m <<= 1) {
+        for (size_t l = 0; l < 64; ++l) w[l] = v[l] + v[l ^ m];
+        std::copy(w, w + 64, v);
+    }
+    return v[0];
+}
+double DenseQuadF::operator()(const vector<double>& x) const {
+    const size_t n = b->size();
+    if (x.size() != n) throw std::invalid_argument("dense quadratic: dimension mismatch");
+    double f = 0.0;
+    for (size_t i = 0; i < n; ++i) {
+        const double r = dense_row(A->data() + i * n, x.data(), n);
+        f += x[i] * r + (*b)[i] * x[i];
+    }
+    return f;
+}
+vector<double> DenseQuadG::operator()(const vector<double>& x) const {
+    const size_t n = b->size();
+    if (x.size() != n) throw std::invalid_argument("dense quadratic: dimension mismatch");
+    vector<double> g(n);
+    for (size_t i = 0; i < n; ++i) g[i] = 2.0 * dense_row(A->data() + i * n, x.data(), n) + (*b)[i];
+    return g;
+}
+std::function<double(const vector<double>&)> dense_quadratic_function(const vector<double>& A,
+                                                                       const vector<double>& b) {
+    if (A.size() != b.size() * b.size()) throw std::invalid_argument("dense quadratic: A must be n x n");
+    return DenseQuadF{std::make_shared<const vector<double>>(A), std::make_shared<const vector<double>>(b)};
+}
+std::function<vector<double>(const vector<double>&)> dense_quadratic_gradient(const vector<double>& A,
+                                                                              const vector<double>& b) {
+    if (A.size() != b.size() * b.size()) throw std::invalid_argument("dense quadratic: A must be n x n");
+    return DenseQuadG{std::make_shared<const vector<double>>(A), std::make_shared<const vector<double>>(b)};
+}
 }  // namespace lbfgs_amd
 
 std::function<double(const vector<double>&)> generate_quadratic_function(int n) {
@@ -98,6 +139,11 @@ using FnGc = std::function<vector<double>(const vector<double>&)>;
 typedef double (*PlainF)(const vector<double>&);
 typedef vector<double> (*PlainG)(const vector<double>&);
 
+const lbfgs_amd::DenseQuadF* dense_f(const FnF& f) {
+    const FnFc* wf = f.target<FnFc>();
+    return wf ? wf->target<lbfgs_amd::DenseQuadF>() : f.target<lbfgs_amd::DenseQuadF>();
+}
+
 int identify(const FnF& f, const FnG& g, int n) {
     const PlainF* pf = f.target<PlainF>();
     const PlainG* pg = g.target<PlainG>();
@@ -110,6 +156,11 @@ int identify(const FnF& f, const FnG& g, int n) {
     const lbfgs_amd::QuadTridiagF* qf = wf ? wf->target<lbfgs_amd::QuadTridiagF>() : f.target<lbfgs_amd::QuadTridiagF>();
     const lbfgs_amd::QuadTridiagG* qg = wg ? wg->target<lbfgs_amd::QuadTridiagG>() : g.target<lbfgs_amd::QuadTridiagG>();
     if (qf && qg && qf->n == n && qg->n == n) return LBFGS_OBJ_QUAD_TRIDIAG;
+    const lbfgs_amd::DenseQuadF* df = dense_f(f);
+    const lbfgs_amd::DenseQuadG* dg = wg ? wg->target<lbfgs_amd::DenseQuadG>() : g.target<lbfgs_amd::DenseQuadG>();
+    if (df && dg && (int64_t)df->b->size() == n && (df->A == dg->A || *df->A == *dg->A) &&
+        (df->b == dg->b || *df->b == *dg->b))  // the same problem (each factory keeps its own copy)
+        return LBFGS_OBJ_DENSE_QUAD;
     return LBFGS_OBJ_HOST;
 }
 
@@ -214,6 +265,11 @@ double line_search(int ls, const vector<double>& x, const vector<double>& d, con
         else if (qf && qf->n == (int)n) o = LBFGS_OBJ_QUAD_TRIDIAG;
     }
     lbfgs_ctx* c = util_context(n);
+    if (o == LBFGS_OBJ_DENSE_QUAD) {
+        const lbfgs_amd::DenseQuadF* df = dense_f(f);
+        if (lbfgs_set_dense_quadratic(c, df->A->data(), df->b->data()) != 0)
+            throw std::runtime_error(std::string("lbfgs_set_dense_quadratic failed: ") + lbfgs_last_error(c));
+    }
     HostFns hf{&f, grad ? grad : &no_grad, {}};
     lbfgs_host_fn cb{host_f, grad ? host_g : nullptr, &hf};
     lbfgs_constants k;
@@ -242,13 +298,18 @@ vector<double> run(const FnF& f, const FnG& grad, const vector<double>& x0, int 
     unsigned flags = verbose ? LBFGS_FLAG_VERBOSE : 0u;
     if (const char* mode = std::getenv("LBFGS_MODE")) {
         const std::string md(mode);
-        if (md == "vector_free" && obj != LBFGS_OBJ_HOST && m <= 20) flags |= LBFGS_FLAG_VECTOR_FREE;
-        else if (md == "unfused" && obj != LBFGS_OBJ_HOST) flags |= LBFGS_FLAG_UNFUSED;
+        if (md == "vector_free" && obj < LBFGS_OBJ_HOST && m <= 20) flags |= LBFGS_FLAG_VECTOR_FREE;
+        else if (md == "unfused" && obj < LBFGS_OBJ_HOST) flags |= LBFGS_FLAG_UNFUSED;
     }
     // host callables: LBFGS_REFERENCE_CALLS=1 calls f / grad exactly as the reference does (its
     // re-evaluations included); default one call per distinct point
     if (const char* rcalls = std::getenv("LBFGS_REFERENCE_CALLS"))
         if (std::atoi(rcalls) != 0) flags |= LBFGS_FLAG_REFERENCE_CALLS;
+    if (obj == LBFGS_OBJ_DENSE_QUAD) {  // the matrix and b onto the device (re-uploaded per call)
+        const lbfgs_amd::DenseQuadF* df = dense_f(f);
+        if (lbfgs_set_dense_quadratic(c, df->A->data(), df->b->data()) != 0)
+            throw std::runtime_error(std::string("lbfgs_set_dense_quadratic failed: ") + lbfgs_last_error(c));
+    }
     int rc = lbfgs_minimize(c, obj, obj == LBFGS_OBJ_HOST ? &cb : nullptr, ls, &k, x0.data(), x.data(),
                             max_iterations, tolerance, flags, &res);
     if (!hf.error.empty()) throw std::runtime_error("objective callback failed: " + hf.error);

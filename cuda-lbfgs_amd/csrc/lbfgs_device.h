@@ -56,6 +56,8 @@ extern "C" {
 #define LBK_OBJ_QUAD_TRIDIAG 1
 #define LBK_OBJ_QUAD_SEPARABLE 2
 #define LBK_OBJ_NONE 3 /* gradient supplied in a buffer, f computed elsewhere (host callback) */
+#define LBK_OBJ_DENSE 4 /* f = x'Ax + b'x (lbk_dense_set / lbk_dense_eval; not a stencil pass) */
+#define LBK_DENSE_NMAX 65536
 
 /* direction modes of the commit kernel */
 #define LBK_D_BUF 0     /* d read from a buffer */
@@ -171,6 +173,10 @@ int lbk_commit(lbk_ctx* c, int obj, int dmode, const double* x, const double* ds
 int lbk_trials(lbk_ctx* c, int obj, int dmode, const double* x, const double* dsrc, const double* s_last,
                const double* g, double rho, int ref_beta, int ref_alpha, const double* alphas, int nc, int dphi,
                int slot);
+/* dense quadratic objective: A (n x n, row-major, symmetric) and b uploaded once; eval at x writes
+ * slot components f and (with gout) gout . gout, and grad = 2 A x + b into gout */
+int lbk_dense_set(lbk_ctx* c, const double* A, const double* b);
+int lbk_dense_eval(lbk_ctx* c, const double* x, double* gout, int slot);
 /* z = x + alpha * d (host-callback objectives) */
 int lbk_point(lbk_ctx* c, double* z, const double* x, const double* d, double alpha);
 /* elementwise primitives (op: 0 alpha*a, 1 a+b, 2 -a, 3 a+alpha*b) over the local range */

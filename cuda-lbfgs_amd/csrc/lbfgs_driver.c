@@ -79,6 +79,7 @@ struct lbfgs_ctx {
     int hf_valid; /* f(z) at hf_alpha, this iteration */
     double hf_alpha, hf_val;
     int refcalls; /* LBFGS_FLAG_REFERENCE_CALLS */
+    int dense_set; /* lbfgs_set_dense_quadratic called */
     int64_t cb_f, cb_g;
     /* per-iteration working state */
     int dmode, d_ready;
@@ -372,6 +373,18 @@ int lbfgs_peer_enable(lbfgs_ctx* c, int on) {
     return lbk_peer_enable(c->dev, on) == 0 ? 0 : LBFGS_ERR_STATE;
 }
 
+int lbfgs_set_dense_quadratic(lbfgs_ctx* c, const double* A, const double* b) {
+    if (!c || !A || !b || c->geo->world != 1) return LBFGS_ERR_BAD_ARG;
+    const int rc = lbk_dense_set(c->dev, A, b);
+    if (rc != 0) {
+        snprintf(c->err, sizeof c->err, "%s", lbk_last_error(c->dev));
+        return rc == -1 ? LBFGS_ERR_BAD_ARG : LBFGS_ERR_HIP;
+    }
+    c->inited = 0;
+    c->dense_set = 1;
+    return 0;
+}
+
 int lbfgs_exchange_backend(const lbfgs_ctx* c) { return c ? lbk_exchange_backend(c->dev) : LBFGS_ERR_BAD_ARG; }
 
 int lbfgs_exchange_latency(lbfgs_ctx* c, int backend, int components, int iters, double* us) {
@@ -401,6 +414,11 @@ int lbfgs_exchange_latency(lbfgs_ctx* c, int backend, int components, int iters,
 #define XF_X 1
 #define XF_G0 2 /* + buffer */
 
+/* objectives evaluated outside the fused stencil passes: host callbacks, and the dense quadratic
+ * (a matrix-vector product needs the whole trial point first). Both run the same driver path:
+ * z = x + alpha d formed on the device, f / grad at z, the commit with the gradient supplied. */
+static int ext_obj(const lbfgs_ctx* c) { return c->obj == LBFGS_OBJ_HOST || c->obj == LBFGS_OBJ_DENSE_QUAD; }
+
 static int host_bufs(lbfgs_ctx* c) {
     const size_t b = sizeof(double) * (size_t)c->n;
     if (!c->hx) c->hx = (double*)lbk_host_alloc(b);
@@ -422,6 +440,13 @@ static int host_point_issue(lbfgs_ctx* c, double alpha) {
     if (c->hz_valid && c->hz_alpha == alpha) return 0;
     if (c->hz_pending) DEVNC(lbk_xfer_wait(c->dev, XF_Z)); /* hx is still being written */
     DEV(lbk_point(c->dev, c->xn, c->x, c->d, alpha));
+    if (c->obj == LBFGS_OBJ_DENSE_QUAD) { /* z stays on the device (xn) */
+        c->hz_valid = 1;
+        c->hz_pending = 0;
+        c->hz_alpha = alpha;
+        c->hf_valid = 0;
+        return 0;
+    }
     DEVNC(lbk_download_local_async(c->dev, c->hx, c->xn, XF_Z));
     c->hz_valid = c->hz_pending = 1;
     c->hz_alpha = alpha;
@@ -447,8 +472,15 @@ static int host_f_at(lbfgs_ctx* c, double alpha, int fresh, double* f) {
     }
     int rc = host_point(c, alpha);
     if (rc) return rc;
-    *f = c->cb.f(c->hx, c->n, c->cb.user);
-    c->cb_f++;
+    if (c->obj == LBFGS_OBJ_DENSE_QUAD) { /* f and, for free, grad into gt */
+        DEV(lbk_dense_eval(c->dev, c->xn, c->gt, SLOT_TRIAL(c->m)));
+        DEVNC(lbk_fetch(c->dev, SLOT_TRIAL(c->m), 1, f));
+        c->gt_valid = 1;
+        c->gt_alpha = alpha;
+    } else {
+        *f = c->cb.f(c->hx, c->n, c->cb.user);
+        c->cb_f++;
+    }
     c->hf_valid = 1;
     c->hf_alpha = alpha;
     c->hf_val = *f;
@@ -463,6 +495,21 @@ static int host_g_at(lbfgs_ctx* c, double alpha, int fresh, double* dst) {
     }
     int rc = host_point(c, alpha);
     if (rc) return rc;
+    if (c->obj == LBFGS_OBJ_DENSE_QUAD) {
+        double f;
+        DEV(lbk_dense_eval(c->dev, c->xn, dst, SLOT_TRIAL(c->m)));
+        DEVNC(lbk_fetch(c->dev, SLOT_TRIAL(c->m), 1, &f));
+        c->hf_valid = 1;
+        c->hf_alpha = alpha;
+        c->hf_val = f;
+        if (dst == c->gt) {
+            c->gt_valid = 1;
+            c->gt_alpha = alpha;
+        } else if (c->gt_valid && c->gt_alpha == alpha) {
+            c->gt_valid = 0;
+        }
+        return 0;
+    }
     const int b = c->hg_cur;
     c->hg_cur ^= 1;
     DEVNC(lbk_xfer_wait(c->dev, XF_G0 + b)); /* the upload that last read this buffer */
@@ -613,7 +660,7 @@ static int trial(lbfgs_ctx* c, double alpha, int need_g, double* f, double* dphi
                 return 0;
             }
     }
-    if (c->batch && !c->unfused && c->obj != LBFGS_OBJ_HOST) return trial_batched(c, alpha, need_g, f, dphi);
+    if (c->batch && !c->unfused && !ext_obj(c)) return trial_batched(c, alpha, need_g, f, dphi);
     int rc = materialize_d(c);
     if (rc) return rc;
     if (c->unfused) {
@@ -628,7 +675,7 @@ static int trial(lbfgs_ctx* c, double alpha, int need_g, double* f, double* dphi
             DEVNC(lbk_fetch(c->dev, SLOT_MISC(c->m) + 3, 1, &t[1]));
             if (dphi) *dphi = t[1];
         }
-    } else if (c->obj == LBFGS_OBJ_HOST) {
+    } else if (ext_obj(c)) {
         /* reference order: the backtracking-Wolfe search takes grad(x_new) before f(x_new)
          * (line_search.cpp:39-42); the Wolfe search's gradient follows its own f call at the
          * same point (:146,160), never a second f */
@@ -849,7 +896,7 @@ static int commit(lbfgs_ctx* c, int dmode, double alpha, int cslot, double* tot,
     const double* dsrc = dmode == LBK_D_BUF ? c->d : c->rc;
     const double* s_last = dmode == LBK_D_TWOLOOP ? c->S[c->s_last_pair] : NULL;
     int obj = c->obj;
-    if (c->obj == LBFGS_OBJ_HOST) {
+    if (ext_obj(c)) {
         /* f(x_new) (lbfgs.cpp:160), then - unless the step failed (:164-168) - grad(x_new)
          * (:171) onto the device for the commit kernel; both from the line search's cache
          * unless the reference call order asks for the reference's fresh calls */
@@ -909,7 +956,7 @@ static int iterate(lbfgs_ctx* c) {
     /* ---- search direction (:87-143) ---- */
     int dmode = LBK_D_NEG_G;
     int small_done = 0;
-    const int small = c->obj != LBFGS_OBJ_HOST && !c->unfused && c->geo->world == 1 && lbk_small_ok(c->dev, h);
+    const int small = !ext_obj(c) && !c->unfused && c->geo->world == 1 && lbk_small_ok(c->dev, h);
     c->d_ready = 0;
     c->spec_valid = 0;
     c->cand_valid = 0;
@@ -1013,7 +1060,7 @@ static int iterate(lbfgs_ctx* c) {
     double gd;
     c->a0 = c->K.initial_step;
     const int sharded = c->geo->world > 1;
-    if (c->obj != LBFGS_OBJ_HOST && !c->unfused) {
+    if (!ext_obj(c) && !c->unfused) {
         /* last two-loop pass + first trial at a0 + commit fused in one pass. Sharded, the
          * stencil's halo of d at the rank edges comes from the neighbours' edge r (published
          * with the last second-loop pass's reduction) and s_{h-1}'s ghost cells; d = -g is
@@ -1078,7 +1125,7 @@ static int iterate(lbfgs_ctx* c) {
     /* ---- commit (:159-198) ---- */
     if (!(c->spec_valid && alpha == c->a0)) {
         /* batched: d may still be unmaterialised (formed on the fly again, same bits) */
-        if (!(c->batch && !c->unfused && c->obj != LBFGS_OBJ_HOST && !c->d_ready &&
+        if (!(c->batch && !c->unfused && !ext_obj(c) && !c->d_ready &&
               (c->dmode == LBK_D_TWOLOOP || (c->dmode == LBK_D_NEG_G && c->geo->world == 1)))) {
             rc = materialize_d(c);
             if (rc) return rc;
@@ -1358,8 +1405,9 @@ int lbfgs_solver_init(lbfgs_ctx* c, int objective, const lbfgs_host_fn* cb, int 
                       const lbfgs_constants* k, const double* x0_host, double tolerance,
                       unsigned flags) {
     if (!c || !x0_host) return LBFGS_ERR_BAD_ARG;
-    if (objective < 0 || objective > LBFGS_OBJ_HOST) return LBFGS_ERR_BAD_ARG;
+    if (objective < 0 || objective > LBFGS_OBJ_DENSE_QUAD) return LBFGS_ERR_BAD_ARG;
     if (line_search < 0 || line_search > LBFGS_LS_BACKTRACKING_WOLFE) return LBFGS_ERR_BAD_ARG;
+    if (objective == LBFGS_OBJ_DENSE_QUAD && !c->dense_set) return LBFGS_ERR_STATE;
     c->refcalls = (flags & LBFGS_FLAG_REFERENCE_CALLS) != 0;
     if (objective == LBFGS_OBJ_HOST) {
         if (!cb || !cb->f || !cb->grad || c->geo->world != 1) return LBFGS_ERR_BAD_ARG;
@@ -1375,7 +1423,7 @@ int lbfgs_solver_init(lbfgs_ctx* c, int objective, const lbfgs_host_fn* cb, int 
         const char* e = getenv("LBFGS_BATCH");
         if (e) c->batch = atoi(e) != 0;
     }
-    if (c->unfused && (objective == LBFGS_OBJ_HOST || c->geo->world != 1)) return LBFGS_ERR_BAD_ARG;
+    if (c->unfused && (objective >= LBFGS_OBJ_HOST || c->geo->world != 1)) return LBFGS_ERR_BAD_ARG;
     /* ping-pong q/r (LBFGS_PINGPONG=1): measured neutral at n=1e8 and -8 % at n=1e7 (the
      * in-place passes keep q/r in the Infinity Cache), so in-place is the default */
     c->pingpong = 0;
@@ -1390,7 +1438,7 @@ int lbfgs_solver_init(lbfgs_ctx* c, int objective, const lbfgs_host_fn* cb, int 
     }
     c->vf = (flags & LBFGS_FLAG_VECTOR_FREE) != 0;
     if (c->vf) {
-        if (c->unfused || objective == LBFGS_OBJ_HOST || c->m > LBK_VF_HMAX) return LBFGS_ERR_BAD_ARG;
+        if (c->unfused || objective >= LBFGS_OBJ_HOST || c->m > LBK_VF_HMAX) return LBFGS_ERR_BAD_ARG;
         const size_t P = (size_t)c->m + 1;
         if (!c->Gss) {
             c->Gss = (double*)calloc(P * P, sizeof(double));
@@ -1434,7 +1482,10 @@ int lbfgs_solver_init(lbfgs_ctx* c, int objective, const lbfgs_host_fn* cb, int 
         DEVNC(lbk_fetch(c->dev, SLOT_INIT, 1, &c->gg));
     } else {
         double t[2];
-        DEV(lbk_eval(c->dev, objective, c->x, c->g, SLOT_INIT));
+        if (objective == LBFGS_OBJ_DENSE_QUAD)
+            DEV(lbk_dense_eval(c->dev, c->x, c->g, SLOT_INIT));
+        else
+            DEV(lbk_eval(c->dev, objective, c->x, c->g, SLOT_INIT));
         DEVNC(lbk_fetch(c->dev, SLOT_INIT, 2, t));
         c->f_cur = t[0];
         c->gg = t[1];
@@ -1560,11 +1611,15 @@ int lbfgs_dev_norm(lbfgs_ctx* c, const double* v, double* out) {
 }
 
 int lbfgs_dev_objective(lbfgs_ctx* c, int obj, const double* x, double* f_out, double* g_out) {
-    if (!c || !x || obj < 0 || obj >= LBFGS_OBJ_HOST) return LBFGS_ERR_BAD_ARG;
+    if (!c || !x || obj < 0 || obj == LBFGS_OBJ_HOST || obj > LBFGS_OBJ_DENSE_QUAD) return LBFGS_ERR_BAD_ARG;
+    if (obj == LBFGS_OBJ_DENSE_QUAD && !c->dense_set) return LBFGS_ERR_STATE;
     c->inited = 0;
     double t[2];
     DEVNC(lbk_upload(c->dev, c->q, x));
-    DEV(lbk_eval(c->dev, obj, c->q, c->gt, SLOT_MISC(c->m)));
+    if (obj == LBFGS_OBJ_DENSE_QUAD)
+        DEV(lbk_dense_eval(c->dev, c->q, c->gt, SLOT_MISC(c->m)));
+    else
+        DEV(lbk_eval(c->dev, obj, c->q, c->gt, SLOT_MISC(c->m)));
     DEVNC(lbk_fetch(c->dev, SLOT_MISC(c->m), 2, t));
     if (f_out) *f_out = t[0];
     if (g_out) DEVNC(lbk_download(c->dev, g_out, c->gt));
@@ -1635,8 +1690,9 @@ int lbfgs_line_search(lbfgs_ctx* c, int objective, const lbfgs_host_fn* cb, int 
                       const lbfgs_constants* k, const double* x, const double* d, const double* g,
                       double* alpha_out) {
     if (!c || !x || !d || !g || !alpha_out || c->geo->world != 1) return LBFGS_ERR_BAD_ARG;
-    if (objective < 0 || objective > LBFGS_OBJ_HOST) return LBFGS_ERR_BAD_ARG;
+    if (objective < 0 || objective > LBFGS_OBJ_DENSE_QUAD) return LBFGS_ERR_BAD_ARG;
     if (line_search < 0 || line_search > LBFGS_LS_BACKTRACKING_WOLFE) return LBFGS_ERR_BAD_ARG;
+    if (objective == LBFGS_OBJ_DENSE_QUAD && !c->dense_set) return LBFGS_ERR_STATE;
     c->refcalls = 0; /* the standalone search evaluates f(x) once (see above) */
     if (objective == LBFGS_OBJ_HOST) {
         if (!cb || !cb->f || (!cb->grad && (line_search == LBFGS_LS_WOLFE || line_search == LBFGS_LS_BACKTRACKING_WOLFE)))
@@ -1668,6 +1724,9 @@ int lbfgs_line_search(lbfgs_ctx* c, int objective, const lbfgs_host_fn* cb, int 
     if (objective == LBFGS_OBJ_HOST) {
         c->f_cur = c->cb.f(x, c->n, c->cb.user);
         c->cb_f++;
+    } else if (objective == LBFGS_OBJ_DENSE_QUAD) {
+        DEV(lbk_dense_eval(c->dev, c->x, c->gt, SLOT_MISC(m)));
+        DEVNC(lbk_fetch(c->dev, SLOT_MISC(m), 1, &c->f_cur));
     } else {
         double t[2];
         DEV(lbk_eval(c->dev, objective, c->x, NULL, SLOT_MISC(m)));

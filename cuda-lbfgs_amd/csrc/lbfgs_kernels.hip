@@ -1255,6 +1255,57 @@ __global__ __launch_bounds__(LB_BLOCK) void k_trials(const double* __restrict__ 
 }
 
 // ---------------------------------------------------------------------------------------
+// Dense quadratic objective f(x) = x'Ax + b'x, grad = 2 A x + b: the known-answer problems of
+// the reference's sequential-implementation/matrices.h (mat<n>, linear<n>, minimum<n>;
+// SURVEY 8f item 4). Row i of A x is one wave: lane l accumulates fma(A_ij, x_j) over
+// j = l, l + 64, ... in ascending order, then the wave butterfly; g_i = 2 r_i + b_i and the f term
+// t_i = x_i r_i + b_i x_i, which the pass after it sums in the canonical order. The row order
+// is restated by oracle/lbfgs_oracle.c (dense_row).
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_dense_rows(const double* __restrict__ A, const double* __restrict__ b,
+                                                    const double* __restrict__ x, double* __restrict__ g,
+                                                    double* __restrict__ t, int64_t n) {
+    const int lane = threadIdx.x & 63;
+    const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= n) return;  // wave-uniform
+    const double* __restrict__ a = A + i * n;
+    double v = 0.0;
+    for (int64_t j = lane; j < n; j += 64) v = fma(a[j], x[j], v);
+    v = wave_sum(v);
+    if (lane == 0) {
+        const double xi = x[i];
+        if (g) g[i] = 2.0 * v + b[i];
+        t[i] = xi * v + b[i] * xi;
+    }
+}
+
+// f = canonical sum of the terms t; with g, also g . g (lbk_eval's components)
+template <bool NT>
+struct OpTermsDot {
+    const double* __restrict__ t;
+    const double* __restrict__ g;
+    struct Row {
+        double2 t, g;
+    };
+    __device__ void load(Row& r, int64_t i) const {
+        r.t = ldv<NT>(t + i);
+        if (g) r.g = ldv<NT>(g + i);
+    }
+    template <bool MASK>
+    __device__ void apply(Row& r, int64_t, int64_t, bool v0, bool v1, double (&acc)[2]) const {
+        if (!MASK || v0) acc[0] = acc[0] + r.t.x;
+        if (!MASK || v1) acc[0] = acc[0] + r.t.y;
+        if (g) acc[1] = fma2<MASK>(r.g, r.g, acc[1], v0, v1);
+    }
+};
+
+template <bool NT>
+__global__ __launch_bounds__(LB_BLOCK) void k_terms_dot(const double* __restrict__ t, const double* __restrict__ g,
+                                                        Geo geo, Red red) {
+    run_pass<OpTermsDot<NT>, 2>(OpTermsDot<NT>{t, g}, geo, red);
+}
+
+// ---------------------------------------------------------------------------------------
 // Vector-free mode (LBFGS_FLAG_VECTOR_FREE). The two-loop runs on the host in coefficient
 // space over the Gram matrix of the basis b = [s_0..s_{h-1}, y_0..y_{h-1}, g]; the device
 // pass forms d = sum_l c_l b_l + cg g on the fly (l ascending, then g; each product rounded,
@@ -2066,6 +2117,7 @@ struct lbk_ctx {
     double* coop_redge;            // 2 per segment
     double wall_khz;
     hipEvent_t xfer_ev[4];  // lbk_*_local_async completion (host-callback transfers)
+    double *dq_A, *dq_b, *dq_t;  // dense quadratic objective (lbk_dense_set): A (n x n), b, terms
 };
 
 namespace {
@@ -2603,6 +2655,9 @@ void lbk_destroy(lbk_ctx* c) {
     for (auto e : c->xfer_ev)
         if (e) (void)hipEventDestroy(e);
     if (c->comm) ncclCommDestroy(c->comm);
+    if (c->dq_A) (void)hipFree(c->dq_A);
+    if (c->dq_b) (void)hipFree(c->dq_b);
+    if (c->dq_t) (void)hipFree(c->dq_t - LBK_FRONT);
     lbk_xgmi_destroy(c->xg);
     if (c->d_ckslot) (void)hipFree(c->d_ckslot);
     (void)hipFree(c->partials);
@@ -2926,6 +2981,43 @@ int lbk_trials(lbk_ctx* c, int obj, int dmode, const double* x, const double* ds
     }, K);
 #undef TRIALS_DM
 #undef TRIALS_LAUNCH
+}
+
+int lbk_dense_set(lbk_ctx* c, const double* A, const double* b) {
+    const int64_t n = c->geo.n;
+    if (c->geo.world != 1 || n > LBK_DENSE_NMAX || !A || !b) {
+        snprintf(c->err, sizeof c->err, "dense quadratic: one rank and n <= %d only", LBK_DENSE_NMAX);
+        return -1;
+    }
+    if (!c->dq_A) {
+        HIPCHK(c, hipMalloc(&c->dq_A, sizeof(double) * (size_t)(n * n)));
+        HIPCHK(c, hipMalloc(&c->dq_b, sizeof(double) * (size_t)n));
+        double* t = lbk_vec_alloc(c);
+        if (!t) return -2;
+        c->dq_t = t;
+    }
+    HIPCHK(c, hipMemcpyAsync(c->dq_A, A, sizeof(double) * (size_t)(n * n), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->dq_b, b, sizeof(double) * (size_t)n, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+int lbk_dense_eval(lbk_ctx* c, const double* x, double* gout, int slot) {
+    if (!c->dq_A) {
+        snprintf(c->err, sizeof c->err, "dense quadratic: no matrix (lbfgs_set_dense_quadratic)");
+        return -1;
+    }
+    const int64_t n = c->geo.n;
+    const int nb = (int)((n + 3) / 4);
+    // the row pass reads A once (n^2 doubles) and x; its bytes are counted with the terms pass
+    hipLaunchKernelGGL(k_dense_rows, dim3(nb), dim3(256), 0, c->stream, c->dq_A, c->dq_b, x, gout, c->dq_t, n);
+    HIPCHK(c, hipGetLastError());
+    Geo g = kgeo(c);
+    Red r = kred(c, slot, 2);
+    return launch(c, LBK_K_EVAL, (double)n + 3.0 + (gout ? 2.0 : 0.0), slot, [&] {
+        NT_DISPATCH(c, hipLaunchKernelGGL(k_terms_dot<NT_>, dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, c->dq_t,
+                                          gout, g, r));
+    }, 2);
 }
 
 int lbk_point(lbk_ctx* c, double* z, const double* x, const double* d, double alpha) {

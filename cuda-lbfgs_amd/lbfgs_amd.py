@@ -16,7 +16,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LBFGS_LIB") or os.path.join(HERE, "liblbfgs_hip.so")  # LBFGS_LIB: A/B builds
 
-OBJECTIVES = {"rosenbrock": 0, "quad_tridiag": 1, "quad_sep": 2, "host": 3}
+OBJECTIVES = {"rosenbrock": 0, "quad_tridiag": 1, "quad_sep": 2, "host": 3, "dense": 4}
 LINE_SEARCHES = {"backtracking": 0, "interpolation": 1, "wolfe": 2, "backtracking_wolfe": 3}
 STATUS = {0: "converged", 1: "max_iter", 2: "ls_failed", 3: "running"}
 FLAG_VERBOSE, FLAG_QUIET, FLAG_TRACE, FLAG_UNFUSED, FLAG_VECTOR_FREE = 1, 2, 4, 8, 16
@@ -133,7 +133,7 @@ EXPORTED_SYMBOLS = [
     "lbfgs_dev_dot", "lbfgs_dev_norm", "lbfgs_dev_objective", "lbfgs_dev_trial",
     "lbfgs_dev_twoloop", "lbfgs_dev_elementwise", "lbfgs_line_search", "lbfgs_prof_enable",
     "lbfgs_prof_reset", "lbfgs_prof_get", "lbfgs_peer_handle", "lbfgs_peer_connect", "lbfgs_peer_enable",
-    "lbfgs_exchange_backend", "lbfgs_exchange_latency", "lbfgs_device_count",
+    "lbfgs_exchange_backend", "lbfgs_exchange_latency", "lbfgs_device_count", "lbfgs_set_dense_quadratic",
 ]
 PEER_HANDLE_BYTES = 64
 BACKENDS = {0: "single", 1: "rccl", 2: "xgmi", 3: "host-group"}
@@ -240,6 +240,15 @@ class Context:
             self.close()
         except Exception:
             pass
+
+    def set_dense_quadratic(self, A, b):
+        """Upload A (n x n, symmetric) and b for the "dense" objective f = x'Ax + b'x."""
+        A = np.ascontiguousarray(A, np.float64)
+        b = np.ascontiguousarray(b, np.float64)
+        assert A.shape == (self.n, self.n) and b.shape == (self.n,)
+        rc = lib().lbfgs_set_dense_quadratic(self.h, A.ctypes.data_as(C.c_void_p), b.ctypes.data_as(C.c_void_p))
+        if rc != 0:
+            self._err("lbfgs_set_dense_quadratic", rc)
 
     # ---- sharded runs: xGMI peer exchange ----
     def peer_handle(self):

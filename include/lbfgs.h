@@ -13,6 +13,7 @@
 #ifndef LBFGS_AMD_LBFGS_H
 #define LBFGS_AMD_LBFGS_H
 #include <functional>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -36,9 +37,26 @@ std::vector<double> LBFGS_CUDA(const std::function<double(std::vector<double>)> 
 
 namespace lbfgs_amd {
 /* which objective path the calling thread's last LBFGS / LBFGS_CUDA call took: 0 Rosenbrock,
- * 1 tridiagonal quadratic, 2 separable quadratic (device kernels), 3 host callbacks
- * (LBFGS_OBJ_* of lbfgs_hip.h); -1 before the first call. Diagnostic for tests. */
+ * 1 tridiagonal quadratic, 2 separable quadratic (device kernels), 3 host callbacks, 4 dense
+ * quadratic (device) (LBFGS_OBJ_* of lbfgs_hip.h); -1 before the first call. Diagnostic. */
 int last_objective();
+
+/* Dense quadratic f(x) = x'Ax + b'x, grad = 2Ax + b (A symmetric, n x n row-major): the problems
+ * of the reference's sequential-implementation/matrices.h (mat<n>, linear<n>). Passed to LBFGS()
+ * as a pair, they are recognised and evaluated on the device (LBFGS_OBJ_DENSE_QUAD); called
+ * directly they compute the same values on the host. */
+struct DenseQuadF {
+    std::shared_ptr<const std::vector<double>> A, b;
+    double operator()(const std::vector<double>& x) const;
+};
+struct DenseQuadG {
+    std::shared_ptr<const std::vector<double>> A, b;
+    std::vector<double> operator()(const std::vector<double>& x) const;
+};
+std::function<double(const std::vector<double>&)> dense_quadratic_function(const std::vector<double>& A,
+                                                                           const std::vector<double>& b);
+std::function<std::vector<double>(const std::vector<double>&)> dense_quadratic_gradient(
+    const std::vector<double>& A, const std::vector<double>& b);
 }  // namespace lbfgs_amd
 
 #endif

@@ -46,7 +46,8 @@ enum {
     LBFGS_OBJ_ROSENBROCK = 0,     /* benchmark.cpp:58-81 */
     LBFGS_OBJ_QUAD_TRIDIAG = 1,   /* generate_quadratic_function(n), benchmark.cpp:16-56 */
     LBFGS_OBJ_QUAD_SEPARABLE = 2, /* main.cpp:7-21 */
-    LBFGS_OBJ_HOST = 3            /* user callbacks (lbfgs_host_fn) */
+    LBFGS_OBJ_HOST = 3,           /* user callbacks (lbfgs_host_fn) */
+    LBFGS_OBJ_DENSE_QUAD = 4      /* f = x'Ax + b'x on the device (lbfgs_set_dense_quadratic) */
 };
 
 /* line searches, lbfgs.cpp:40-70 */
@@ -106,6 +107,14 @@ typedef struct {
 
 void lbfgs_constants_default(lbfgs_constants* k); /* sequential-implementation/config.h */
 void lbfgs_constants_cuda(lbfgs_constants* k);    /* parallel-implementation/constants.h */
+
+/* Dense quadratic objective (LBFGS_OBJ_DENSE_QUAD): f(x) = x'Ax + b'x, grad = 2Ax + b, A symmetric
+ * n x n row-major (n <= 65536), evaluated on the device - the known-answer problems of the
+ * reference's sequential-implementation/matrices.h (mat<n>, linear<n>, minimum<n>). Row i of Ax is
+ * one wavefront (lane l sums j = l, l+64, ... with fma, then a butterfly); f sums the terms
+ * x_i (Ax)_i + b_i x_i in the canonical order (restated by the oracle). Uploads A and b into the
+ * context; one rank. */
+int lbfgs_set_dense_quadratic(lbfgs_ctx* ctx, const double* A, const double* b);
 
 /* Host-callback objective (LBFGS_OBJ_HOST). x has n entries (global vector). */
 typedef double (*lbfgs_host_f)(const double* x, int64_t n, void* user);

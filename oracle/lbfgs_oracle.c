@@ -266,7 +266,45 @@ static double* terms_buf(int64_t n) {
     return g_terms;
 }
 
+static const double* g_dense_A;
+static const double* g_dense_b;
+
+void orc_dense_set(const double* A, const double* b) {
+    g_dense_A = A;
+    g_dense_b = b;
+}
+
+/* row of A x in the device's order (lbfgs_kernels.hip k_dense_rows) */
+static double dense_row(const double* a, const double* x, int64_t n) {
+    double v[64], w[64];
+    for (int l = 0; l < 64; ++l) {
+        v[l] = 0.0;
+        for (int64_t j = l; j < n; j += 64) v[l] = fma(a[j], x[j], v[l]);
+    }
+    for (int m = 1; m < 64; m <<= 1) {
+        for (int l = 0; l < 64; ++l) w[l] = v[l] + v[l ^ m];
+        memcpy(v, w, sizeof v);
+    }
+    return v[0];
+}
+
 double orc_f(int obj, const double* x, int64_t n, int mode) {
+    if (obj == ORC_OBJ_DENSE) {
+        double* t = (double*)malloc(sizeof(double) * (size_t)(n > 0 ? n : 1));
+        for (int64_t i = 0; i < n; ++i) {
+            const double r = dense_row(g_dense_A + i * n, x, n);
+            t[i] = x[i] * r + g_dense_b[i] * x[i];
+        }
+        double f;
+        if (mode == ORC_SEQ) {
+            f = 0.0;
+            for (int64_t i = 0; i < n; ++i) f += t[i];
+        } else {
+            f = orc_sum(t, n, n, mode);
+        }
+        free(t);
+        return f;
+    }
     if (mode == ORC_SEQ) {
         double sum = 0.0;
         if (obj == ORC_OBJ_ROSENBROCK) { /* benchmark.cpp:58-68 */
@@ -305,6 +343,10 @@ double orc_f(int obj, const double* x, int64_t n, int mode) {
 }
 
 void orc_grad(int obj, const double* x, int64_t n, double* g) {
+    if (obj == ORC_OBJ_DENSE) {
+        for (int64_t i = 0; i < n; ++i) g[i] = 2.0 * dense_row(g_dense_A + i * n, x, n) + g_dense_b[i];
+        return;
+    }
     if (obj == ORC_OBJ_ROSENBROCK) { /* benchmark.cpp:70-81 */
         for (int64_t i = 0; i < n; ++i) g[i] = 0.0;
         for (int64_t i = 0; i + 1 < n; i++) {

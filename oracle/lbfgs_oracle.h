@@ -22,7 +22,8 @@ extern "C" {
 
 /* ORC_OBJ_HOST: the caller's f/grad callbacks (the reference's LBFGS takes any
  * std::function objective, lbfgs.h:9-10); used with the dense quadratics of matrices.h */
-enum { ORC_OBJ_ROSENBROCK = 0, ORC_OBJ_QUAD_TRIDIAG = 1, ORC_OBJ_QUAD_SEPARABLE = 2, ORC_OBJ_HOST = 3 };
+enum { ORC_OBJ_ROSENBROCK = 0, ORC_OBJ_QUAD_TRIDIAG = 1, ORC_OBJ_QUAD_SEPARABLE = 2, ORC_OBJ_HOST = 3,
+       ORC_OBJ_DENSE = 4 /* x'Ax + b'x, the matrices.h problems (orc_dense_set) */ };
 enum { ORC_LS_BACKTRACKING = 0, ORC_LS_INTERPOLATION = 1, ORC_LS_WOLFE = 2, ORC_LS_BACKTRACKING_WOLFE = 3 };
 enum { ORC_SEQ = 0, ORC_CANON = 1, ORC_CANON_VF = 2 /* contiguous rows per wave */,
        ORC_PAIR = 3 /* pairwise sums */, ORC_REV = 4 /* right-to-left sums */,
@@ -69,6 +70,12 @@ void orc_canon_geometry(int64_t n, int64_t* seg_len, int64_t* nseg);
 int orc_vf_factor(int64_t n); /* vector-free commit segment, in canonical segments */
 /* group partials Q_0..Q_7 of the canonical order (total = sequential sum of the 8). */
 void orc_canon_dot_groups(const double* a, const double* b, int64_t n, double* q8);
+
+/* Dense quadratic data for ORC_OBJ_DENSE (A n x n row-major, b; kept by pointer). Row i of Ax is
+ * formed as the product's k_dense_rows does in every mode: 64 lane sums over j = l, l+64, ...
+ * (fma, ascending), then the butterfly v_l + v_{l^m}, m = 1, 2, ..., 32; grad_i = 2 r_i + b_i,
+ * f = sum of x_i r_i + b_i x_i in the mode's order. */
+void orc_dense_set(const double* A, const double* b);
 
 /* Objectives (benchmark.cpp:16-81, main.cpp:7-21). */
 double orc_f(int obj, const double* x, int64_t n, int mode);

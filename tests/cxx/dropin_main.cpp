@@ -10,6 +10,7 @@
 #include <stdexcept>
 
 #include <benchmark.h>
+#include <lbfgs.h>
 #include <line_search.h>
 #include <vector_utils.h>
 
@@ -74,5 +75,22 @@ int main() {
     put_x("x_cuda", LBFGS_CUDA(rosenbrock, rosenbrock_grad, x0, "wolfe", 20, 5, 1e-5));
     put_x("x_cuda_bt", LBFGS_CUDA(rosenbrock, rosenbrock_grad, x0, 20, 5, 1e-5));
     std::printf("KEY C2 %a\n", C2);
+    // 8. dense quadratic (matrices.h form x'Ax + b'x) -> device dense objective
+    {
+        const int nd = 300;
+        vector<double> A((size_t)nd * nd), bv(nd), xd0(nd);
+        std::mt19937 gd(7);
+        std::uniform_real_distribution<> u(-1, 1);
+        for (int i = 0; i < nd; ++i)
+            for (int j = 0; j <= i; ++j) A[(size_t)i * nd + j] = A[(size_t)j * nd + i] = u(gd) / nd + (i == j ? 1.0 : 0.0);
+        for (double& v : bv) v = u(gd);
+        for (double& v : xd0) v = 2 * u(gd);
+        auto df = lbfgs_amd::dense_quadratic_function(A, bv);
+        auto dg = lbfgs_amd::dense_quadratic_gradient(A, bv);
+        vector<double> xd = LBFGS(df, dg, xd0, "backtracking", 5000, 5, 1e-6, false);
+        std::printf("KEY dense_objective %d\n", lbfgs_amd::last_objective());
+        put("dense_gnorm", vectorNorm(dg(xd)));
+        put_x("dense_x", xd);
+    }
     return 0;
 }

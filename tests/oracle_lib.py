@@ -16,7 +16,7 @@ ORACLE_DIR = os.path.join(ROOT, "oracle")
 ORACLE_SO = os.environ.get("ORACLE_LIB") or os.path.join(ORACLE_DIR, "_build", "liboracle.so")
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 
-OBJ = {"rosenbrock": 0, "quad_tridiag": 1, "quad_sep": 2, "host": 3}
+OBJ = {"rosenbrock": 0, "quad_tridiag": 1, "quad_sep": 2, "host": 3, "dense": 4}
 LS = {"backtracking": 0, "interpolation": 1, "wolfe": 2, "backtracking_wolfe": 3}
 SEQ, CANON = 0, 1
 PAIR, REV, FMA = 3, 4, 5  # alternative summation orders (horizon yardsticks)
@@ -181,6 +181,17 @@ def lbfgs(obj, x0, ls, m, maxit, tol, mode=CANON, consts=None, log_calls=False, 
                 iters=res.iters, status=STATUS[res.status], nf_total=res.nf, ng_total=res.ng,
                 flog=flog[:fn.value].copy(), glog=glog[:gn.value].reshape(-1, 3).copy(),
                 messages=msg.value.decode())
+
+
+_dense_refs = []
+
+
+def dense_set(A, b):
+    """Data of the "dense" objective (x'Ax + b'x); the arrays are kept alive here."""
+    A = np.ascontiguousarray(A, np.float64)
+    b = np.ascontiguousarray(b, np.float64)
+    _dense_refs[:] = [A, b]
+    lib().orc_dense_set(A.ctypes.data_as(C.c_void_p), b.ctypes.data_as(C.c_void_p))
 
 
 def load_golden(name):

@@ -25,6 +25,7 @@ struct lbk_ctx {
     double bytes;
     char err[256];
     double* scratch[6];
+    double *dA, *db; /* dense quadratic data */
 };
 
 struct lbk_group {
@@ -72,6 +73,8 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
 }
 void lbk_destroy(lbk_ctx* c) {
     if (!c) return;
+    free(c->dA);
+    free(c->db);
     for (int i = 0; i < 6; ++i) free(c->scratch[i]);
     free(c);
 }
@@ -395,6 +398,34 @@ int lbk_update(lbk_ctx* c, int op, double* out, const double* a, const double* b
 }
 int lbk_checksum(lbk_ctx* c, const double* x, uint64_t* c1, uint64_t* c2) {
     orc_checksum(x, c->geo.n, c1, c2);
+    return 0;
+}
+
+/* ---- dense quadratic objective (the oracle's dense_row order) ---- */
+int lbk_dense_set(lbk_ctx* c, const double* A, const double* b) {
+    const int64_t n = c->geo.n;
+    free(c->dA);
+    free(c->db);
+    c->dA = (double*)malloc(sizeof(double) * (size_t)(n * n));
+    c->db = (double*)malloc(sizeof(double) * (size_t)n);
+    if (!c->dA || !c->db) return -4;
+    memcpy(c->dA, A, sizeof(double) * (size_t)(n * n));
+    memcpy(c->db, b, sizeof(double) * (size_t)n);
+    return 0;
+}
+int lbk_dense_eval(lbk_ctx* c, const double* x, double* gout, int slot) {
+    CHECK_SLOT(slot);
+    if (!c->dA) return -1;
+    const int64_t n = c->geo.n;
+    double* t = c->scratch[4];
+    for (int64_t i = 0; i < n; ++i) {
+        const double r = dense_row(c->dA + i * n, x, n);
+        t[i] = x[i] * r + c->db[i] * x[i];
+        if (gout) gout[i] = 2.0 * r + c->db[i];
+    }
+    put(c, slot, 0, t, NULL, n, 1);
+    if (gout) put(c, slot, 1, gout, gout, n, 0);
+    ACCOUNT((double)n + 3.0);
     return 0;
 }
 

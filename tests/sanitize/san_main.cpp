@@ -189,6 +189,37 @@ static void host_callbacks() {
         }
 }
 
+// the dense quadratic objective (matrices.h form), every line search, against the oracle
+static void dense_objective() {
+    const int64_t n = 97;
+    std::vector<double> A((size_t)(n * n)), b(n);
+    for (int64_t i = 0; i < n; ++i) {
+        for (int64_t j = 0; j <= i; ++j)
+            A[(size_t)(i * n + j)] = A[(size_t)(j * n + i)] = std::sin(0.37 * (double)(i * 31 + j)) / (double)n +
+                                                              (i == j ? 1.5 : 0.0);
+        b[(size_t)i] = std::cos(0.11 * (double)i);
+    }
+    orc_dense_set(A.data(), b.data());
+    const auto x0 = x0_for(n, 11);
+    for (int ls = 0; ls < 4; ++ls) {
+        lbfgs_ctx* c = nullptr;
+        lbfgs_ctx_create(&c, n, 5, 0);
+        EXPECT(lbfgs_minimize(c, LBFGS_OBJ_DENSE_QUAD, nullptr, ls, nullptr, x0.data(), nullptr, 10, 1e-5, 0,
+                              nullptr) == LBFGS_ERR_STATE,
+               "dense without data");
+        EXPECT(lbfgs_set_dense_quadratic(c, A.data(), b.data()) == 0, "set dense");
+        std::vector<double> x(n);
+        lbfgs_result res;
+        const int st = lbfgs_minimize(c, LBFGS_OBJ_DENSE_QUAD, nullptr, ls, nullptr, x0.data(), x.data(), 200, 1e-5,
+                                      LBFGS_FLAG_QUIET | LBFGS_FLAG_TRACE, &res);
+        char tag[48];
+        std::snprintf(tag, sizeof tag, "dense ls=%d", ls);
+        EXPECT(st == LBFGS_STATUS_CONVERGED, "%s: status %d", tag, st);
+        if (st >= 0) compare(tag, c, st, x, res, oracle(ORC_OBJ_DENSE, ls, n, 5, 200, x0));
+        lbfgs_ctx_destroy(c);
+    }
+}
+
 // stepping API, standalone line search, primitives, error paths
 static void api_surface() {
     const int64_t n = 3000;
@@ -285,6 +316,7 @@ static void cxx_dropin() {
 int main() {
     device_objectives();
     host_callbacks();
+    dense_objective();
     api_surface();
     cxx_dropin();
     if (g_fail) {

@@ -79,6 +79,9 @@ def test_cxx_dropin_on_gpu(tmp_path):
     assert _ck(k["x_cuda_bt"]) == O.checksum(ob["x"])
     assert _fx(k["C2"]) == 0.9
     assert "Maximum iterations reached" in r.stdout and "Converged!" in r.stdout
+    # dense quadratic functors -> the device dense objective (LBFGS_OBJ_DENSE_QUAD), converged
+    assert k["dense_objective"] == "4"
+    assert _fx(k["dense_gnorm"]) < 1e-6
 
 
 @pytest.mark.gpu

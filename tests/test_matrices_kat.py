@@ -75,3 +75,15 @@ def test_gpu_host_objective_bit_exact_and_known_minimum(n, ls):
     assert np.array_equal(r["tr_f"].view(np.uint64), o["f"].view(np.uint64))
     assert np.array_equal(r["x"].view(np.uint64), o["x"].view(np.uint64))
     assert np.abs(r["x"] - xs).max() < 1e-4
+
+
+@pytest.mark.parametrize("ls", LINE_SEARCHES)
+@pytest.mark.parametrize("n", SIZES)
+def test_oracle_dense_objective_reaches_known_minimum(n, ls):
+    """The device dense-quadratic objective's restatement (ORC_OBJ_DENSE: rows of A x in the
+    device's lane-strided order) solves every matrices.h problem to the header's minimizer."""
+    A, b, xs, _, _ = problem(n)
+    O.dense_set(A, b)
+    r = O.lbfgs("dense", x0(n), ls, 5, 1000, 1e-5, mode=O.CANON)
+    assert r["status"] == "converged", r["messages"][-300:]
+    assert np.abs(r["x"] - xs).max() < 1e-4
