@@ -492,6 +492,7 @@ def main():
                        "passes": res["passes"]},
             "vector_free": vf,
             "config4_n1e9": c4,
+            "build": dict(zip(("library", "tree_sources", "current"), L.build_info())),
         }
         print(json.dumps(out), flush=True)
     D.close()

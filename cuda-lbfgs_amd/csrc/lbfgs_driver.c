@@ -215,6 +215,13 @@ void lbfgs_constants_cuda(lbfgs_constants* k) { /* parallel-implementation/const
     k->c2 = 0.7;
 }
 
+#ifndef LBFGS_SRC_HASH
+#define LBFGS_SRC_HASH "unknown"
+#endif
+const char* lbfgs_build_info(void) {
+    return "src=" LBFGS_SRC_HASH " built=" __DATE__ " " __TIME__ " arch=gfx950";
+}
+
 int lbfgs_unique_id(void* out128) { return lbk_unique_id(out128) == 0 ? 0 : LBFGS_ERR_RCCL; }
 
 int lbfgs_device_count(void) { return lbk_device_count(); }

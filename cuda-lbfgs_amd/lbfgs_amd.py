@@ -133,7 +133,7 @@ EXPORTED_SYMBOLS = [
     "lbfgs_dev_dot", "lbfgs_dev_norm", "lbfgs_dev_objective", "lbfgs_dev_trial",
     "lbfgs_dev_twoloop", "lbfgs_dev_elementwise", "lbfgs_line_search", "lbfgs_prof_enable",
     "lbfgs_prof_reset", "lbfgs_prof_get", "lbfgs_peer_handle", "lbfgs_peer_connect", "lbfgs_peer_enable",
-    "lbfgs_exchange_backend", "lbfgs_exchange_latency", "lbfgs_device_count", "lbfgs_set_dense_quadratic",
+    "lbfgs_exchange_backend", "lbfgs_exchange_latency", "lbfgs_device_count", "lbfgs_set_dense_quadratic", "lbfgs_build_info",
 ]
 PEER_HANDLE_BYTES = 64
 BACKENDS = {0: "single", 1: "rccl", 2: "xgmi", 3: "host-group"}
@@ -152,6 +152,30 @@ def shard_range(n, rank, world):
     if rc != 0:
         raise LbfgsError(f"cannot shard n={n} over {world} ranks")
     return lo.value, nl.value
+
+
+def build_info():
+    """(the library's embedded build string, the source hash of this tree, match?): a library
+    built from other sources than the ones beside it is stale."""
+    lib().lbfgs_build_info.restype = C.c_char_p
+    info = lib().lbfgs_build_info().decode()
+    return info, source_hash(), info.startswith("src=" + source_hash() + " ")
+
+
+def source_hash():
+    """sha256 over the library's sources, in cuda-lbfgs_amd/Makefile's SRC_HASH order."""
+    import glob
+    import hashlib
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    rel = []
+    for pat in ("csrc/*.hip", "csrc/*.h", "csrc/*.c", "csrc/*.cpp", "../include/*.h"):
+        rel += glob.glob(pat, root_dir=here)
+    h = hashlib.sha256()
+    for r in sorted(set(rel)):
+        with open(os.path.join(here, r), "rb") as fp:
+            h.update(fp.read())
+    return h.hexdigest()[:16]
 
 
 def device_count():
@@ -248,7 +272,7 @@ class Context:
         assert A.shape == (self.n, self.n) and b.shape == (self.n,)
         rc = lib().lbfgs_set_dense_quadratic(self.h, A.ctypes.data_as(C.c_void_p), b.ctypes.data_as(C.c_void_p))
         if rc != 0:
-            self._err("lbfgs_set_dense_quadratic", rc)
+            self._err("lbfgs_set_dense_quadratic", "lbfgs_build_info", rc)
 
     # ---- sharded runs: xGMI peer exchange ----
     def peer_handle(self):

@@ -142,6 +142,10 @@ typedef struct {
     int64_t grad_calls;
 } lbfgs_result;
 
+/* "src=<16 hex digits of sha256 over the library's sources> built=<date time> arch=gfx950":
+ * identifies the sources a loaded library was built from (build provenance) */
+const char* lbfgs_build_info(void);
+
 /* ---- context ---------------------------------------------------------------------------- */
 /* n: global problem size; m: history length (1..64); device: HIP device ordinal. */
 int lbfgs_ctx_create(lbfgs_ctx** out, int64_t n, int m, int device);

@@ -115,3 +115,10 @@ def test_vector_free_segment_factor_matches_oracle(n, F):
     lib.lbk_vf_factor.argtypes = [ctypes.c_int64]
     assert lib.lbk_vf_factor(n) == F
     assert O.vf_factor(n) == F
+
+
+def test_build_provenance():
+    """The library embeds the hash of the sources it was built from; it matches this tree."""
+    info, tree, ok = L.build_info()
+    assert ok, (info, tree)
+    assert "arch=gfx950" in info
