@@ -31,6 +31,21 @@
 #include "lbfgs_device.h"
 #include "lbfgs_hip.h"
 
+/* roctx ranges (SURVEY §5 tracing): "lbfgs iteration" around every iteration and "line search"
+ * around its trials, visible under rocprofv3 --marker-trace; no-ops without a tool attached.
+ * The product build defines LBFGS_ROCTX (cuda-lbfgs_amd/Makefile); other host builds of this
+ * file (the sanitizer job) compile them out. */
+#ifdef LBFGS_ROCTX
+struct hsa_agent_s; /* named in roctx.h's prototypes (C: declare before use) */
+struct ihipStream_t;
+#include <rocprofiler-sdk-roctx/roctx.h>
+#define TRACE_PUSH(name) roctxRangePushA(name)
+#define TRACE_POP() roctxRangePop()
+#else
+#define TRACE_PUSH(name) ((void)0)
+#define TRACE_POP() ((void)0)
+#endif
+
 #define MMAX 64
 
 /* result slots */
@@ -851,6 +866,19 @@ static int ls_wolfe(lbfgs_ctx* c, double gd, double* out) {
     return 0;
 }
 
+static int run_line_search(lbfgs_ctx* c, double gd, double* alpha) {
+    TRACE_PUSH("line search");
+    int rc;
+    switch (c->ls) {
+        case LBFGS_LS_BACKTRACKING: rc = ls_backtracking(c, gd, alpha); break;
+        case LBFGS_LS_INTERPOLATION: rc = ls_interpolation(c, gd, alpha); break;
+        case LBFGS_LS_WOLFE: rc = ls_wolfe(c, gd, alpha); break;
+        default: rc = ls_backtracking_wolfe(c, gd, alpha); break;
+    }
+    TRACE_POP();
+    return rc;
+}
+
 /* ------------------------------------------------------------------------------------------
  * Commit at step alpha: x_new, g_new, s, y and their reductions into tot[].
  * ---------------------------------------------------------------------------------------- */
@@ -1120,12 +1148,7 @@ static int iterate(lbfgs_ctx* c) {
     }
 
     double alpha = 0.0;
-    switch (c->ls) {
-        case LBFGS_LS_BACKTRACKING: rc = ls_backtracking(c, gd, &alpha); break;
-        case LBFGS_LS_INTERPOLATION: rc = ls_interpolation(c, gd, &alpha); break;
-        case LBFGS_LS_WOLFE: rc = ls_wolfe(c, gd, &alpha); break;
-        default: rc = ls_backtracking_wolfe(c, gd, &alpha); break;
-    }
+    rc = run_line_search(c, gd, &alpha);
     if (rc) return rc;
     if (c->flags & LBFGS_FLAG_TRACE) c->tr_a[c->tr_len - 1] = alpha;
 
@@ -1318,12 +1341,7 @@ static int iterate_vf(lbfgs_ctx* c) {
     c->spec_dphi = dgn;
 
     double alpha = 0.0;
-    switch (c->ls) {
-        case LBFGS_LS_BACKTRACKING: rc = ls_backtracking(c, gd, &alpha); break;
-        case LBFGS_LS_INTERPOLATION: rc = ls_interpolation(c, gd, &alpha); break;
-        case LBFGS_LS_WOLFE: rc = ls_wolfe(c, gd, &alpha); break;
-        default: rc = ls_backtracking_wolfe(c, gd, &alpha); break;
-    }
+    rc = run_line_search(c, gd, &alpha);
     if (rc) return rc;
     if (c->flags & LBFGS_FLAG_TRACE) c->tr_a[c->tr_len - 1] = alpha;
 
@@ -1527,7 +1545,9 @@ int lbfgs_solver_step(lbfgs_ctx* c, int max_steps, lbfgs_result* out) {
     c->h_max = -1;
     if (!c->finished) {
         for (int s = 0; s < max_steps; ++s) {
+            TRACE_PUSH("lbfgs iteration");
             int rc = c->vf ? iterate_vf(c) : iterate(c);
+            TRACE_POP();
             if (rc < 0) return rc;
             if (rc == 1) {
                 c->finished = 1;
