@@ -17,7 +17,7 @@
 //   <prefix>.ret.bin returned x: u64 c1, u64 c2, then (if n <= 200000) the n doubles
 //
 // usage: ref_lbfgs <obj> <n> <m> <method> <maxit> <tol> <seed> <lo> <hi> <prefix> <full_upto>
-//   obj ∈ {rosenbrock, quad_tridiag, quad_sep}
+//   obj ∈ {rosenbrock, quad_tridiag, quad_sep, stress_tiny_sq, stress_scaled_sq, stress_quartic_well}
 //   x0 ~ std::uniform_real_distribution<>(lo, hi) over std::mt19937(seed), as main.cpp:36-43.
 // usage: ref_lbfgs kat <n> <seed> <prefix>       (objective known-answer vectors)
 #include <chrono>
@@ -136,6 +136,46 @@ int main(int argc, char** argv) {
     } else if (obj == "quad_sep") {
         base_f = quadratic;
         base_g = quadratic_grad;
+    } else if (obj == "stress_tiny_sq" || obj == "stress_scaled_sq" || obj == "stress_quartic_well") {
+        // Stress objectives (ours, not the reference's) that drive the reference LBFGS() down
+        // its guard paths (lbfgs.cpp:102-124 invalid rho / gamma, :148-153 non-descent,
+        // :164-168 line-search failure). Written term by term, summed left to right, with the
+        // operand order tests/oracle_lib.py stress_objective() uses, so both sides agree bit
+        // for bit.
+        if (obj == "stress_tiny_sq") {  // x ~ 1e-155: s.y subnormal -> 1/(s.y) = inf
+            base_f = [](const vector<double>& x) {
+                double s = 0.0;
+                for (double v : x) s += v * v;
+                return s;
+            };
+            base_g = [](const vector<double>& x) {
+                vector<double> g(x.size());
+                for (size_t i = 0; i < x.size(); ++i) g[i] = 2.0 * x[i];
+                return g;
+            };
+        } else if (obj == "stress_scaled_sq") {  // gradients ~1e100: y.y overflows -> gamma = 0
+            base_f = [](const vector<double>& x) {
+                double s = 0.0;
+                for (double v : x) s += 1e100 * v * v;
+                return s;
+            };
+            base_g = [](const vector<double>& x) {
+                vector<double> g(x.size());
+                for (size_t i = 0; i < x.size(); ++i) g[i] = 2.0 * 1e100 * x[i];
+                return g;
+            };
+        } else {  // double well: the Wolfe search's quirky cubic leaves a negative step
+            base_f = [](const vector<double>& x) {
+                double s = 0.0;
+                for (double v : x) s += -0.2 * v * v + 0.0016 * v * v * v * v;
+                return s;
+            };
+            base_g = [](const vector<double>& x) {
+                vector<double> g(x.size());
+                for (size_t i = 0; i < x.size(); ++i) g[i] = 2.0 * -0.2 * x[i] + 4.0 * 0.0016 * x[i] * x[i] * x[i];
+                return g;
+            };
+        }
     } else {
         std::fprintf(stderr, "unknown objective %s\n", obj.c_str());
         return 2;

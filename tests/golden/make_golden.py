@@ -46,6 +46,20 @@ CASES = {
     "rosen_n4097_m7_interp": ("rosenbrock", 4097, 7, "interpolation", 150, 1e-5, 7, -2.0, 2.0, 2),
 }
 
+# Guard paths of lbfgs.cpp driven by our own stress objectives (oracle/ref_driver.cpp), run by
+# the reference itself: invalid rho + non-descent + skipped updates (tiny scale, tol 0), invalid
+# gamma (y.y overflow), line-search failure (Wolfe on a double well).
+STRESS = {
+    "stress_tiny_sq_bt": ("stress_tiny_sq", 10, 3, "backtracking", 30, 0.0, 42, -1e-155, 1e-155, 0),
+    "stress_tiny_sq_interp": ("stress_tiny_sq", 10, 3, "interpolation", 30, 0.0, 42, -1e-155, 1e-155, 0),
+    "stress_tiny_sq_wolfe": ("stress_tiny_sq", 10, 3, "wolfe", 30, 0.0, 42, -1e-155, 1e-155, 0),
+    "stress_tiny_sq_btw": ("stress_tiny_sq", 10, 3, "backtracking_wolfe", 30, 0.0, 42, -1e-155, 1e-155, 0),
+    "stress_scaled_sq_bt": ("stress_scaled_sq", 10, 3, "backtracking", 4, 1e-5, 42, -1e-10, 1e-10, 0),
+    "stress_quartic_well_wolfe": ("stress_quartic_well", 8, 3, "wolfe", 50, 1e-8, 42, -1.3, -1.2, 1),
+    "stress_quartic_well_n1_wolfe": ("stress_quartic_well", 1, 3, "wolfe", 50, 1e-8, 42, -1.5, -1.0, 1),
+}
+CASES.update(STRESS)
+
 KATS = {"kat_n1000": (1000, 7), "kat_n5": (5, 3)}
 
 

@@ -203,7 +203,29 @@ def load_golden(name):
 
 def golden_cases():
     return sorted(f[:-5] for f in os.listdir(GOLDEN)
-                  if f.endswith(".json") and not f.startswith("kat_") and f != "horizons.json")
+                  if f.endswith(".json") and not f.startswith(("kat_", "stress_")) and f != "horizons.json")
+
+
+def stress_cases():
+    """Guard-path goldens: the reference run on our stress objectives (oracle/ref_driver.cpp)."""
+    return sorted(f[:-5] for f in os.listdir(GOLDEN) if f.startswith("stress_") and f.endswith(".json"))
+
+
+def _seqsum(t):
+    # left-to-right, from 0.0, as the reference's `for (...) sum += term`
+    return float(np.cumsum(t)[-1]) if len(t) else 0.0
+
+
+def stress_objective(name):
+    """(f, grad) of a stress objective, operand for operand as oracle/ref_driver.cpp writes it."""
+    if name == "stress_tiny_sq":
+        return (lambda x: _seqsum(x * x)), (lambda x: 2.0 * x)
+    if name == "stress_scaled_sq":
+        return (lambda x: _seqsum(1e100 * x * x)), (lambda x: 2.0 * 1e100 * x)
+    if name == "stress_quartic_well":
+        return ((lambda x: _seqsum(-0.2 * x * x + 0.0016 * x * x * x * x)),
+                (lambda x: 2.0 * -0.2 * x + 4.0 * 0.0016 * x * x * x))
+    raise KeyError(name)
 
 
 def twoloop(g, S, Y, mode=CANON):
