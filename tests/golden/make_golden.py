@@ -57,6 +57,11 @@ STRESS = {
     "stress_scaled_sq_bt": ("stress_scaled_sq", 10, 3, "backtracking", 4, 1e-5, 42, -1e-10, 1e-10, 0),
     "stress_quartic_well_wolfe": ("stress_quartic_well", 8, 3, "wolfe", 50, 1e-8, 42, -1.3, -1.2, 1),
     "stress_quartic_well_n1_wolfe": ("stress_quartic_well", 1, 3, "wolfe", 50, 1e-8, 42, -1.5, -1.0, 1),
+    # the same guards through a benchmark objective (the device's fused path): the tridiagonal
+    # quadratic at the 1e-155 scale (invalid rho; Wolfe: line-search failure)
+    "stress_qtri_tiny_bt": ("quad_tridiag", 10, 3, "backtracking", 30, 0.0, 42, -1e-155, 1e-155, 0),
+    "stress_qtri_tiny_wolfe": ("quad_tridiag", 10, 3, "wolfe", 30, 0.0, 42, -1e-155, 1e-155, 0),
+    "stress_qtri_tiny_btw": ("quad_tridiag", 10, 3, "backtracking_wolfe", 30, 0.0, 42, -1e-155, 1e-155, 0),
 }
 CASES.update(STRESS)
 

@@ -12,11 +12,15 @@ import oracle_lib as O
 @pytest.mark.parametrize("name", O.stress_cases())
 def test_oracle_reproduces_reference_guard_paths(name):
     meta, g = O.load_golden(name)
-    f, grad = O.stress_objective(meta["objective"])
     x0 = O.x0_uniform(meta["n"], meta["seed"], meta["lo"], meta["hi"])
     with np.errstate(all="ignore"):
-        o = O.lbfgs("host", x0, meta["method"], meta["m"], meta["maxit"], meta["tol"], mode=O.SEQ, f=f, grad=grad,
-                    log_calls=True)
+        if meta["objective"] in O.OBJ:  # a benchmark objective at a stress scale
+            o = O.lbfgs(meta["objective"], x0, meta["method"], meta["m"], meta["maxit"], meta["tol"], mode=O.SEQ,
+                        log_calls=True)
+        else:
+            f, grad = O.stress_objective(meta["objective"])
+            o = O.lbfgs("host", x0, meta["method"], meta["m"], meta["maxit"], meta["tol"], mode=O.SEQ, f=f,
+                        grad=grad, log_calls=True)
     assert np.array_equal(o["flog"].view(np.uint64), g["f_calls"].view(np.uint64))
     assert np.array_equal(o["glog"][:, :2], g["grad_c"])
     assert np.array_equal(o["glog"][:, 2].view(np.float64).view(np.uint64), g["grad_norm"].view(np.uint64))
