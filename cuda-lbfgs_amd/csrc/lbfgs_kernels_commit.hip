@@ -77,8 +77,8 @@ int lbk_trials(lbk_ctx* c, int obj, int dmode, const double* x, const double* ds
     OBJ_DISPATCH(obj, {                                                                                    \
         OpTrials<O_, DM, NCC, DP, NT_> op{x, da, {}, c->geo.n, c->geo.n_loc};                               \
         for (int j = 0; j < NCC; ++j) op.a[j] = alphas[j];                                                   \
-        hipLaunchKernelGGL((k_trials<O_, DM, NCC, DP, NT_>), dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, x, \
-                           da, g, r, op);                                                                  \
+        hipLaunchKernelGGL((k_trials<O_, DM, NCC, DP, NT_>), dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, g, r, \
+                           op);                                                                            \
     })
 #define TRIALS_DM(DM)                                                   \
     if (nc == 1 && dphi) {                                              \

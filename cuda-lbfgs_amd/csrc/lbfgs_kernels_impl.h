@@ -1248,16 +1248,13 @@ struct OpTrials {
 };
 
 template <int OBJ, int DMODE, int NC, bool DPHI, bool NT>
-__global__ __launch_bounds__(LB_BLOCK) void k_trials(const double* __restrict__ x, DirArgs da, Geo geo, Red red,
-                                                     OpTrials<OBJ, DMODE, NC, DPHI, NT> op) {
-    if (DMODE == LBK_D_TWOLOOP) {
-        const double beta = da.rho * src_total(da.pb, geo);
-        const double alph = da.rho * slot_total(da.pa);
+__global__ __launch_bounds__(LB_BLOCK) void k_trials(Geo geo, Red red, OpTrials<OBJ, DMODE, NC, DPHI, NT> op) {
+    if (DMODE == LBK_D_TWOLOOP) {  // alpha - beta of the last second-loop update (as k_commit)
+        const double beta = op.da.rho * src_total(op.da.pb, geo);
+        const double alph = op.da.rho * slot_total(op.da.pa);
         op.da.coef = alph - beta;
     }
     run_pass_halo<OpTrials<OBJ, DMODE, NC, DPHI, NT>, OpTrials<OBJ, DMODE, NC, DPHI, NT>::K>(op, geo, red);
-    (void)x;
-    (void)da;
 }
 
 // ---------------------------------------------------------------------------------------

@@ -53,3 +53,15 @@ def test_guard_paths_match_reference(name, refcalls):
     assert np.array_equal(bits(r["x"]), bits(o["x"]))
     if refcalls:
         assert r["f_calls"] == len(g["f_calls"]) and r["grad_calls"] == len(g["grad_c"])
+    if device:  # the unfused launch structure and one trial pass per step reach the same guards
+        for kw, env in ((dict(unfused=True), None), ({}, "0")):
+            if env is not None:
+                os.environ["LBFGS_BATCH"] = env
+            try:
+                with np.errstate(all="ignore"), L.Context(n, meta["m"]) as c:
+                    r2 = c.minimize(meta["objective"], x0, meta["method"], meta["maxit"], tolerance=meta["tol"],
+                                    trace=True, **kw)
+            finally:
+                os.environ.pop("LBFGS_BATCH", None)
+            assert r2["messages"] == meta["stdout"]
+            assert np.array_equal(bits(r2["tr_f"]), bits(o["f"])) and np.array_equal(bits(r2["x"]), bits(o["x"]))
