@@ -21,6 +21,7 @@ import json
 import os
 import platform
 import shutil
+import struct
 import subprocess
 import sys
 import tempfile
@@ -304,6 +305,33 @@ def measure(a, D, n, x0, dev, rank, world, uid, unfused=False, vector_free=False
     return T, res, prof, bytes_all, done_steps, (backend, lat)
 
 
+def shard_check(a, D, n, x0, dev, rank, world, res):
+    """Sharded runs: rank 0 repeats the measured solve on its GPU alone (world = 1, the same
+    fill, warm-up and timed step counts) and compares f and |g| bit for bit with the sharded
+    result. The canonical reduction order is a function of n only, so every
+    exchange path must reproduce the one-GPU trajectory exactly; this checks it on the node the
+    scaling series runs on. The other ranks wait at a barrier."""
+    out = None
+    if rank == 0:
+        try:
+            t0 = time.perf_counter()
+            with L.Context(n, a.history, device=dev) as c:
+                c.init(a.objective, x0, a.line_search, tolerance=1e-5, unfused=a.unfused,
+                       vector_free=a.vector_free)
+                c.step(a.history)
+                c.step(a.warmup)
+                r1 = c.step(a.steps)
+            bits = lambda v: struct.pack("<d", v).hex()  # noqa: E731
+            same = bits(r1["f"]) == bits(res["f"]) and bits(r1["gnorm"]) == bits(res["gnorm"])
+            out = {"one_gpu_f": r1["f"], "one_gpu_gnorm": r1["gnorm"], "iterations": r1["iterations"],
+                   "bit_identical": bool(same and r1["iterations"] == res["iterations"]),
+                   "seconds": round(time.perf_counter() - t0, 2)}
+        except L.LbfgsError as e:
+            out = {"error": str(e)}
+    D.barrier()
+    return out
+
+
 def config4(a, D, dev, rank, world):
     """BASELINE configs[4]: Rosenbrock n = 1e9, m = 10, sharded over 8 GPUs, default mode, the
     xGMI peer exchange (no RCCL communicator: a rank that fails early cannot strand the others in
@@ -407,6 +435,7 @@ def main():
         dev = dev % ndev
     T, res, prof, bytes_all, done_steps, (backend, xlat) = measure(a, D, n, x0, dev, rank, world, uid,
                                                   unfused=a.unfused, vector_free=a.vector_free)
+    check = shard_check(a, D, n, x0, dev, rank, world, res) if world > 1 else None
     # the opt-in vector-free mode alongside the default (outside the bit-parity contract with
     # the reference's operation order); sharded runs need a fresh RCCL id
     vf = None
@@ -490,6 +519,7 @@ def main():
             "solver": {"status": res["status"], "f": res["f"], "gnorm": res["gnorm"],
                        "trials_f": res["trials_f"], "commits": res["commits"],
                        "passes": res["passes"]},
+            "shard_check": check,
             "vector_free": vf,
             "config4_n1e9": c4,
             "build": dict(zip(("library", "tree_sources", "current"), L.build_info())),

@@ -198,10 +198,33 @@ int lbk_vf_ghost_init(lbk_ctx* c, double* x, double* g, int wslot);
  * commit at a0 into slot_c, in one single-workgroup launch; the same slot contents and vectors as
  * the multi-launch sequence. S/Y in ring order (oldest first). */
 int lbk_small_ok(const lbk_ctx* c, int h);
+/* Speculative launch of the NEXT iteration (cooperative form, one rank, host-mirrored slots):
+ * enqueued behind the current iteration's launch before the host has read its results. The
+ * kernel's prologue restates, from the current iteration's commit slot `prev_slot`, every host
+ * decision between the two iterations - the line search `ls` (LBFGS_LS_* numbering) takes the
+ * first trial a0 (f at x is `fx`), the pair is stored (s.y > 0), the next iteration has not
+ * converged (|g| >= tol), its rho and gamma are valid - and computes the newest pair's rho and
+ * gamma itself (rho[h-1] and gamma are ignored). If any test fails no workgroup writes anything.
+ * `chain_epoch` (0: none) is the launch this one follows when that was speculative as well: its
+ * device verdict must be "went". */
+typedef struct {
+    int prev_slot, ls;
+    double fx, c1, c2, tol;
+    unsigned long long chain_epoch;
+} lbk_spec;
+int lbk_small_spec_ok(const lbk_ctx* c, int h);
+/* *epoch: the launch's id for lbk_small_fetch (0: not a cooperative host-mirrored launch) */
 int lbk_small_iter(lbk_ctx* c, int obj, int h, const double* g, double* q, double* r, const double* const* S,
                    const double* const* Y, const double* rho, double gamma, int p0_ref, double a0, const double* x,
                    double* xn, double* gn, double* so, double* yo, int slot_p0, int slot_a0, int slot_b0,
-                   int slot_c);
+                   int slot_c, const lbk_spec* spec, unsigned long long* epoch);
+/* waits for launch `epoch` to finish its commit (spinning on a pinned word, no stream
+ * synchronisation: a speculative launch queued behind it keeps running), then the fixed-order
+ * totals of slot_c. *went (may be NULL): 0 if a speculative launch found a test failing (it wrote
+ * nothing and its reservations are released; the slot is stale); *rho / *gamma: the values a
+ * speculative launch computed. epoch 0: lbk_fetch. */
+int lbk_small_fetch(lbk_ctx* c, unsigned long long epoch, int slot, int ncomp, double* totals, int* went,
+                    double* rho, double* gamma);
 
 /* unfused mode: out = op(a, b) with device-side coefficients (see k_update) */
 enum { LBK_U_AXPY_Q = 0, LBK_U_AXPY_R, LBK_U_SCALE, LBK_U_NEG, LBK_U_SUB, LBK_U_POINT };

@@ -129,6 +129,22 @@ struct lbfgs_ctx {
     /* f at the backtracking candidates a0 beta, a0 beta^2, reduced by the first commit pass */
     double vf_cand[LBK_VF_NA], vf_cand_f[LBK_VF_NA];
     int vf_cand_valid;
+    /* speculative next iteration (small n, cooperative form): the launch of
+     * iteration sp_k queued behind iteration sp_k - 1's before the host has read that one's
+     * results, with the arguments the host will pass if the first trial is taken and the pair
+     * stored (the kernel checks exactly that, see lbk_spec) */
+    int spec_on;                  /* LBFGS_SPEC (default 1) */
+    int steps_left;               /* iterations still to run in this lbfgs_solver_step call */
+    unsigned long long cur_epoch; /* this iteration's cooperative launch (0: none) */
+    int cur_spec;                 /* ... which was a speculative one, adopted */
+    double cur_rho, cur_gamma;    /* the host's rho of the newest pair and gamma, this iteration */
+    int cur_p0;
+    int sp_pend, sp_k, sp_h, sp_free, sp_p0, sp_cslot, sp_hostgo;
+    int sp_ring[MMAX + 1];
+    double *sp_x, *sp_xn, *sp_g, *sp_gn;
+    double sp_rho[MMAX];
+    unsigned long long sp_epoch;
+    int64_t sp_adopted, sp_dropped;
     /* counters */
     int64_t trials_f, trials_fg, commits, passes;
     int h_min, h_max; /* pairs stored at the top of the iterations of the current call */
@@ -233,6 +249,13 @@ void lbfgs_constants_cuda(lbfgs_constants* k) { /* parallel-implementation/const
 #ifndef LBFGS_SRC_HASH
 #define LBFGS_SRC_HASH "unknown"
 #endif
+int lbfgs_spec_stats(const lbfgs_ctx* c, int64_t* adopted, int64_t* dropped) {
+    if (!c) return LBFGS_ERR_BAD_ARG;
+    if (adopted) *adopted = c->sp_adopted;
+    if (dropped) *dropped = c->sp_dropped;
+    return 0;
+}
+
 const char* lbfgs_build_info(void) {
     return "src=" LBFGS_SRC_HASH " built=" __DATE__ " " __TIME__ " arch=gfx950";
 }
@@ -972,6 +995,140 @@ static void note_h(lbfgs_ctx* c) {
     if (c->h > c->h_max) c->h_max = c->h;
 }
 
+/* a queued speculative launch the host does not take: wait for its record. It either did not go
+ * (nothing written, reservations released) or ran on buffers the host no longer reads - which
+ * holds only if the host also took the first trial and stored the pair in the iteration before
+ * (the kernel's other tests - convergence, rho, gamma - can only differ by a rounding the
+ * host then handles itself). */
+static int spec_drop(lbfgs_ctx* c) {
+    if (!c->sp_pend) return 0;
+    c->sp_pend = 0;
+    c->sp_dropped++;
+    double t[1];
+    int went = 0;
+    DEVNC(lbk_small_fetch(c->dev, c->sp_epoch, c->sp_cslot, 1, t, &went, NULL, NULL));
+    if (went && !c->sp_hostgo) {
+        snprintf(c->err, sizeof c->err, "speculative iteration %d ran where the host stopped", c->sp_k);
+        return LBFGS_ERR_STATE;
+    }
+    return 0;
+}
+
+/* queue iteration k + 1 behind iteration k's cooperative launch, assuming the line search takes
+ * a0 and the pair is stored: the ring then drops its oldest pair (h = m) or grows, the new pair
+ * is the current free one, x/xn and g/gn swap, and alpha_{h-1} of the first loop is the commit's
+ * s.g (component SG) */
+static int spec_next(lbfgs_ctx* c) {
+    const int m = c->m, h = c->h, k = c->k;
+    if (!c->spec_on || c->steps_left <= 0 || c->cur_epoch == 0 || c->K.initial_step < 1e-10) return 0;
+    const int h1 = h < m ? h + 1 : m;
+    if (!lbk_small_spec_ok(c->dev, h1)) return 0;
+    int ring1[MMAX + 1], free1;
+    if (h >= m) {
+        for (int i = 0; i + 1 < m; ++i) ring1[i] = c->ring[i + 1];
+        ring1[m - 1] = c->free_pair;
+        free1 = c->ring[0];
+    } else {
+        for (int i = 0; i < h; ++i) ring1[i] = c->ring[i];
+        ring1[h] = c->free_pair;
+        free1 = h + 1;
+    }
+    const double* Sr[MMAX];
+    const double* Yr[MMAX];
+    double rho1[MMAX];
+    for (int i = 0; i < h1; ++i) {
+        Sr[i] = c->S[ring1[i]];
+        Yr[i] = c->Y[ring1[i]];
+        rho1[i] = i + 1 < h1 ? 1.0 / c->sy[ring1[i]] : 0.0; /* the new pair's: the kernel's */
+    }
+    const int cslot = SLOT_COMMIT0 + (k & 1), cslot1 = SLOT_COMMIT0 + ((k + 1) & 1);
+    const int p01 = REF(cslot, LBK_C_SG);
+    lbk_spec sp;
+    sp.prev_slot = cslot;
+    sp.ls = c->ls;
+    sp.fx = c->f_cur;
+    sp.c1 = c->K.c1;
+    sp.c2 = c->K.c2;
+    sp.tol = c->tol;
+    sp.chain_epoch = c->cur_spec ? c->cur_epoch : 0;
+    DEV(lbk_small_iter(c->dev, c->obj, h1, c->gn, c->q, c->r, Sr, Yr, rho1, 0.0, p01, c->K.initial_step, c->xn,
+                       c->x, c->g, c->S[free1], c->Y[free1], SLOT_P0, SLOT_A0, SLOT_B0(m), cslot1, &sp,
+                       &c->sp_epoch));
+    c->sp_pend = 1;
+    c->sp_k = k + 1;
+    c->sp_h = h1;
+    memcpy(c->sp_ring, ring1, sizeof(int) * (size_t)h1);
+    c->sp_free = free1;
+    c->sp_p0 = p01;
+    c->sp_cslot = cslot1;
+    c->sp_x = c->xn;
+    c->sp_xn = c->x;
+    c->sp_g = c->gn;
+    c->sp_gn = c->g;
+    memcpy(c->sp_rho, rho1, sizeof(double) * (size_t)h1);
+    c->sp_hostgo = 0;
+    return 0;
+}
+
+/* this iteration's cooperative (or single-workgroup) launch: the two-loop passes and the commit at a0 */
+static int small_launch(lbfgs_ctx* c, const double* rho, const double* const* Sr, const double* const* Yr,
+                        double gamma, int p0_ref) {
+    DEV(lbk_small_iter(c->dev, c->obj, c->h, c->g, c->q, c->r, Sr, Yr, rho, gamma, p0_ref, c->K.initial_step,
+                       c->x, c->xn, c->gn, c->S[c->free_pair], c->Y[c->free_pair], SLOT_P0, SLOT_A0,
+                       SLOT_B0(c->m), SLOT_COMMIT0 + (c->k & 1), NULL, &c->cur_epoch));
+    c->cur_spec = 0;
+    return 0;
+}
+
+/* the commit totals of this iteration's small launch. An adopted speculative launch that did not
+ * go (its tests disagreed with the host's, possible only through a rounding difference: never
+ * seen) is replaced by an ordinary launch; the one queued behind it was chained to it and did not
+ * go either. One that went with another rho or gamma than the host's cannot be replaced (the
+ * launch behind it has overwritten this iteration's x) and fails the solve. */
+static int small_fetch(lbfgs_ctx* c, int cslot, double* tot) {
+    int went = 1;
+    double vr = 0.0, vg = 0.0;
+    DEVNC(lbk_small_fetch(c->dev, c->cur_epoch, cslot, 7, tot, &went, &vr, &vg));
+    if (!c->cur_spec) return 0;
+    if (!went) {
+        c->sp_pend = 0;
+        c->sp_dropped++;
+        double rho[MMAX];
+        const double* Sr[MMAX];
+        const double* Yr[MMAX];
+        for (int i = 0; i < c->h; ++i) {
+            rho[i] = 1.0 / c->sy[c->ring[i]];
+            Sr[i] = c->S[c->ring[i]];
+            Yr[i] = c->Y[c->ring[i]];
+        }
+        int rc = small_launch(c, rho, Sr, Yr, c->cur_gamma, c->cur_p0);
+        if (rc) return rc;
+        DEVNC(lbk_small_fetch(c->dev, c->cur_epoch, cslot, 7, tot, NULL, NULL, NULL));
+        return 0;
+    }
+    if (memcmp(&vr, &c->cur_rho, sizeof vr) != 0 || memcmp(&vg, &c->cur_gamma, sizeof vg) != 0) {
+        snprintf(c->err, sizeof c->err, "speculative iteration %d: device rho/gamma %.17g/%.17g, host %.17g/%.17g",
+                 c->k, vr, vg, c->cur_rho, c->cur_gamma);
+        return LBFGS_ERR_STATE;
+    }
+    c->sp_adopted++;
+    return 0;
+}
+
+/* the queued launch is this iteration's exactly (same history, buffers, slots and the host's
+ * rho of the older pairs; rho and gamma of the newest pair are compared when its record is read) */
+static int spec_matches(const lbfgs_ctx* c, int h, const double* rho, int p0_ref) {
+    if (!c->sp_pend || c->sp_k != c->k || c->sp_h != h || c->sp_free != c->free_pair || c->sp_p0 != p0_ref ||
+        c->sp_cslot != SLOT_COMMIT0 + (c->k & 1) || c->sp_x != c->x || c->sp_xn != c->xn || c->sp_g != c->g ||
+        c->sp_gn != c->gn)
+        return 0;
+    for (int i = 0; i < h; ++i)
+        if (c->sp_ring[i] != c->ring[i]) return 0;
+    for (int i = 0; i + 1 < h; ++i)
+        if (memcmp(&c->sp_rho[i], &rho[i], sizeof(double)) != 0) return 0;
+    return 1;
+}
+
 static int iterate(lbfgs_ctx* c) {
     const int k = c->k, m = c->m, h = c->h;
     const double gnorm = sqrt(c->gg);
@@ -984,7 +1141,8 @@ static int iterate(lbfgs_ctx* c) {
     if (gnorm < c->tol) { /* :80-84 */
         say(c, "Converged!\n");
         c->status = LBFGS_STATUS_CONVERGED;
-        return 1;
+        rc = spec_drop(c);
+        return rc ? rc : 1;
     }
     note_h(c);
 
@@ -992,6 +1150,8 @@ static int iterate(lbfgs_ctx* c) {
     int dmode = LBK_D_NEG_G;
     int small_done = 0;
     const int small = !ext_obj(c) && !c->unfused && c->geo->world == 1 && lbk_small_ok(c->dev, h);
+    c->cur_epoch = 0;
+    c->cur_spec = 0;
     c->d_ready = 0;
     c->spec_valid = 0;
     c->cand_valid = 0;
@@ -1033,9 +1193,22 @@ static int iterate(lbfgs_ctx* c) {
             }
             const int top = c->ring[h - 1];
             const int p0_ref = c->sg_valid ? c->sg_ref : -1;
-            DEV(lbk_small_iter(c->dev, c->obj, h, c->g, c->q, c->r, Sr, Yr, rho, gamma, p0_ref, c->K.initial_step,
-                               c->x, c->xn, c->gn, c->S[c->free_pair], c->Y[c->free_pair], SLOT_P0, SLOT_A0,
-                               SLOT_B0(m), SLOT_COMMIT0 + (k & 1)));
+            c->cur_rho = rho[h - 1];
+            c->cur_gamma = gamma;
+            c->cur_p0 = p0_ref;
+            if (spec_matches(c, h, rho, p0_ref)) { /* already queued behind the last iteration */
+                c->sp_pend = 0;
+                c->cur_epoch = c->sp_epoch;
+                c->cur_spec = 1;
+            } else {
+                rc = spec_drop(c);
+                if (rc) return rc;
+                rc = small_launch(c, rho, Sr, Yr, gamma, p0_ref);
+                if (rc) return rc;
+            }
+            /* the next iteration, queued before this one's results are read */
+            rc = spec_next(c);
+            if (rc) return rc;
             c->rho_last = rho[h - 1];
             c->ref_b_last = REF(SLOT_B0(m) + h - 1, 0);
             c->ref_a_last = p0_ref >= 0 ? p0_ref : REF(SLOT_P0, 0); /* alpha_{h-1}: s_{h-1} . g */
@@ -1086,6 +1259,10 @@ static int iterate(lbfgs_ctx* c) {
             c->s_last_pair = top;
         }
     }
+    if (c->sp_pend && c->sp_k == k) { /* queued for this iteration, which took another path */
+        rc = spec_drop(c);
+        if (rc) return rc;
+    }
     c->dmode = dmode;
     if (c->unfused && dmode == LBK_D_BUF) c->d_ready = 1;
 
@@ -1109,7 +1286,8 @@ static int iterate(lbfgs_ctx* c) {
         /* the backtracking search's second step, f reduced by the same pass (line_search.cpp:26) */
         const double cand = (c->batch && c->ls == LBFGS_LS_BACKTRACKING) ? c->a0 * c->K.backtracking_alpha : 0.0;
         if (small_done) { /* the commit at a0 ran inside lbk_small_iter */
-            DEVNC(lbk_fetch(c->dev, cslot, 7, tot));
+            rc = small_fetch(c, cslot, tot);
+            if (rc) return rc;
             c->commits++;
         } else {
             rc = commit(c, c->dmode, c->a0, cslot, tot, cand);
@@ -1164,6 +1342,7 @@ static int iterate(lbfgs_ctx* c) {
         if (rc) return rc;
     }
     c->f_cur = tot[LBK_C_F];
+    c->sp_hostgo = alpha == c->a0 && tot[LBK_C_SY] > 0; /* what a queued launch of k + 1 assumed */
     if (alpha < 1e-10) { /* :164-168 */
         say(c, "Warning: Line search failed at iteration %d\n", k);
         c->status = LBFGS_STATUS_LS_FAILED;
@@ -1442,6 +1621,19 @@ int lbfgs_solver_init(lbfgs_ctx* c, int objective, const lbfgs_host_fn* cb, int 
     host_invalidate(c);
     c->hxx_valid = 0;
     c->cb_f = c->cb_g = 0;
+    {
+        const int rc = spec_drop(c);
+        if (rc) return rc;
+    }
+    /* speculative next iteration at small n (LBFGS_SPEC=0: off; the same iterates either way) */
+    c->spec_on = 1;
+    {
+        const char* e = getenv("LBFGS_SPEC");
+        if (e) c->spec_on = atoi(e) != 0;
+    }
+    c->cur_epoch = 0;
+    c->cur_spec = 0;
+    c->sp_adopted = c->sp_dropped = 0;
     c->unfused = (flags & LBFGS_FLAG_UNFUSED) != 0;
     c->batch = 1;
     {
@@ -1545,15 +1737,21 @@ int lbfgs_solver_step(lbfgs_ctx* c, int max_steps, lbfgs_result* out) {
     c->h_max = -1;
     if (!c->finished) {
         for (int s = 0; s < max_steps; ++s) {
+            c->steps_left = max_steps - s - 1;
             TRACE_PUSH("lbfgs iteration");
             int rc = c->vf ? iterate_vf(c) : iterate(c);
             TRACE_POP();
-            if (rc < 0) return rc;
+            if (rc < 0) {
+                (void)spec_drop(c);
+                return rc;
+            }
             if (rc == 1) {
                 c->finished = 1;
                 break;
             }
         }
+        int rc = spec_drop(c);
+        if (rc) return rc;
     }
     fill_result(c, out, t0, b0);
     return c->finished ? c->status : LBFGS_STATUS_RUNNING;

@@ -166,12 +166,19 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
     CK(hipMemset(c->wslots, 0, sizeof(double) * LBK_NWSLOTS * LBK_WSLOT));
     CK(hipMemset(c->cnt, 0, sizeof(unsigned) * 16));
     CK(hipMemset(c->slots, 0, sizeof(double) * LBK_NSLOTS * LBK_SLOT));
-    CK(hipMalloc(&c->coop_bar, sizeof(unsigned long long)));
-    CK(hipMemset(c->coop_bar, 0, sizeof(unsigned long long)));
-    CK(hipMalloc(&c->coop_redge, sizeof(double) * 2 * LBK_COOP_SEGMAX));
+    {
+        const size_t llb = sizeof(unsigned long long) * 2 * LBK_LL_COMPS * LBK_LL_SEGS * 2;
+        CK(hipMalloc(&c->coop_ll, llb));
+        CK(hipMemset(c->coop_ll, 0, llb));  // tag 0: no pass (sequence numbers start at 1)
+    }
     CK(hipHostMalloc((void**)&c->coop_err_h, sizeof(unsigned), hipHostMallocMapped | hipHostMallocCoherent));
     *c->coop_err_h = 0;
     CK(hipHostGetDevicePointer((void**)&c->coop_err_d, c->coop_err_h, 0));
+    CK(hipHostMalloc((void**)&c->sp_h, sizeof(unsigned long long) * 20, hipHostMallocMapped | hipHostMallocCoherent));
+    memset(c->sp_h, 0, sizeof(unsigned long long) * 20);
+    CK(hipHostGetDevicePointer((void**)&c->sp_dh, c->sp_h, 0));
+    CK(hipMalloc(&c->sp_vd, sizeof(unsigned long long) * 4));
+    CK(hipMemset(c->sp_vd, 0, sizeof(unsigned long long) * 4));
     {
         int khz = 0;
         CK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device));
@@ -242,9 +249,10 @@ void lbk_destroy(lbk_ctx* c) {
     lbk_xgmi_destroy(c->xg);
     if (c->d_ckslot) (void)hipFree(c->d_ckslot);
     (void)hipFree(c->partials);
-    (void)hipFree(c->coop_bar);
-    (void)hipFree(c->coop_redge);
+    (void)hipFree(c->coop_ll);
     if (c->coop_err_h) (void)hipHostFree(c->coop_err_h);
+    if (c->sp_h) (void)hipHostFree(c->sp_h);
+    if (c->sp_vd) (void)hipFree(c->sp_vd);
     (void)hipFree(c->cnt);
     (void)hipFree(c->slots);
     (void)hipHostFree(c->h_slots);
@@ -500,8 +508,9 @@ int lbk_elementwise(lbk_ctx* c, int op, double* out, const double* a, const doub
 int lbk_small_iter(lbk_ctx* c, int obj, int h, const double* g, double* q, double* r, const double* const* S,
                    const double* const* Y, const double* rho, double gamma, int p0_ref, double a0, const double* x,
                    double* xn, double* gn, double* so, double* yo, int slot_p0, int slot_a0, int slot_b0,
-                   int slot_c) {
-    if (!lbk_small_ok(c, h)) return -1;
+                   int slot_c, const lbk_spec* spec, unsigned long long* epoch) {
+    if (epoch) *epoch = 0;
+    if (!lbk_small_ok(c, h) || (spec && !lbk_small_spec_ok(c, h))) return -1;
     SmallArgs a;
     memset(&a, 0, sizeof a);
     a.h = h;
@@ -536,15 +545,39 @@ int lbk_small_iter(lbk_ctx* c, int obj, int h, const double* g, double* q, doubl
     // pass, 3 for mid, 8 for the commit)
     const double vec = (p0_ref >= 0 ? 0.0 : 2.0) + 4.0 * (h - 1) + 3.0 + 4.0 * (h - 1) + 8.0;
     if (c->coop_max > 0 && c->geo.nseg <= c->coop_max) {
-        // barrier arrivals of this launch: [P0] + (h-1) first-loop + mid + (h-1) second-loop + commit
+        // passes of this launch (sequence numbers it tags): [P0] + (h-1) first-loop + mid + (h-1)
+        // second-loop + commit
         const int passes = (p0_ref >= 0 ? 0 : 1) + 2 * h;
-        a.part = c->partials;
-        a.redge = c->coop_redge;
-        a.bar = c->coop_bar;
-        a.bar_base = c->coop_base;
+        a.ll = c->coop_ll;
+        a.seq_base = (unsigned)c->coop_base;
         a.err = c->coop_err_d;
         a.timeout = (unsigned long long)(2.0 * c->wall_khz * 1e3);  // 2 s
-        c->coop_base += (unsigned long long)passes * (unsigned long long)c->geo.nseg;
+        if (c->direct) {  // a completion record the host can wait on without a stream sync
+            const unsigned long long e = ++c->sp_epoch;
+            const int i = (int)(e & 3);
+            a.epoch = e;
+            a.done = c->sp_dh;
+            a.rec = c->sp_dh + 4 + 4 * i;
+            c->sp_base[i] = c->coop_base;
+            c->sp_bytes[i] = vec * 8.0 * (double)c->geo.n_loc;
+            c->sp_spec[i] = spec != nullptr;
+            if (spec) {
+                a.spec = 1;
+                a.spec_ls = spec->ls;
+                a.prev_c = c->slots + (int64_t)spec->prev_slot * LBK_SLOT;
+                a.spec_fx = spec->fx;
+                a.spec_c1 = spec->c1;
+                a.spec_c2 = spec->c2;
+                a.spec_tol = spec->tol;
+                a.vd = c->sp_vd + i;
+                if (spec->chain_epoch) {
+                    a.chain = c->sp_vd + (spec->chain_epoch & 3);
+                    a.chain_want = (spec->chain_epoch << 1) | 1ull;
+                }
+            }
+            if (epoch) *epoch = e;
+        }
+        c->coop_base += (unsigned long long)passes;
         geo.rev = 0;
         const int nb = (int)c->geo.nseg;
         return launch(c, LBK_K_SMALL_ITER, vec, -1, [&] {
@@ -562,6 +595,75 @@ int lbk_small_iter(lbk_ctx* c, int obj, int h, const double* g, double* q, doubl
             default: hipLaunchKernelGGL(k_small_iter<LBK_OBJ_QUAD_SEPARABLE>, dim3(1), dim3(LBK_SMALL_THREADS), 0, c->stream, a, geo); break;
         }
     });
+}
+
+int lbk_small_spec_ok(const lbk_ctx* c, int h) {
+    return lbk_small_ok(c, h) && c->direct && c->coop_max > 0 && c->geo.nseg <= c->coop_max;
+}
+
+// spin on the pinned completion word; every 64k polls ask the stream whether it still runs (a
+// faulted or finished stream with the word unset ends the wait with the stream's error)
+static int small_wait(lbk_ctx* c, unsigned long long epoch) {
+    const volatile unsigned long long* done = c->sp_h;
+    for (unsigned long it = 1;; ++it) {
+        if (__atomic_load_n(const_cast<unsigned long long*>(done), __ATOMIC_ACQUIRE) >= epoch) return 0;
+        if ((it & 0xffff) == 0) {
+            if (*(volatile unsigned*)c->coop_err_h) break;
+            const hipError_t q = hipStreamQuery(c->stream);
+            if (q == hipErrorNotReady) continue;
+            if (__atomic_load_n(const_cast<unsigned long long*>(done), __ATOMIC_ACQUIRE) >= epoch) return 0;
+            if (q != hipSuccess) {
+                snprintf(c->err, sizeof c->err, "cooperative iteration: %s", hipGetErrorString(q));
+                return -2;
+            }
+            snprintf(c->err, sizeof c->err, "cooperative iteration %llu: stream idle, no completion record", epoch);
+            return -2;
+        }
+        __builtin_ia32_pause();
+    }
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    snprintf(c->err, sizeof c->err, "cooperative iteration: grid barrier timed out");
+    return -2;
+}
+
+int lbk_small_fetch(lbk_ctx* c, unsigned long long epoch, int slot, int ncomp, double* totals, int* went,
+                    double* rho, double* gamma) {
+    if (went) *went = 1;
+    if (epoch == 0) return lbk_fetch(c, slot, ncomp, totals);
+    if (epoch > c->sp_epoch || epoch + 4 <= c->sp_epoch) {
+        snprintf(c->err, sizeof c->err, "lbk_small_fetch: epoch %llu not outstanding", epoch);
+        return -1;
+    }
+    int rc = small_wait(c, epoch);
+    if (rc) return rc;
+    const int i = (int)(epoch & 3);
+    const unsigned long long* r = c->sp_h + 4 + 4 * i;
+    const unsigned long long v = __atomic_load_n(r, __ATOMIC_ACQUIRE);
+    if ((v >> 1) != epoch) {
+        snprintf(c->err, sizeof c->err, "cooperative iteration %llu: record of %llu", epoch, v >> 1);
+        return -2;
+    }
+    double rg[2];
+    memcpy(&rg[0], &r[1], sizeof(double));
+    memcpy(&rg[1], &r[2], sizeof(double));
+    if (rho) *rho = rg[0];
+    if (gamma) *gamma = rg[1];
+    if (!(v & 1)) {
+        // nothing written: release the launch's sequence numbers and bytes. Launches queued
+        // behind it are speculative and chained to it, so they did not go either: the counter
+        // rolls back to this launch's base
+        c->coop_base = c->sp_base[i];
+        for (unsigned long long e = epoch; e <= c->sp_epoch; ++e) c->bytes_total -= c->sp_bytes[e & 3];
+        if (went) *went = 0;
+        return 0;
+    }
+    double* h = c->h_slots + (int64_t)slot * LBK_SLOT;
+    for (int k = 0; k < ncomp; ++k) {
+        double t = h[k];
+        for (int g = 1; g < LBK_GROUPS; ++g) t = t + h[g * LBK_KMAX + k];
+        totals[k] = t;
+    }
+    return 0;
 }
 
 int lbk_small_ok(const lbk_ctx* c, int h) {

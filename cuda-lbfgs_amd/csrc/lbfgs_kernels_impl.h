@@ -146,6 +146,39 @@ __device__ __forceinline__ double bitsd(unsigned long long u) {
     return __longlong_as_double((long long)u);
 }
 
+// Flagged partials of the cooperative iteration ("LL" words): a double travels as two 64-bit
+// words, each half tagged with the pass's sequence number in its upper 32 bits. Every 64-bit
+// store is single-copy atomic, so a reader that sees both tags has both halves: no separate
+// arrival counter, no drain between the data and the flag. Agent-scope (sc1) stores and loads,
+// coherent across the XCDs' L2s.
+#define LBK_LL_SEGS 512   // == LBK_COOP_SEGMAX
+#define LBK_LL_COMPS 10   // up to 8 reduction components + the 2 edge values of an r pass
+__device__ __forceinline__ void ll_store(unsigned long long* p, double v, unsigned seq) {
+    const unsigned long long u = dbits(v), tag = (unsigned long long)seq << 32;
+    __hip_atomic_store(p, tag | (u & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(p + 1, tag | (u >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// spins until both halves carry `seq`; past `timeout` wall-clock ticks sets *err and returns NaN
+__device__ __forceinline__ double ll_load(const unsigned long long* p, unsigned seq, unsigned* err,
+                                          unsigned long long timeout) {
+    unsigned long long w0 = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned long long w1 = __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((unsigned)(w0 >> 32) != seq || (unsigned)(w1 >> 32) != seq) {
+        const unsigned long long t0 = wall_clock64();
+        for (;;) {
+            __builtin_amdgcn_s_sleep(1);
+            w0 = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            w1 = __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((unsigned)(w0 >> 32) == seq && (unsigned)(w1 >> 32) == seq) break;
+            if (wall_clock64() - t0 > timeout) {
+                if (err) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                return __builtin_nan("");
+            }
+        }
+    }
+    return bitsd((w1 << 32) | (w0 & 0xffffffffull));
+}
+
 // Per-workgroup view of its segment.
 struct Seg {
     int64_t sbeg;   // global index of segment start
@@ -891,8 +924,13 @@ struct DirArgs {
     double rho;
     const double* ghost;  // sharded, D_BUF: all-gathered slot holding the neighbours' edge d
     int g_lo, g_hi;
-    const double* redge;  // cooperative iteration, D_TWOLOOP: first/last r of every segment (sc1)
-    int64_t L;            // ... and the segment length that indexes it
+    // cooperative iteration, D_TWOLOOP: the last r pass's flagged words (components 1 / 2: first /
+    // last r of every segment), that pass's sequence number, the segment length that indexes them
+    const unsigned long long* redge;
+    int64_t L;
+    unsigned redge_seq;
+    unsigned* err;
+    unsigned long long tmo;
 };
 
 template <int DMODE, bool NT>
@@ -952,9 +990,8 @@ __device__ __forceinline__ double halo_z(const double* __restrict__ x, const Dir
                         // r of another workgroup's segment, written in this launch: its published
                         // edge (write-through), not the plain-stored vector
                         const int64_t sg = hi / da.L;
-                        const double rv = bitsd(__hip_atomic_load(
-                            reinterpret_cast<const unsigned long long*>(da.redge + 2 * sg + (hi == sg * da.L ? 0 : 1)),
-                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                        const double rv = ll_load(da.redge + ((hi == sg * da.L ? 1 : 2) * LBK_LL_SEGS + sg) * 2,
+                                                  da.redge_seq, da.err, da.tmo);
                         dh = -(rv + da.s[hi] * da.coef);
                     } else
                         dh = load_dir1<DMODE>(da, hi);
@@ -1638,12 +1675,22 @@ struct SmallArgs {
     double* hslots;         // host mirror base, or nullptr
     int slot_p0, slot_a0, slot_b0, slot_c;
     // cooperative form (k_coop_iter) only
-    double* part;                 // 2 x 8 x LBK_SEGS partials (double-buffered by pass parity)
-    double* redge;                // 2 per segment: first / last r of the last second-loop pass
-    unsigned long long* bar;      // arrival counter, monotonic across launches
-    unsigned long long bar_base;  // its value when this launch starts
+    unsigned long long* ll;       // flagged partials [pass parity][LBK_LL_COMPS][LBK_LL_SEGS][2]
+    unsigned seq_base;            // pass p of this launch is tagged seq_base + p + 1 (monotonic)
     unsigned* err;                // pinned: set on a barrier timeout
     unsigned long long timeout;   // wall-clock ticks
+    // completion record for the host (pinned, nullptr: none): rec = [(epoch << 1) | went, rho
+    // bits, gamma bits], then *done = epoch once block 0's commit results are in the mirror
+    unsigned long long epoch;
+    unsigned long long* done;
+    unsigned long long* rec;
+    // speculative launch (lbk_spec): the prologue's tests (spec_ok) on the previous commit slot
+    int spec, spec_ls;
+    const double* prev_c;
+    double spec_fx, spec_c1, spec_c2, spec_tol;
+    unsigned long long* vd;             // device verdict word of this launch ((epoch << 1) | went)
+    const unsigned long long* chain;    // the previous speculative launch's verdict word, or nullptr
+    unsigned long long chain_want;
 };
 
 __device__ __forceinline__ Seg seg_at(const Geo& geo, int64_t sidx, int tq) {
@@ -1786,11 +1833,72 @@ __global__ __launch_bounds__(LBK_SMALL_THREADS) void k_small_iter(SmallArgs a, G
 // A barrier that waits past its timeout sets *err (pinned host memory) instead of hanging.
 // ---------------------------------------------------------------------------------------
 #define LBK_COOP_SEGMAX 512  // one group; resident at 2 workgroups per CU
+static_assert(LBK_COOP_SEGMAX == LBK_LL_SEGS, "flagged partials cover every cooperative segment");
+
+// component k of a slot: group 0 holds the total's tree, groups 1..7 are empty (+0.0), written
+// explicitly so that every reader - the host's fixed-order sum of the mirror, slot_total() of a
+// later launch - sums the same eight values
+__device__ __forceinline__ void coop_store_total(double* slot, double* hslot, int k, double q0) {
+#pragma unroll
+    for (int g = 0; g < LBK_GROUPS; ++g) {
+        slot[g * LBK_KMAX + k] = g == 0 ? q0 : 0.0;
+        if (hslot) hslot[g * LBK_KMAX + k] = g == 0 ? q0 : 0.0;
+    }
+}
+
+// The prologue of a speculative launch (lbk_spec): the host decisions between the previous
+// iteration and this one, restated on the previous commit's totals with the host's expressions
+// (lbfgs_driver.c iterate(), ls_*; -ffp-contract=off on both sides, IEEE division and square
+// root), so that the launch runs exactly when the host would have made it:
+//   * g.d < 0: no fallback to the gradient direction (lbfgs.cpp:146-153);
+//   * the line search takes a0 at its first trial (line_search.cpp:19-30, 57-121, 125-189, 33-55);
+//   * a0 >= 1e-10 (no line-search failure, lbfgs.cpp:164-168) and s.y > 0 (the pair is stored,
+//     :182-191);
+//   * |g_new| >= tol (the next iteration does not stop, :80-84);
+//   * rho = 1 / s.y finite and gamma = s.y / y.y finite and > 0 (:102-118).
+// rg = {rho, gamma} of the new pair.
+__device__ __forceinline__ int spec_ok(const SmallArgs& a, double (&rg)[2]) {
+    if (a.chain && __hip_atomic_load(a.chain, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != a.chain_want) return 0;
+    const double* p = a.prev_c;
+    const double gd = slot_total(p + LBK_C_GD), ft = slot_total(p + LBK_C_F), dphi = slot_total(p + LBK_C_DPHI);
+    const double sy = slot_total(p + LBK_C_SY), yy = slot_total(p + LBK_C_YY), gg = slot_total(p + LBK_C_GG);
+    const double fx = a.spec_fx, al = a.a0, c1 = a.spec_c1, c2 = a.spec_c2;
+    rg[0] = 1.0 / sy;
+    rg[1] = sy / yy;
+    if (gd >= 0) return 0;
+    int take;
+    switch (a.spec_ls) {
+        case 0: take = !(fx - ft < c1 * al * gd); break;                                 // backtracking
+        case 1: take = ft <= fx + c1 * al * gd; break;                                    // interpolation
+        case 2: take = !(ft > fx + c1 * al * gd) && fabs(dphi) <= -c2 * gd; break;        // Wolfe
+        default: take = !(ft > fx + c1 * al * gd) && !(dphi < c2 * gd); break;           // backtracking Wolfe
+    }
+    if (!take || al < 1e-10 || !(sy > 0)) return 0;
+    if (sqrt(gg) < a.spec_tol) return 0;
+    if (!isfinite(rg[0]) || rg[1] <= 0 || !isfinite(rg[1])) return 0;
+    return 1;
+}
+
+// block 0: the host-visible record, then the completion word (every wave's mirror stores are
+// complete before the word is written)
+__device__ __forceinline__ void coop_publish(const SmallArgs& a, int went, double rho, double gamma) {
+    if (blockIdx.x != 0 || !a.done) return;
+    if (threadIdx.x == 0) {
+        __hip_atomic_store(a.rec + 1, dbits(rho), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(a.rec + 2, dbits(gamma), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(a.rec, (a.epoch << 1) | (unsigned long long)went, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(a.done, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 template <int K, class Op>
 __device__ __forceinline__ void coop_pass(const Op& op, const Geo& geo, const SmallArgs& a, int pass,
                                           double* slot, double* hslot, const double* rvec, double (&tot)[K],
                                           double (&lds)[4][8], double (&tl)[8]) {
+    static_assert(K + 2 <= LBK_LL_COMPS, "flagged components");
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int64_t b = blockIdx.x;
     const Seg s = seg_setup(geo);
@@ -1807,53 +1915,31 @@ __device__ __forceinline__ void coop_pass(const Op& op, const Geo& geo, const Sm
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __syncthreads();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    double* P = a.part + (size_t)(pass & 1) * 8 * LBK_SEGS;
-    if (t == 0) {
+    const unsigned seq = a.seq_base + (unsigned)pass + 1u;
+    unsigned long long* P = a.ll + (size_t)(pass & 1) * LBK_LL_COMPS * LBK_LL_SEGS * 2;
+    if (t == 0) {  // the segment partial(s), and for an r pass the segment's first / last r
 #pragma unroll
         for (int k = 0; k < K; ++k)
-            __hip_atomic_store(reinterpret_cast<unsigned long long*>(P + (int64_t)k * LBK_SEGS + b),
-                               dbits((lds[0][k] + lds[1][k]) + (lds[2][k] + lds[3][k])), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-        if (rvec) {  // the segment's first and last r, for the neighbours' commit halo
-            __hip_atomic_store(reinterpret_cast<unsigned long long*>(a.redge + 2 * b), dbits(rvec[s.lb]),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(reinterpret_cast<unsigned long long*>(a.redge + 2 * b + 1),
-                               dbits(rvec[s.lb + s.len - 1]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_fetch_add(a.bar, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned long long target = a.bar_base + (unsigned long long)(pass + 1) * (unsigned long long)geo.nseg;
-        const unsigned long long t0 = wall_clock64();
-        while (__hip_atomic_load(a.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-            if (wall_clock64() - t0 > a.timeout) {
-                __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                printf("k_coop_iter: block %d pass %d: counter %llu, waiting for %llu\n", (int)b, pass,
-                       __hip_atomic_load(a.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), target);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
+            ll_store(P + ((int64_t)k * LBK_LL_SEGS + b) * 2, (lds[0][k] + lds[1][k]) + (lds[2][k] + lds[3][k]), seq);
+        if (rvec) {
+            ll_store(P + ((int64_t)K * LBK_LL_SEGS + b) * 2, rvec[s.lb], seq);
+            ll_store(P + ((int64_t)(K + 1) * LBK_LL_SEGS + b) * 2, rvec[s.lb + s.len - 1], seq);
         }
     }
-    __syncthreads();
     // every workgroup: the fixed-order totals of this pass (the group tree of stage 2, then the
-    // 8-group sum with groups 1..7 empty)
+    // 8-group sum with groups 1..7 empty), each thread waiting for the words it reads
     if (geo.nseg <= 64) {  // wave w: components w, w + 4; lane j: entry j (the small-group form)
 #pragma unroll
         for (int k = w; k < K; k += 4) {
-            const double p = lane < geo.nseg ? bitsd(__hip_atomic_load(
-                                                   reinterpret_cast<const unsigned long long*>(P + (int64_t)k * LBK_SEGS + lane),
-                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-                                             : 0.0;
+            const double p =
+                lane < geo.nseg ? ll_load(P + ((int64_t)k * LBK_LL_SEGS + lane) * 2, seq, a.err, a.timeout) : 0.0;
             const double q0 = wave_sum(p) + 0.0;  // group 0: the tree's levels above 64 add 0.0
             if (lane == 0) {
                 double tt = q0;
 #pragma unroll
                 for (int g = 1; g < LBK_GROUPS; ++g) tt = tt + 0.0;
                 tl[k] = tt;
-                if (b == 0 && slot) {
-                    slot[k] = q0;
-                    if (hslot) hslot[k] = q0;
-                }
+                if (b == 0 && slot) coop_store_total(slot, hslot, k, q0);
             }
         }
     } else {  // the general form: thread t entries 4t..4t+3, wave butterfly, ((w0+w1)+(w2+w3))
@@ -1863,10 +1949,7 @@ __device__ __forceinline__ void coop_pass(const Op& op, const Geo& geo, const Sm
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int j = 4 * t + i;
-                p[k][i] = j < geo.nseg ? bitsd(__hip_atomic_load(
-                                              reinterpret_cast<const unsigned long long*>(P + (int64_t)k * LBK_SEGS + j),
-                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-                                        : 0.0;
+                p[k][i] = j < geo.nseg ? ll_load(P + ((int64_t)k * LBK_LL_SEGS + j) * 2, seq, a.err, a.timeout) : 0.0;
             }
 #pragma unroll
         for (int k = 0; k < K; ++k) {
@@ -1880,10 +1963,7 @@ __device__ __forceinline__ void coop_pass(const Op& op, const Geo& geo, const Sm
 #pragma unroll
             for (int g = 1; g < LBK_GROUPS; ++g) tt = tt + 0.0;
             tl[t] = tt;
-            if (b == 0 && slot) {
-                slot[t] = q0;
-                if (hslot) hslot[t] = q0;
-            }
+            if (b == 0 && slot) coop_store_total(slot, hslot, t, q0);
         }
     }
     __syncthreads();
@@ -1898,16 +1978,37 @@ __global__ __launch_bounds__(LB_BLOCK) void k_coop_iter(SmallArgs a, Geo geo) {
     __shared__ double lds[4][8];
     __shared__ double tl[8];
     __shared__ double TA[LBK_SMALL_HMAX], TB[LBK_SMALL_HMAX];
+    __shared__ double spec_rg[2];
+    __shared__ int spec_went;
     const int h = a.h;
     int pass = 0;
     double t1[1];
+    double rho_top = a.rho[h - 1], gamma = a.gamma;
+    if (a.spec) {  // every workgroup evaluates the same tests on the same slot: all go or none
+        if (threadIdx.x == 0) {
+            double rg[2];
+            spec_went = spec_ok(a, rg);
+            spec_rg[0] = rg[0];
+            spec_rg[1] = rg[1];
+            if (blockIdx.x == 0)
+                __hip_atomic_store(a.vd, (a.epoch << 1) | (unsigned long long)spec_went, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __syncthreads();
+        if (!spec_went) {
+            coop_publish(a, 0, spec_rg[0], spec_rg[1]);
+            return;
+        }
+        rho_top = spec_rg[0];
+        gamma = spec_rg[1];
+    }
     // alpha_{h-1} = rho_{h-1} (s_{h-1} . g): from the previous commit (SG) or a dot pass
     if (a.p0_from_slot)
         t1[0] = slot_total(a.p0_slot);
     else
         coop_pass<1>(OpDot<false>{a.S[h - 1], a.g}, geo, a, pass++, SL(a.slot_p0), nullptr, nullptr, t1, lds, tl);
     if (threadIdx.x == 0) TA[h - 1] = t1[0];
-    double alpha = a.rho[h - 1] * t1[0];
+    double alpha = rho_top * t1[0];
     const double* qsrc = a.g;
     for (int i = h - 2; i >= 0; --i) {  // q = q - alpha_{i+1} y_{i+1};  s_i . q
         coop_pass<1>(OpAxpyDot<false>{a.q, qsrc, a.Y[i + 1], a.S[i], alpha}, geo, a, pass++, SL(a.slot_a0 + i),
@@ -1916,7 +2017,7 @@ __global__ __launch_bounds__(LB_BLOCK) void k_coop_iter(SmallArgs a, Geo geo) {
         alpha = a.rho[i] * t1[0];
         qsrc = a.q;
     }
-    coop_pass<1>(OpMid<false>{a.r, qsrc, a.Y[0], alpha, a.gamma}, geo, a, pass++, SL(a.slot_b0), nullptr,
+    coop_pass<1>(OpMid<false>{a.r, qsrc, a.Y[0], alpha, gamma}, geo, a, pass++, SL(a.slot_b0), nullptr,
                  h == 1 ? a.r : nullptr, t1, lds, tl);
     if (threadIdx.x == 0) TB[0] = t1[0];
     __syncthreads();
@@ -1929,16 +2030,20 @@ __global__ __launch_bounds__(LB_BLOCK) void k_coop_iter(SmallArgs a, Geo geo) {
         __syncthreads();
     }
     // the last second-loop update, the first trial at a0 and the commit (k_commit TWOLOOP)
-    DirArgs da = {a.r, a.S[h - 1], a.g, 0.0, nullptr, nullptr, a.rho[h - 1], nullptr, geo.g_lo, geo.g_hi,
-                  a.redge, geo.L};
+    // the halo of d across segments: the last r pass's (pass - 1) flagged edge words
+    const int rp = pass - 1;
+    DirArgs da = {a.r, a.S[h - 1], a.g, 0.0, nullptr, nullptr, rho_top, nullptr, geo.g_lo, geo.g_hi,
+                  a.ll + (size_t)(rp & 1) * LBK_LL_COMPS * LBK_LL_SEGS * 2, geo.L, a.seq_base + (unsigned)rp + 1u, a.err,
+                  a.timeout};
     {
-        const double beta = a.rho[h - 1] * TB[h - 1];
-        const double alph = a.rho[h - 1] * TA[h - 1];
+        const double beta = rho_top * TB[h - 1];
+        const double alph = rho_top * TA[h - 1];
         da.coef = alph - beta;
     }
     double t7[7];
     coop_pass<7>(OpCommit<OBJ, LBK_D_TWOLOOP, false>{a.x, da, a.a0, a.xn, a.gn, a.so, a.yo, geo.n, geo.n_loc}, geo, a,
                  pass++, SL(a.slot_c), HS(a.slot_c), nullptr, t7, lds, tl);
+    coop_publish(a, 1, rho_top, gamma);
 }
 #undef SL
 
@@ -2113,12 +2218,20 @@ struct lbk_ctx {
     int pend_taken;       // the launch in progress consumes it
     // cooperative small-n iteration (k_coop_iter): nseg <= coop_max (0: off)
     int coop_max;
-    unsigned long long* coop_bar;  // device arrival counter
-    unsigned long long coop_base;  // its value at the next launch
+    unsigned long long* coop_ll;   // flagged partials (SmallArgs::ll)
+    unsigned long long coop_base;  // passes tagged so far (the next launch's sequence base)
     unsigned* coop_err_h;          // pinned: barrier timeout
     unsigned* coop_err_d;
-    double* coop_redge;            // 2 per segment
     double wall_khz;
+    // cooperative launches' completion records (pinned; sp_h[0] = done word, sp_h[4 + 4 e..] the
+    // record of epoch e mod 4) and speculative verdicts (device, 4 words)
+    unsigned long long* sp_h;
+    unsigned long long* sp_dh;
+    unsigned long long* sp_vd;
+    unsigned long long sp_epoch;     // last epoch issued
+    unsigned long long sp_base[4];   // coop_base at each epoch's launch (release on a no-go)
+    double sp_bytes[4];
+    int sp_spec[4];                  // the epoch's launch was speculative
     hipEvent_t xfer_ev[4];  // lbk_*_local_async completion (host-callback transfers)
     double *dq_A, *dq_b, *dq_t;  // dense quadratic objective (lbk_dense_set): A (n x n), b, terms
 };

@@ -114,6 +114,7 @@ def lib():
     L.lbfgs_peer_enable.argtypes = [vp, C.c_int]
     L.lbfgs_exchange_backend.argtypes = [vp]
     L.lbfgs_exchange_latency.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_double)]
+    L.lbfgs_spec_stats.argtypes = [vp, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
     L.lbfgs_prof_enable.argtypes = [vp, C.c_int]
     L.lbfgs_prof_enable.restype = None
     L.lbfgs_prof_reset.argtypes = [vp]
@@ -134,6 +135,7 @@ EXPORTED_SYMBOLS = [
     "lbfgs_dev_twoloop", "lbfgs_dev_elementwise", "lbfgs_line_search", "lbfgs_prof_enable",
     "lbfgs_prof_reset", "lbfgs_prof_get", "lbfgs_peer_handle", "lbfgs_peer_connect", "lbfgs_peer_enable",
     "lbfgs_exchange_backend", "lbfgs_exchange_latency", "lbfgs_device_count", "lbfgs_set_dense_quadratic", "lbfgs_build_info",
+    "lbfgs_spec_stats",
 ]
 PEER_HANDLE_BYTES = 64
 BACKENDS = {0: "single", 1: "rccl", 2: "xgmi", 3: "host-group"}
@@ -265,6 +267,13 @@ class Context:
         except Exception:
             pass
 
+    def spec_stats(self):
+        """(adopted, dropped): speculative next-iteration launches the host took / discarded
+        since solver init (small n, cooperative iteration; LBFGS_SPEC=0: none)."""
+        a, d = C.c_int64(), C.c_int64()
+        lib().lbfgs_spec_stats(self.h, C.byref(a), C.byref(d))
+        return a.value, d.value
+
     def set_dense_quadratic(self, A, b):
         """Upload A (n x n, symmetric) and b for the "dense" objective f = x'Ax + b'x."""
         A = np.ascontiguousarray(A, np.float64)
@@ -272,7 +281,7 @@ class Context:
         assert A.shape == (self.n, self.n) and b.shape == (self.n,)
         rc = lib().lbfgs_set_dense_quadratic(self.h, A.ctypes.data_as(C.c_void_p), b.ctypes.data_as(C.c_void_p))
         if rc != 0:
-            self._err("lbfgs_set_dense_quadratic", "lbfgs_build_info", rc)
+            self._err("lbfgs_set_dense_quadratic", rc)
 
     # ---- sharded runs: xGMI peer exchange ----
     def peer_handle(self):

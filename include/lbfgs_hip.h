@@ -146,6 +146,13 @@ typedef struct {
  * identifies the sources a loaded library was built from (build provenance) */
 const char* lbfgs_build_info(void);
 
+/* Small n (cooperative iteration): iteration k + 1 is queued on the device behind iteration k
+ * before the host has read k's results, and runs only if its prologue finds every host decision
+ * in between as assumed (first trial taken, pair stored, no stop, valid rho and gamma); the host
+ * then takes it instead of launching. Launches the host took / discarded since solver init.
+ * LBFGS_SPEC=0 turns it off (bit-identical iterates either way). */
+int lbfgs_spec_stats(const lbfgs_ctx* c, int64_t* adopted, int64_t* dropped);
+
 /* ---- context ---------------------------------------------------------------------------- */
 /* n: global problem size; m: history length (1..64); device: HIP device ordinal. */
 int lbfgs_ctx_create(lbfgs_ctx** out, int64_t n, int m, int device);

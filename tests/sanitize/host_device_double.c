@@ -26,6 +26,12 @@ struct lbk_ctx {
     char err[256];
     double* scratch[6];
     double *dA, *db; /* dense quadratic data */
+    /* the small-n single-launch iteration and its speculative form (LBFGS_DOUBLE_SMALL=1; the
+     * product uses it for nseg <= its cooperative limit): launches run at once, in stream order */
+    int small_on;
+    unsigned long long epoch, vd[4];
+    int rec_went[4];
+    double rec_rho[4], rec_gamma[4];
 };
 
 struct lbk_group {
@@ -68,6 +74,8 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
         c->scratch[i] = (double*)calloc((size_t)n + 2, sizeof(double));
         if (!c->scratch[i]) return -4;
     }
+    const char* e = getenv("LBFGS_DOUBLE_SMALL");
+    c->small_on = e && atoi(e) != 0;
     *out = c;
     return 0;
 }
@@ -448,17 +456,96 @@ int lbk_vf_ghost_init(lbk_ctx* c, double* x, double* g, int wslot) {
     (void)c, (void)x, (void)g, (void)wslot;
     return 0;
 }
-int lbk_small_ok(const lbk_ctx* c, int h) {
-    (void)c, (void)h;
-    return 0;
+int lbk_small_ok(const lbk_ctx* c, int h) { return c->small_on && h >= 1 && h <= 16; }
+int lbk_small_spec_ok(const lbk_ctx* c, int h) { return lbk_small_ok(c, h); }
+
+/* the prologue of a speculative launch (k_coop_iter's spec_ok), on this double's slots */
+static int spec_tests(lbk_ctx* c, const lbk_spec* sp, double a0, double* rg) {
+    if (sp->chain_epoch && c->vd[sp->chain_epoch & 3] != ((sp->chain_epoch << 1) | 1ull)) return 0;
+    const int p = sp->prev_slot * LBK_KMAX;
+    const double gd = ref_total(c, p + LBK_C_GD), ft = ref_total(c, p + LBK_C_F), dphi = ref_total(c, p + LBK_C_DPHI);
+    const double sy = ref_total(c, p + LBK_C_SY), yy = ref_total(c, p + LBK_C_YY), gg = ref_total(c, p + LBK_C_GG);
+    const double fx = sp->fx, al = a0, c1 = sp->c1, c2 = sp->c2;
+    rg[0] = 1.0 / sy;
+    rg[1] = sy / yy;
+    if (gd >= 0) return 0;
+    int take;
+    switch (sp->ls) {
+        case 0: take = !(fx - ft < c1 * al * gd); break;
+        case 1: take = ft <= fx + c1 * al * gd; break;
+        case 2: take = !(ft > fx + c1 * al * gd) && fabs(dphi) <= -c2 * gd; break;
+        default: take = !(ft > fx + c1 * al * gd) && !(dphi < c2 * gd); break;
+    }
+    if (!take || al < 1e-10 || !(sy > 0)) return 0;
+    if (sqrt(gg) < sp->tol) return 0;
+    if (!isfinite(rg[0]) || rg[1] <= 0 || !isfinite(rg[1])) return 0;
+    return 1;
 }
+
+/* the launch sequence the cooperative kernel fuses: P0 dot unless p0_ref >= 0, the first loop,
+ * mid, the second loop, the TWOLOOP commit at a0 */
 int lbk_small_iter(lbk_ctx* c, int obj, int h, const double* g, double* q, double* r, const double* const* S,
                    const double* const* Y, const double* rho, double gamma, int p0_ref, double a0, const double* x,
-                   double* xn, double* gn, double* so, double* yo, int slot_p0, int slot_a0, int slot_b0, int slot_c) {
-    (void)c, (void)obj, (void)h, (void)g, (void)q, (void)r, (void)S, (void)Y, (void)rho, (void)gamma, (void)p0_ref;
-    (void)a0, (void)x, (void)xn, (void)gn, (void)so, (void)yo, (void)slot_p0, (void)slot_a0, (void)slot_b0,
-        (void)slot_c;
-    return -1;
+                   double* xn, double* gn, double* so, double* yo, int slot_p0, int slot_a0, int slot_b0, int slot_c,
+                   const lbk_spec* spec, unsigned long long* epoch) {
+    if (epoch) *epoch = 0;
+    if (!lbk_small_ok(c, h) || h > 16) return -1;
+    const unsigned long long e = ++c->epoch;
+    const int i4 = (int)(e & 3);
+    if (epoch) *epoch = e;
+    double rho_top = rho[h - 1];
+    if (spec) {
+        double rg[2];
+        const int went = spec_tests(c, spec, a0, rg);
+        c->vd[i4] = (e << 1) | (unsigned long long)went;
+        c->rec_went[i4] = went;
+        c->rec_rho[i4] = rg[0];
+        c->rec_gamma[i4] = rg[1];
+        if (!went) return 0;
+        rho_top = rg[0];
+        gamma = rg[1];
+    } else {
+        c->rec_went[i4] = 1;
+        c->rec_rho[i4] = rho_top;
+        c->rec_gamma[i4] = gamma;
+    }
+    int refA[16], refB[16];
+    if (p0_ref >= 0) {
+        refA[h - 1] = p0_ref;
+    } else {
+        if (lbk_dot(c, S[h - 1], g, slot_p0)) return -1;
+        refA[h - 1] = slot_p0 * LBK_KMAX;
+    }
+    const double* qsrc = g;
+    for (int i = h - 2; i >= 0; --i) {
+        if (lbk_axpy_dot(c, q, qsrc, Y[i + 1], S[i], i + 1 == h - 1 ? rho_top : rho[i + 1], refA[i + 1], slot_a0 + i))
+            return -1;
+        refA[i] = (slot_a0 + i) * LBK_KMAX;
+        qsrc = q;
+    }
+    if (lbk_mid(c, r, qsrc, Y[0], h == 1 ? rho_top : rho[0], gamma, refA[0], slot_b0)) return -1;
+    refB[0] = slot_b0 * LBK_KMAX;
+    for (int i = 0; i + 1 < h; ++i) {
+        if (lbk_axpy2_dot(c, r, r, S[i], Y[i + 1], rho[i], refB[i], refA[i], slot_b0 + i + 1)) return -1;
+        refB[i + 1] = (slot_b0 + i + 1) * LBK_KMAX;
+    }
+    return lbk_commit(c, obj, LBK_D_TWOLOOP, x, r, S[h - 1], g, rho_top, refB[h - 1], refA[h - 1], a0, xn, gn, so, yo,
+                      slot_c, 0.0);
+}
+
+int lbk_small_fetch(lbk_ctx* c, unsigned long long epoch, int slot, int ncomp, double* totals, int* went,
+                    double* rho, double* gamma) {
+    if (went) *went = 1;
+    if (epoch == 0) return lbk_fetch(c, slot, ncomp, totals);
+    if (epoch > c->epoch || epoch + 4 <= c->epoch) return -1;
+    const int i4 = (int)(epoch & 3);
+    if (rho) *rho = c->rec_rho[i4];
+    if (gamma) *gamma = c->rec_gamma[i4];
+    if (!c->rec_went[i4]) {
+        if (went) *went = 0;
+        return 0;
+    }
+    return lbk_fetch(c, slot, ncomp, totals);
 }
 
 /* ---- profiling ---- */

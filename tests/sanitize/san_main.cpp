@@ -113,17 +113,21 @@ static std::vector<double> x0_for(int64_t n, uint32_t seed) {
     return x;
 }
 
-// device objectives, every line search, default / batched-off / unfused
+// device objectives, every line search, default / batched-off / unfused / the small-n single
+// launch per iteration with and without the speculative next iteration
 static void device_objectives() {
     const int64_t sizes[] = {1, 2, 3, 1000, 4097, 70001};
     const int objs[] = {LBFGS_OBJ_ROSENBROCK, LBFGS_OBJ_QUAD_TRIDIAG, LBFGS_OBJ_QUAD_SEPARABLE};
+    int64_t adopted = 0, dropped = 0;
     for (int64_t n : sizes)
         for (int obj : objs)
             for (int ls = 0; ls < 4; ++ls)
-                for (int mode = 0; mode < 3; ++mode) {
+                for (int mode = 0; mode < 5; ++mode) {
                     const int m = n < 10 ? 2 : 5, maxit = n > 10000 ? 12 : 40;
                     if (obj == LBFGS_OBJ_QUAD_SEPARABLE && ls == LBFGS_LS_WOLFE) continue;  // diverges to NaN
                     setenv("LBFGS_BATCH", mode == 1 ? "0" : "1", 1);
+                    setenv("LBFGS_DOUBLE_SMALL", mode >= 3 ? "1" : "0", 1);
+                    setenv("LBFGS_SPEC", mode == 4 ? "0" : "1", 1);
                     const auto x0 = x0_for(n, 42 + (uint32_t)n);
                     lbfgs_ctx* c = nullptr;
                     EXPECT(lbfgs_ctx_create(&c, n, m, 0) == 0, "create n=%lld", (long long)n);
@@ -138,9 +142,20 @@ static void device_objectives() {
                     char tag[96];
                     std::snprintf(tag, sizeof tag, "n=%lld obj=%d ls=%d mode=%d", (long long)n, obj, ls, mode);
                     if (st >= 0) compare(tag, c, st, x, res, oracle(obj, ls, n, m, maxit, x0));
+                    int64_t a = 0, d = 0;
+                    lbfgs_spec_stats(c, &a, &d);
+                    EXPECT(mode == 3 || a + d == 0, "%s: speculative launches outside the speculative mode", tag);
+                    adopted += a;
+                    dropped += d;
                     lbfgs_ctx_destroy(c);
                 }
+    EXPECT(adopted > 100 && dropped > 10, "speculative launches: %lld taken, %lld dropped", (long long)adopted,
+           (long long)dropped);
+    std::printf("speculative next iteration: %lld launches taken, %lld dropped\n", (long long)adopted,
+                (long long)dropped);
     setenv("LBFGS_BATCH", "1", 1);
+    setenv("LBFGS_DOUBLE_SMALL", "0", 1);
+    setenv("LBFGS_SPEC", "1", 1);
 }
 
 // host callbacks: the reference call sequence call for call, and one call per point by default

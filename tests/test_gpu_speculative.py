@@ -1,0 +1,115 @@
+"""Speculative next iteration at small n: iteration k + 1's cooperative launch is
+queued behind iteration k's before the host reads k's results; its prologue restates the host's
+decisions in between and the launch writes nothing unless all hold. The host takes the queued
+launch (LBFGS_SPEC=1, default) or drops it; the iterates must be bit-identical to LBFGS_SPEC=0
+and to the oracle's canonical order, over every line search, objective, history fill, the
+stepping API and the guard paths (line-search failure, skipped updates, convergence)."""
+import numpy as np
+import pytest
+
+import lbfgs_amd as L
+import oracle_lib as O
+
+pytestmark = pytest.mark.gpu
+
+
+def bits(a):
+    return np.asarray(a, dtype=np.float64).view(np.uint64)
+
+
+def run(monkeypatch, spec, n, m, obj, ls, iters, seed=3, tol=1e-5):
+    monkeypatch.setenv("LBFGS_SPEC", "1" if spec else "0")
+    x0 = L.x0_uniform(n, seed, -2.0, 2.0)
+    with L.Context(n, m) as c:
+        r = c.minimize(obj, x0, ls, iters, tolerance=tol, trace=True)
+        r["spec"] = c.spec_stats()
+    return x0, r
+
+
+def same(a, b):
+    for key in ("tr_f", "tr_gnorm", "tr_alpha", "x"):
+        assert np.array_equal(bits(a[key]), bits(b[key])), key
+    assert np.array_equal(a["tr_c1"], b["tr_c1"]) and np.array_equal(a["tr_c2"], b["tr_c2"])
+    assert a["messages"] == b["messages"] and a["iterations"] == b["iterations"]
+    assert a["status"] == b["status"]
+
+
+@pytest.mark.parametrize("n,m,obj,ls", [
+    (10_000, 5, "rosenbrock", "backtracking"),
+    (10_000, 5, "rosenbrock", "interpolation"),
+    (10_000, 5, "rosenbrock", "wolfe"),
+    (10_000, 5, "rosenbrock", "backtracking_wolfe"),
+    (4097, 1, "rosenbrock", "backtracking"),
+    (30_001, 16, "rosenbrock", "backtracking"),
+    (100_000, 10, "quad_tridiag", "wolfe"),
+    (65_536, 7, "quad_sep", "backtracking"),
+    (131_072, 10, "rosenbrock", "backtracking_wolfe"),
+])
+def test_speculative_bit_exact(monkeypatch, n, m, obj, ls):
+    x0, a = run(monkeypatch, False, n, m, obj, ls, 120)
+    _, b = run(monkeypatch, True, n, m, obj, ls, 120)
+    same(a, b)
+    assert a["spec"] == (0, 0)
+    adopted, dropped = b["spec"]
+    assert adopted > 0 or b["iterations"] <= 3, (b["spec"], b["iterations"])  # quad_sep: 2 iterations
+    # every launch the host ran through the cooperative path after the first was queued ahead
+    assert adopted + dropped <= b["iterations"]
+    o = O.lbfgs(obj, x0, ls, m, 120, 1e-5, mode=O.CANON)
+    k = len(o["f"])
+    assert np.array_equal(bits(b["tr_f"][:k]), bits(o["f"])) and len(b["tr_f"]) == k
+
+
+def test_speculative_to_convergence(monkeypatch):
+    """configs[0]: n = 1e4, m = 5, backtracking, to tol 1e-5 (tens of thousands of iterations,
+    most of them taken ahead); the converging iteration's queued launch is dropped."""
+    x0, a = run(monkeypatch, False, 10_000, 5, "rosenbrock", "backtracking", 30_000, seed=42)
+    _, b = run(monkeypatch, True, 10_000, 5, "rosenbrock", "backtracking", 30_000, seed=42)
+    same(a, b)
+    assert b["status"] == "converged"
+    adopted, dropped = b["spec"]
+    assert adopted > 0.8 * b["iterations"], b["spec"]
+
+
+def test_speculative_stepping(monkeypatch):
+    """step(K) in chunks: no launch is queued past the last step of a call, and the next call
+    continues from the same state (bit-identical to one call and to LBFGS_SPEC=0)."""
+    n, m = 20_000, 6
+    x0 = L.x0_uniform(n, 9, -2.0, 2.0)
+    fs = []
+    for spec, chunks in (("0", [60]), ("1", [60]), ("1", [1] * 7 + [13, 2, 38])):
+        monkeypatch.setenv("LBFGS_SPEC", spec)
+        with L.Context(n, m) as c:
+            c.init("rosenbrock", x0, "backtracking", tolerance=1e-5)
+            for k in chunks:
+                r = c.step(k)
+            fs.append((r["f"], r["gnorm"], r["iterations"], bits(c.get_x()).sum()))
+            if spec == "1" and len(chunks) > 1:
+                adopted, _ = c.spec_stats()
+                assert adopted > 0
+    assert fs[0] == fs[1] == fs[2]
+
+
+DEVICE_STRESS = [nm for nm in O.stress_cases() if O.load_golden(nm)[0]["objective"] in L.OBJECTIVES]
+
+
+@pytest.mark.parametrize("name", DEVICE_STRESS)
+def test_speculative_guard_paths(monkeypatch, name):
+    """The reference's guard paths (invalid rho, line-search failure over long backtracking
+    chains, skipped updates; tests/golden/stress_*) with launches queued ahead whose assumptions
+    fail: the reference's stdout, and bit-identical to LBFGS_SPEC=0 and the oracle."""
+    meta, _ = O.load_golden(name)
+    n = meta["n"]
+    x0 = O.x0_uniform(n, meta["seed"], meta["lo"], meta["hi"])
+    out = []
+    with np.errstate(all="ignore"):
+        for spec in ("0", "1"):
+            monkeypatch.setenv("LBFGS_SPEC", spec)
+            with L.Context(n, meta["m"]) as c:
+                r = c.minimize(meta["objective"], x0, meta["method"], meta["maxit"], tolerance=meta["tol"],
+                               trace=True)
+                r["spec"] = c.spec_stats()
+            out.append(r)
+        o = O.lbfgs(meta["objective"], x0, meta["method"], meta["m"], meta["maxit"], meta["tol"], mode=O.CANON)
+    same(out[0], out[1])
+    assert out[1]["messages"] == meta["stdout"]
+    assert np.array_equal(bits(out[1]["tr_f"]), bits(o["f"]))
