@@ -119,8 +119,10 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
     // with the mid-n 2048-element segments (4x the work per workgroup) the crossover to the
     // deferred stage 2 comes earlier: at 245 segments (n = 5e5) deferred runs 6.8-7.0k it/s
     // against 5.4-5.6k cooperative, at 196 they tie, at 147 cooperative leads 7.9-8.1k to
-    // 7.0-7.8k (profiles/r01/coop_long_ab.txt)
-    c->coop_max = G.L > 512 ? 192 : 256;
+    // 7.0-7.8k (profiles/r01/coop_long_ab.txt). Round 2's flagged partials and speculative
+    // launches move it: at 245 segments (n = 5e5) cooperative 8.26k against deferred 6.61k, at
+    // 342 (7e5) deferred leads 5.07k to 4.81k (profiles/r02/small_n/coop_limit_ab.txt)
+    c->coop_max = 256;
     if (const char* e = getenv("LBFGS_COOP")) c->coop_max = std::min(atoi(e), LBK_COOP_SEGMAX);  // max segments
     c->pend_slot = -1;
     // measured (profiles/r01/defer_ab.txt): +21..32 % at n = 3e5 (586 segments); -14 % at 1954

@@ -4,11 +4,16 @@ decisions in between and the launch writes nothing unless all hold. The host tak
 launch (LBFGS_SPEC=1, default) or drops it; the iterates must be bit-identical to LBFGS_SPEC=0
 and to the oracle's canonical order, over every line search, objective, history fill, the
 stepping API and the guard paths (line-search failure, skipped updates, convergence)."""
+import os
+import sys
+
 import numpy as np
 import pytest
 
-import lbfgs_amd as L
-import oracle_lib as O
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "cuda-lbfgs_amd"))
+import lbfgs_amd as L  # noqa: E402
+import oracle_lib as O  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 
