@@ -205,6 +205,8 @@ int lbk_small_ok(const lbk_ctx* c, int h);
  * first trial a0 (f at x is `fx`), the pair is stored (s.y > 0), the next iteration has not
  * converged (|g| >= tol), its rho and gamma are valid - and computes the newest pair's rho and
  * gamma itself (rho[h-1] and gamma are ignored). If any test fails no workgroup writes anything.
+ * ls = -1: the current iteration's step is already decided (a recommit at the line search's
+ * step): no line-search test. cand > 0: the commit also reduces f at x + cand d (LBK_C_FC).
  * `chain_epoch` (0: none) is the launch this one follows when that was speculative as well: its
  * device verdict must be "went". */
 typedef struct {
@@ -217,7 +219,7 @@ int lbk_small_spec_ok(const lbk_ctx* c, int h);
 int lbk_small_iter(lbk_ctx* c, int obj, int h, const double* g, double* q, double* r, const double* const* S,
                    const double* const* Y, const double* rho, double gamma, int p0_ref, double a0, const double* x,
                    double* xn, double* gn, double* so, double* yo, int slot_p0, int slot_a0, int slot_b0,
-                   int slot_c, const lbk_spec* spec, unsigned long long* epoch);
+                   int slot_c, double cand, const lbk_spec* spec, unsigned long long* epoch);
 /* waits for launch `epoch` to finish its commit (spinning on a pinned word, no stream
  * synchronisation: a speculative launch queued behind it keeps running), then the fixed-order
  * totals of slot_c. *went (may be NULL): 0 if a speculative launch found a test failing (it wrote
@@ -225,6 +227,10 @@ int lbk_small_iter(lbk_ctx* c, int obj, int h, const double* g, double* q, doubl
  * speculative launch computed. epoch 0: lbk_fetch. */
 int lbk_small_fetch(lbk_ctx* c, unsigned long long epoch, int slot, int ncomp, double* totals, int* went,
                     double* rho, double* gamma);
+/* a mark in the stream after the launches so far, and the fixed-order totals of a host-mirrored
+ * slot once the stream has passed the mark (work queued after the mark keeps running) */
+int lbk_mark(lbk_ctx* c);
+int lbk_fetch_marked(lbk_ctx* c, int slot, int ncomp, double* totals);
 
 /* unfused mode: out = op(a, b) with device-side coefficients (see k_update) */
 enum { LBK_U_AXPY_Q = 0, LBK_U_AXPY_R, LBK_U_SCALE, LBK_U_NEG, LBK_U_SUB, LBK_U_POINT };

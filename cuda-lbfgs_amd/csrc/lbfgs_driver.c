@@ -140,6 +140,7 @@ struct lbfgs_ctx {
     double cur_rho, cur_gamma;    /* the host's rho of the newest pair and gamma, this iteration */
     int cur_p0;
     int sp_pend, sp_k, sp_h, sp_free, sp_p0, sp_cslot, sp_hostgo;
+    double sp_alpha; /* the step the queued launch assumes iteration sp_k - 1 commits */
     int sp_ring[MMAX + 1];
     double *sp_x, *sp_xn, *sp_g, *sp_gn;
     double sp_rho[MMAX];
@@ -995,6 +996,11 @@ static void note_h(lbfgs_ctx* c) {
     if (c->h > c->h_max) c->h_max = c->h;
 }
 
+/* the backtracking search's second step, f reduced by the commit pass (line_search.cpp:26) */
+static double first_cand(const lbfgs_ctx* c) {
+    return (c->batch && c->ls == LBFGS_LS_BACKTRACKING) ? c->K.initial_step * c->K.backtracking_alpha : 0.0;
+}
+
 /* a queued speculative launch the host does not take: wait for its record. It either did not go
  * (nothing written, reservations released) or ran on buffers the host no longer reads - which
  * holds only if the host also took the first trial and stored the pair in the iteration before
@@ -1018,7 +1024,7 @@ static int spec_drop(lbfgs_ctx* c) {
  * a0 and the pair is stored: the ring then drops its oldest pair (h = m) or grows, the new pair
  * is the current free one, x/xn and g/gn swap, and alpha_{h-1} of the first loop is the commit's
  * s.g (component SG) */
-static int spec_next(lbfgs_ctx* c) {
+static int spec_next(lbfgs_ctx* c, double decided) {
     const int m = c->m, h = c->h, k = c->k;
     if (!c->spec_on || c->steps_left <= 0 || c->cur_epoch == 0 || c->K.initial_step < 1e-10) return 0;
     const int h1 = h < m ? h + 1 : m;
@@ -1045,15 +1051,16 @@ static int spec_next(lbfgs_ctx* c) {
     const int p01 = REF(cslot, LBK_C_SG);
     lbk_spec sp;
     sp.prev_slot = cslot;
-    sp.ls = c->ls;
+    sp.ls = decided > 0.0 ? -1 : c->ls; /* a recommit's step is the host's already */
     sp.fx = c->f_cur;
     sp.c1 = c->K.c1;
     sp.c2 = c->K.c2;
     sp.tol = c->tol;
-    sp.chain_epoch = c->cur_spec ? c->cur_epoch : 0;
+    sp.chain_epoch = c->cur_spec && decided <= 0.0 ? c->cur_epoch : 0;
     DEV(lbk_small_iter(c->dev, c->obj, h1, c->gn, c->q, c->r, Sr, Yr, rho1, 0.0, p01, c->K.initial_step, c->xn,
-                       c->x, c->g, c->S[free1], c->Y[free1], SLOT_P0, SLOT_A0, SLOT_B0(m), cslot1, &sp,
-                       &c->sp_epoch));
+                       c->x, c->g, c->S[free1], c->Y[free1], SLOT_P0, SLOT_A0, SLOT_B0(m), cslot1, first_cand(c),
+                       &sp, &c->sp_epoch));
+    c->sp_alpha = decided > 0.0 ? decided : c->K.initial_step;
     c->sp_pend = 1;
     c->sp_k = k + 1;
     c->sp_h = h1;
@@ -1075,7 +1082,7 @@ static int small_launch(lbfgs_ctx* c, const double* rho, const double* const* Sr
                         double gamma, int p0_ref) {
     DEV(lbk_small_iter(c->dev, c->obj, c->h, c->g, c->q, c->r, Sr, Yr, rho, gamma, p0_ref, c->K.initial_step,
                        c->x, c->xn, c->gn, c->S[c->free_pair], c->Y[c->free_pair], SLOT_P0, SLOT_A0,
-                       SLOT_B0(c->m), SLOT_COMMIT0 + (c->k & 1), NULL, &c->cur_epoch));
+                       SLOT_B0(c->m), SLOT_COMMIT0 + (c->k & 1), first_cand(c), NULL, &c->cur_epoch));
     c->cur_spec = 0;
     return 0;
 }
@@ -1088,7 +1095,7 @@ static int small_launch(lbfgs_ctx* c, const double* rho, const double* const* Sr
 static int small_fetch(lbfgs_ctx* c, int cslot, double* tot) {
     int went = 1;
     double vr = 0.0, vg = 0.0;
-    DEVNC(lbk_small_fetch(c->dev, c->cur_epoch, cslot, 7, tot, &went, &vr, &vg));
+    DEVNC(lbk_small_fetch(c->dev, c->cur_epoch, cslot, 8, tot, &went, &vr, &vg));
     if (!c->cur_spec) return 0;
     if (!went) {
         c->sp_pend = 0;
@@ -1103,7 +1110,7 @@ static int small_fetch(lbfgs_ctx* c, int cslot, double* tot) {
         }
         int rc = small_launch(c, rho, Sr, Yr, c->cur_gamma, c->cur_p0);
         if (rc) return rc;
-        DEVNC(lbk_small_fetch(c->dev, c->cur_epoch, cslot, 7, tot, NULL, NULL, NULL));
+        DEVNC(lbk_small_fetch(c->dev, c->cur_epoch, cslot, 8, tot, NULL, NULL, NULL));
         return 0;
     }
     if (memcmp(&vr, &c->cur_rho, sizeof vr) != 0 || memcmp(&vg, &c->cur_gamma, sizeof vg) != 0) {
@@ -1112,6 +1119,23 @@ static int small_fetch(lbfgs_ctx* c, int cslot, double* tot) {
         return LBFGS_ERR_STATE;
     }
     c->sp_adopted++;
+    return 0;
+}
+
+/* small n, the line search took another step than a0: the recommit, then iteration k + 1 queued
+ * behind it (no line-search test: the step is decided), then the commit's totals once the stream
+ * has passed the recommit */
+static int commit_queued(lbfgs_ctx* c, int dmode, double alpha, int cslot, double* tot) {
+    const int pair = c->free_pair;
+    const double* dsrc = dmode == LBK_D_BUF ? c->d : c->rc;
+    const double* s_last = dmode == LBK_D_TWOLOOP ? c->S[c->s_last_pair] : NULL;
+    DEV(lbk_commit(c->dev, c->obj, dmode, c->x, dsrc, s_last, c->g, c->rho_last, c->ref_b_last, c->ref_a_last, alpha,
+                   c->xn, c->gn, c->S[pair], c->Y[pair], cslot, 0.0));
+    DEV(lbk_mark(c->dev));
+    int rc = alpha >= 1e-10 ? spec_next(c, alpha) : 0;
+    if (rc) return rc;
+    DEVNC(lbk_fetch_marked(c->dev, cslot, 7, tot));
+    c->commits++;
     return 0;
 }
 
@@ -1207,7 +1231,7 @@ static int iterate(lbfgs_ctx* c) {
                 if (rc) return rc;
             }
             /* the next iteration, queued before this one's results are read */
-            rc = spec_next(c);
+            rc = spec_next(c, 0.0);
             if (rc) return rc;
             c->rho_last = rho[h - 1];
             c->ref_b_last = REF(SLOT_B0(m) + h - 1, 0);
@@ -1289,6 +1313,11 @@ static int iterate(lbfgs_ctx* c) {
             rc = small_fetch(c, cslot, tot);
             if (rc) return rc;
             c->commits++;
+            if (cand > 0.0) {
+                c->cand_valid = 1;
+                c->cand_alpha = cand;
+                c->cand_f = tot[LBK_C_FC];
+            }
         } else {
             rc = commit(c, c->dmode, c->a0, cslot, tot, cand);
             if (rc) return rc;
@@ -1338,11 +1367,16 @@ static int iterate(lbfgs_ctx* c) {
             rc = materialize_d(c);
             if (rc) return rc;
         }
-        rc = commit(c, c->d_ready ? LBK_D_BUF : c->dmode, alpha, cslot, tot, 0.0);
+        if (small_done && c->spec_on) { /* the next iteration queued behind the recommit */
+            rc = spec_drop(c);
+            if (!rc) rc = commit_queued(c, c->d_ready ? LBK_D_BUF : c->dmode, alpha, cslot, tot);
+        } else {
+            rc = commit(c, c->d_ready ? LBK_D_BUF : c->dmode, alpha, cslot, tot, 0.0);
+        }
         if (rc) return rc;
     }
     c->f_cur = tot[LBK_C_F];
-    c->sp_hostgo = alpha == c->a0 && tot[LBK_C_SY] > 0; /* what a queued launch of k + 1 assumed */
+    c->sp_hostgo = alpha == c->sp_alpha && tot[LBK_C_SY] > 0; /* what a queued launch of k + 1 assumed */
     if (alpha < 1e-10) { /* :164-168 */
         say(c, "Warning: Line search failed at iteration %d\n", k);
         c->status = LBFGS_STATUS_LS_FAILED;

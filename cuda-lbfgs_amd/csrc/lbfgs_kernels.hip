@@ -255,6 +255,7 @@ void lbk_destroy(lbk_ctx* c) {
     if (c->coop_err_h) (void)hipHostFree(c->coop_err_h);
     if (c->sp_h) (void)hipHostFree(c->sp_h);
     if (c->sp_vd) (void)hipFree(c->sp_vd);
+    if (c->mark_ev) (void)hipEventDestroy(c->mark_ev);
     (void)hipFree(c->cnt);
     (void)hipFree(c->slots);
     (void)hipHostFree(c->h_slots);
@@ -510,7 +511,7 @@ int lbk_elementwise(lbk_ctx* c, int op, double* out, const double* a, const doub
 int lbk_small_iter(lbk_ctx* c, int obj, int h, const double* g, double* q, double* r, const double* const* S,
                    const double* const* Y, const double* rho, double gamma, int p0_ref, double a0, const double* x,
                    double* xn, double* gn, double* so, double* yo, int slot_p0, int slot_a0, int slot_b0,
-                   int slot_c, const lbk_spec* spec, unsigned long long* epoch) {
+                   int slot_c, double cand, const lbk_spec* spec, unsigned long long* epoch) {
     if (epoch) *epoch = 0;
     if (!lbk_small_ok(c, h) || (spec && !lbk_small_spec_ok(c, h))) return -1;
     SmallArgs a;
@@ -528,6 +529,7 @@ int lbk_small_iter(lbk_ctx* c, int obj, int h, const double* g, double* q, doubl
     }
     a.gamma = gamma;
     a.a0 = a0;
+    a.cand = cand;
     a.x = x;
     a.xn = xn;
     a.gn = gn;
@@ -660,6 +662,33 @@ int lbk_small_fetch(lbk_ctx* c, unsigned long long epoch, int slot, int ncomp, d
         return 0;
     }
     double* h = c->h_slots + (int64_t)slot * LBK_SLOT;
+    for (int k = 0; k < ncomp; ++k) {
+        double t = h[k];
+        for (int g = 1; g < LBK_GROUPS; ++g) t = t + h[g * LBK_KMAX + k];
+        totals[k] = t;
+    }
+    return 0;
+}
+
+int lbk_mark(lbk_ctx* c) {
+    if (!c->mark_ev) HIPCHK(c, hipEventCreateWithFlags(&c->mark_ev, hipEventDisableTiming));
+    if (c->pend_slot >= 0) {  // a deferred stage 2 completes before the mark
+        const int rc = flush_pending(c);
+        if (rc) return rc;
+    }
+    HIPCHK(c, hipEventRecord(c->mark_ev, c->stream));
+    return 0;
+}
+
+int lbk_fetch_marked(lbk_ctx* c, int slot, int ncomp, double* totals) {
+    if (!c->mark_ev || slot < 0 || slot >= LBK_NSLOTS || !c->slot_mirror[slot] || ncomp > LBK_KMAX)
+        return lbk_fetch(c, slot, ncomp, totals);
+    HIPCHK(c, hipEventSynchronize(c->mark_ev));
+    if (*(volatile unsigned*)c->coop_err_h) {
+        snprintf(c->err, sizeof c->err, "cooperative iteration: grid barrier timed out");
+        return -2;
+    }
+    const double* h = c->h_slots + (int64_t)slot * LBK_SLOT;
     for (int k = 0; k < ncomp; ++k) {
         double t = h[k];
         for (int g = 1; g < LBK_GROUPS; ++g) t = t + h[g * LBK_KMAX + k];

@@ -1033,7 +1033,13 @@ __device__ __forceinline__ double2 halo_xd(const double* __restrict__ x, const D
                     dh = ghost_d(da, hi, n_loc);
                 else if (DMODE == LBK_D_TWOLOOP && da.ghost && (hi == -1 || hi == n_loc))
                     dh = -(ghost_d(da, hi, n_loc) + da.s[hi] * da.coef);
-                else
+                else if (DMODE == LBK_D_TWOLOOP && da.redge && hi >= 0 && hi < n_loc && hi / da.L != i / da.L) {
+                    // cooperative iteration: another workgroup's r from this launch (as halo_z)
+                    const int64_t sg = hi / da.L;
+                    const double rv = ll_load(da.redge + ((hi == sg * da.L ? 1 : 2) * LBK_LL_SEGS + sg) * 2,
+                                              da.redge_seq, da.err, da.tmo);
+                    dh = -(rv + da.s[hi] * da.coef);
+                } else
                     dh = load_dir1<DMODE>(da, hi);
                 xd = make_double2(x[hi], dh);
             }
@@ -1668,6 +1674,7 @@ struct SmallArgs {
     const double* Y[LBK_SMALL_HMAX];
     double rho[LBK_SMALL_HMAX];
     double gamma, a0;
+    double cand;            // cooperative commit: also f at x + cand d (component FC)
     const double* p0_slot;  // previous commit's slot, component SG (p0_from_slot)
     const double* x;
     double *xn, *gn, *so, *yo;
@@ -1865,15 +1872,17 @@ __device__ __forceinline__ int spec_ok(const SmallArgs& a, double (&rg)[2]) {
     const double fx = a.spec_fx, al = a.a0, c1 = a.spec_c1, c2 = a.spec_c2;
     rg[0] = 1.0 / sy;
     rg[1] = sy / yy;
-    if (gd >= 0) return 0;
-    int take;
-    switch (a.spec_ls) {
+    int take = 1;
+    if (a.spec_ls < 0) {  // the previous commit's step was already decided by the host
+    } else if (gd >= 0) {
+        return 0;
+    } else switch (a.spec_ls) {
         case 0: take = !(fx - ft < c1 * al * gd); break;                                 // backtracking
         case 1: take = ft <= fx + c1 * al * gd; break;                                    // interpolation
         case 2: take = !(ft > fx + c1 * al * gd) && fabs(dphi) <= -c2 * gd; break;        // Wolfe
         default: take = !(ft > fx + c1 * al * gd) && !(dphi < c2 * gd); break;           // backtracking Wolfe
     }
-    if (!take || al < 1e-10 || !(sy > 0)) return 0;
+    if (!take || (a.spec_ls >= 0 && al < 1e-10) || !(sy > 0)) return 0;
     if (sqrt(gg) < a.spec_tol) return 0;
     if (!isfinite(rg[0]) || rg[1] <= 0 || !isfinite(rg[1])) return 0;
     return 1;
@@ -2040,9 +2049,10 @@ __global__ __launch_bounds__(LB_BLOCK) void k_coop_iter(SmallArgs a, Geo geo) {
         const double alph = rho_top * TA[h - 1];
         da.coef = alph - beta;
     }
-    double t7[7];
-    coop_pass<7>(OpCommit<OBJ, LBK_D_TWOLOOP, false>{a.x, da, a.a0, a.xn, a.gn, a.so, a.yo, geo.n, geo.n_loc}, geo, a,
-                 pass++, SL(a.slot_c), HS(a.slot_c), nullptr, t7, lds, tl);
+    double t8[8];
+    coop_pass<8>(OpCommit<OBJ, LBK_D_TWOLOOP, false, true>{a.x, da, a.a0, a.xn, a.gn, a.so, a.yo, geo.n, geo.n_loc,
+                                                           a.cand},
+                 geo, a, pass++, SL(a.slot_c), HS(a.slot_c), nullptr, t8, lds, tl);
     coop_publish(a, 1, rho_top, gamma);
 }
 #undef SL
@@ -2233,6 +2243,7 @@ struct lbk_ctx {
     double sp_bytes[4];
     int sp_spec[4];                  // the epoch's launch was speculative
     hipEvent_t xfer_ev[4];  // lbk_*_local_async completion (host-callback transfers)
+    hipEvent_t mark_ev;     // lbk_mark / lbk_fetch_marked
     double *dq_A, *dq_b, *dq_t;  // dense quadratic objective (lbk_dense_set): A (n x n), b, terms
 };
 

@@ -468,15 +468,17 @@ static int spec_tests(lbk_ctx* c, const lbk_spec* sp, double a0, double* rg) {
     const double fx = sp->fx, al = a0, c1 = sp->c1, c2 = sp->c2;
     rg[0] = 1.0 / sy;
     rg[1] = sy / yy;
-    if (gd >= 0) return 0;
-    int take;
-    switch (sp->ls) {
+    int take = 1;
+    if (sp->ls < 0) {
+    } else if (gd >= 0) {
+        return 0;
+    } else switch (sp->ls) {
         case 0: take = !(fx - ft < c1 * al * gd); break;
         case 1: take = ft <= fx + c1 * al * gd; break;
         case 2: take = !(ft > fx + c1 * al * gd) && fabs(dphi) <= -c2 * gd; break;
         default: take = !(ft > fx + c1 * al * gd) && !(dphi < c2 * gd); break;
     }
-    if (!take || al < 1e-10 || !(sy > 0)) return 0;
+    if (!take || (sp->ls >= 0 && al < 1e-10) || !(sy > 0)) return 0;
     if (sqrt(gg) < sp->tol) return 0;
     if (!isfinite(rg[0]) || rg[1] <= 0 || !isfinite(rg[1])) return 0;
     return 1;
@@ -487,7 +489,7 @@ static int spec_tests(lbk_ctx* c, const lbk_spec* sp, double a0, double* rg) {
 int lbk_small_iter(lbk_ctx* c, int obj, int h, const double* g, double* q, double* r, const double* const* S,
                    const double* const* Y, const double* rho, double gamma, int p0_ref, double a0, const double* x,
                    double* xn, double* gn, double* so, double* yo, int slot_p0, int slot_a0, int slot_b0, int slot_c,
-                   const lbk_spec* spec, unsigned long long* epoch) {
+                   double cand, const lbk_spec* spec, unsigned long long* epoch) {
     if (epoch) *epoch = 0;
     if (!lbk_small_ok(c, h) || h > 16) return -1;
     const unsigned long long e = ++c->epoch;
@@ -530,8 +532,13 @@ int lbk_small_iter(lbk_ctx* c, int obj, int h, const double* g, double* q, doubl
         refB[i + 1] = (slot_b0 + i + 1) * LBK_KMAX;
     }
     return lbk_commit(c, obj, LBK_D_TWOLOOP, x, r, S[h - 1], g, rho_top, refB[h - 1], refA[h - 1], a0, xn, gn, so, yo,
-                      slot_c, 0.0);
+                      slot_c, cand);
 }
+int lbk_mark(lbk_ctx* c) {
+    (void)c;
+    return 0;
+}
+int lbk_fetch_marked(lbk_ctx* c, int slot, int ncomp, double* totals) { return lbk_fetch(c, slot, ncomp, totals); }
 
 int lbk_small_fetch(lbk_ctx* c, unsigned long long epoch, int slot, int ncomp, double* totals, int* went,
                     double* rho, double* gamma) {
