@@ -1013,6 +1013,7 @@ static int spec_drop(lbfgs_ctx* c) {
     double t[1];
     int went = 0;
     DEVNC(lbk_small_fetch(c->dev, c->sp_epoch, c->sp_cslot, 1, t, &went, NULL, NULL));
+    if (!went) c->passes--; /* a launch that did nothing is no pass */
     if (went && !c->sp_hostgo) {
         snprintf(c->err, sizeof c->err, "speculative iteration %d ran where the host stopped", c->sp_k);
         return LBFGS_ERR_STATE;
@@ -1098,6 +1099,7 @@ static int small_fetch(lbfgs_ctx* c, int cslot, double* tot) {
     DEVNC(lbk_small_fetch(c->dev, c->cur_epoch, cslot, 8, tot, &went, &vr, &vg));
     if (!c->cur_spec) return 0;
     if (!went) {
+        c->passes -= c->sp_pend ? 2 : 1; /* this launch and the one chained behind it did nothing */
         c->sp_pend = 0;
         c->sp_dropped++;
         double rho[MMAX];
