@@ -1021,10 +1021,11 @@ static int spec_drop(lbfgs_ctx* c) {
     return 0;
 }
 
-/* queue iteration k + 1 behind iteration k's cooperative launch, assuming the line search takes
- * a0 and the pair is stored: the ring then drops its oldest pair (h = m) or grows, the new pair
- * is the current free one, x/xn and g/gn swap, and alpha_{h-1} of the first loop is the commit's
- * s.g (component SG) */
+/* queue iteration k + 1 behind iteration k's latest commit, assuming the pair is stored: the ring
+ * then drops its oldest pair (h = m) or grows, the new pair is the current free one, x/xn and g/gn
+ * swap, and alpha_{h-1} of the first loop is the commit's s.g (component SG). decided = 0: behind
+ * the cooperative launch, whose commit at a0 the line search has yet to judge (the kernel
+ * re-checks its first-trial test); decided > 0: behind a recommit at that step */
 static int spec_next(lbfgs_ctx* c, double decided) {
     const int m = c->m, h = c->h, k = c->k;
     if (!c->spec_on || c->steps_left <= 0 || c->cur_epoch == 0 || c->K.initial_step < 1e-10) return 0;
