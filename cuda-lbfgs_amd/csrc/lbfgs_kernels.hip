@@ -540,6 +540,9 @@ int lbk_small_iter(lbk_ctx* c, int obj, int h, const double* g, double* q, doubl
     c->slot_mirror[slot_p0] = 0;  // single-component passes: device only (see mirrored())
     for (int i = 0; i < h; ++i) c->slot_mirror[slot_a0 + i] = c->slot_mirror[slot_b0 + i] = 0;
     c->slot_mirror[slot_c] = c->direct ? 1 : 0;
+    // written here, not by a ticket launch: no ticket completion word stands for them
+    c->slot_s2[slot_p0] = c->slot_s2[slot_c] = 0;
+    for (int i = 0; i < h; ++i) c->slot_s2[slot_a0 + i] = c->slot_s2[slot_b0 + i] = 0;
     a.slot_p0 = slot_p0;
     a.slot_a0 = slot_a0;
     a.slot_b0 = slot_b0;
@@ -607,8 +610,8 @@ int lbk_small_spec_ok(const lbk_ctx* c, int h) {
 
 // spin on the pinned completion word; every 64k polls ask the stream whether it still runs (a
 // faulted or finished stream with the word unset ends the wait with the stream's error)
-static int small_wait(lbk_ctx* c, unsigned long long epoch) {
-    const volatile unsigned long long* done = c->sp_h;
+static int small_wait(lbk_ctx* c, unsigned long long epoch, int word = 0) {
+    const volatile unsigned long long* done = c->sp_h + word;
     for (unsigned long it = 1;; ++it) {
         if (__atomic_load_n(const_cast<unsigned long long*>(done), __ATOMIC_ACQUIRE) >= epoch) return 0;
         if ((it & 0xffff) == 0) {
@@ -681,7 +684,8 @@ int lbk_mark(lbk_ctx* c) {
 }
 
 int lbk_fetch_marked(lbk_ctx* c, int slot, int ncomp, double* totals) {
-    if (!c->mark_ev || slot < 0 || slot >= LBK_NSLOTS || !c->slot_mirror[slot] || ncomp > LBK_KMAX)
+    if (!c->mark_ev || slot < 0 || slot >= LBK_NSLOTS || !c->slot_mirror[slot] || ncomp > LBK_KMAX ||
+        c->slot_s2[slot])  // no mark needed: the slot's launch writes a completion word
         return lbk_fetch(c, slot, ncomp, totals);
     HIPCHK(c, hipEventSynchronize(c->mark_ev));
     if (*(volatile unsigned*)c->coop_err_h) {
@@ -807,6 +811,13 @@ int lbk_fetch_groups(lbk_ctx* c, int slot, double* groups64) {
     if (frc) return frc;
     double* h = slot_host(c, slot);
     const size_t bytes = sizeof(double) * LBK_GROUPS * slot_stride(slot);
+    const int si = slot < LBK_NSLOTS ? slot : LBK_NSLOTS + slot - LBK_WSLOT0;
+    if (c->slot_s2[si] && c->slot_mirror[si]) {  // a ticket launch's completion word, no stream sync
+        const int rc = small_wait(c, c->slot_s2[si], 1);
+        if (rc) return rc;
+        memcpy(groups64, h, bytes);
+        return 0;
+    }
     if (!c->slot_mirror[slot < LBK_NSLOTS ? slot : LBK_NSLOTS + slot - LBK_WSLOT0])
         HIPCHK(c, hipMemcpyAsync(h, slot_base(c, slot), bytes, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));

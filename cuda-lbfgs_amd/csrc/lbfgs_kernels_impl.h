@@ -70,6 +70,10 @@ struct Red {
     double* hslot;     // its pinned host mirror, written alongside (one rank), or nullptr
     int ticket;        // 1: in-launch last-arriver stage 2; 0: k_group_reduce after the launch
     int kstride;       // LBK_KMAX (regular slots) or LBK_KW (wide slots)
+    // tickets, one rank, host-read slot: the last arriver stores `epoch` into this pinned word
+    // after the slot's mirror, so the host waits on it instead of synchronising the stream
+    unsigned long long* done;
+    unsigned long long epoch;
 };
 
 // Streaming loads/stores; NT = non-temporal (the vectors are touched once per pass and, at
@@ -349,6 +353,11 @@ __device__ __forceinline__ void reduce_publish(double (&acc)[K], const Geo& geo,
     group_tree<K, true>(red.partials, gseg0 - geo.seg_lo, gseg0, geo.nseg, geo.spg, red.slot + g * red.kstride,
                         red.hslot ? red.hslot + g * red.kstride : nullptr, lds);
     if (t == 0) __hip_atomic_store(red.cnt + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (red.done) {  // every wave's mirror stores complete before the word
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        __syncthreads();
+        if (t == 0) __hip_atomic_store(red.done, red.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 // Reduce-kernel mode: one workgroup per group of this rank (stage 2 after the boundary).
@@ -2244,6 +2253,10 @@ struct lbk_ctx {
     int sp_spec[4];                  // the epoch's launch was speculative
     hipEvent_t xfer_ev[4];  // lbk_*_local_async completion (host-callback transfers)
     hipEvent_t mark_ev;     // lbk_mark / lbk_fetch_marked
+    // ticket launches' completion words (Red::done = sp_h + 1): the epoch last issued, and per
+    // slot the epoch of the launch that last wrote its mirror (0: none, fetch synchronises)
+    unsigned long long s2_epoch;
+    unsigned long long slot_s2[LBK_NSLOTS + LBK_NWSLOTS];
     double *dq_A, *dq_b, *dq_t;  // dense quadratic objective (lbk_dense_set): A (n x n), b, terms
 };
 
@@ -2340,6 +2353,15 @@ Red kred(lbk_ctx* c, int slot, int K = 1) {
     c->slot_mirror[slot < LBK_NSLOTS ? slot : LBK_NSLOTS + slot - LBK_WSLOT0] = r.hslot != nullptr;
     r.kstride = slot_stride(slot);
     r.ticket = c->ticket;
+    r.done = nullptr;
+    r.epoch = 0;
+    const int si = slot < LBK_NSLOTS ? slot : LBK_NSLOTS + slot - LBK_WSLOT0;
+    c->slot_s2[si] = 0;
+    if (r.ticket && r.hslot && c->geo.world == 1 && !c->comm && !c->grp && c->sp_dh) {
+        r.done = c->sp_dh + 1;
+        r.epoch = ++c->s2_epoch;
+        c->slot_s2[si] = r.epoch;
+    }
     return r;
 }
 
