@@ -141,3 +141,24 @@ def test_speculative_sweep(monkeypatch, n, m, obj, ls, seed):
         _, a = run(monkeypatch, False, n, m, obj, ls, 80, seed=seed)
         _, b = run(monkeypatch, True, n, m, obj, ls, 80, seed=seed)
     same(a, b)
+
+
+@pytest.mark.parametrize("n,m,obj,ls,vf", [(10_000, 5, "rosenbrock", "backtracking", False),
+                                           (10_000, 5, "rosenbrock", "wolfe", False),
+                                           (30_001, 8, "quad_tridiag", "interpolation", False),
+                                           (10_000, 5, "rosenbrock", "backtracking", True),
+                                           (200_001, 6, "rosenbrock", "backtracking_wolfe", False)])
+def test_without_host_mirrors(monkeypatch, n, m, obj, ls, vf):
+    """LBFGS_DIRECT=0: no pinned mirrors, so no completion words and no launches queued ahead;
+    every fetch synchronises the stream and copies. The same bits as the default."""
+    x0 = L.x0_uniform(n, 21, -2.0, 2.0)
+    out = []
+    for direct in ("1", "0"):
+        monkeypatch.setenv("LBFGS_DIRECT", direct)
+        with L.Context(n, m) as c:
+            r = c.minimize(obj, x0, ls, 60, trace=True, vector_free=vf)
+            r["spec"] = c.spec_stats()
+        out.append(r)
+    same(out[0], out[1])
+    assert out[1]["spec"] == (0, 0)
+    assert vf or n > 131072 or out[0]["spec"][0] > 0
