@@ -337,7 +337,9 @@ vector<double> LBFGS_CUDA(const FnF f, const FnG grad, const vector<double> x0, 
 
 vector<double> LBFGS_CUDA(const FnF f, const FnG grad, const vector<double> x0, const int max_iterations,
                           const int m, const double tolerance) {
-    return LBFGS_CUDA(f, grad, x0, std::string("backtracking"), max_iterations, m, tolerance);
+    // the variant a caller built without -DLBFGS_CUDA_VARIANT runs (lbfgs.h): env, else backtracking
+    const char* v = std::getenv("LBFGS_CUDA_VARIANT");
+    return LBFGS_CUDA(f, grad, x0, std::string(v && *v ? v : "backtracking"), max_iterations, m, tolerance);
 }
 
 int lbfgs_amd::last_objective() { return g_last_objective; }

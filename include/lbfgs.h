@@ -28,12 +28,26 @@ std::vector<double> LBFGS_CUDA(const std::function<double(std::vector<double>)> 
                                const std::vector<double> x0, const std::string line_search_method,
                                const int max_iterations, const int m, const double tolerance);
 
-/* the variants' form without a method string (L-BFGS-Backtracking.cu:139-145 and siblings);
- * uses the backtracking line search of the prebuilt lbfgs_cuda variant */
+/* the variants' form without a method string (L-BFGS-Backtracking.cu:139-145, and the same
+ * signature in L-BFGS-Interpolation.cu:105, L-BFGS-Wolfe.cu:105, L-BFGS-Backtracking_Wolfe.cu:106).
+ * In the reference the line search is fixed by which .cu file was compiled (run.sh $1); here the
+ * caller names its variant at compile time, -DLBFGS_CUDA_VARIANT='"wolfe"' (or "backtracking",
+ * "interpolation", "backtracking_wolfe"), or at run time with the environment variable
+ * LBFGS_CUDA_VARIANT; with neither it is "backtracking" (L-BFGS-Backtracking.cu). An unknown name
+ * throws std::invalid_argument as the string form does. */
+#ifdef LBFGS_CUDA_VARIANT
+static inline std::vector<double> LBFGS_CUDA(const std::function<double(std::vector<double>)> f,
+                                             const std::function<std::vector<double>(std::vector<double>)> grad,
+                                             const std::vector<double> x0, const int max_iterations, const int m,
+                                             const double tolerance) {
+    return LBFGS_CUDA(f, grad, x0, std::string(LBFGS_CUDA_VARIANT), max_iterations, m, tolerance);
+}
+#else
 std::vector<double> LBFGS_CUDA(const std::function<double(std::vector<double>)> f,
                                const std::function<std::vector<double>(std::vector<double>)> grad,
                                const std::vector<double> x0, const int max_iterations, const int m,
                                const double tolerance);
+#endif
 
 namespace lbfgs_amd {
 /* which objective path the calling thread's last LBFGS / LBFGS_CUDA call took: 0 Rosenbrock,

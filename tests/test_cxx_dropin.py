@@ -180,3 +180,113 @@ def test_reference_main_on_gpu():
     assert abs(v) <= 1e-20 and abs(_quad_seq(g["ret_x"])) <= 1e-20
     assert sum(ln.startswith("Elapsed time: ") for ln in lines) == 2  # benchmark() + main.cpp:55
     assert lines.count("---------------------------------------------") == 1
+
+
+# ---- the CUDA path's callers (parallel-implementation/*.cu main()) ----------------------------
+CUDA_DIR = "/root/reference/parallel-implementation"
+# .cu file -> (executable suffix, line search the variant implies, n, method passed as a string)
+CUDA_MAINS = {
+    "L-BFGS.cu": ("LBFGS", "wolfe", 5),                              # L-BFGS.cu:384-409
+    "L-BFGS-Backtracking.cu": ("Backtracking", "backtracking", 50000),  # :429-457
+    "L-BFGS-Interpolation.cu": ("Interpolation", "interpolation", 50000),  # :444-472
+    "L-BFGS-Wolfe.cu": ("Wolfe", "wolfe", 50000),                     # :456-484
+    "L-BFGS-Backtracking_Wolfe.cu": ("Backtracking_Wolfe", "backtracking_wolfe", 50000),  # :504-532
+}
+
+
+def _cuda_exe(tag):
+    return os.path.join(CXX_DIR, "_build", "cuda_main_" + tag)
+
+
+def test_cuda_path_mains_compile_unchanged():
+    """Each parallel-implementation .cu file's own main() builds unchanged against include/
+    (functions.h, constants.h, line_search.h, vector_utils.h, lbfgs.h) and links
+    liblbfgs_hip.so (tests/cxx/Makefile `cuda`: the prelude replaces the file's CUDA/cuBLAS
+    includes and its LBFGS_CUDA definition; the main() text is piped from the reference)."""
+    exes = [_cuda_exe(v[0]) for v in CUDA_MAINS.values()]
+    if not os.path.isdir(CUDA_DIR):
+        if all(os.path.exists(e) for e in exes):
+            return
+        pytest.skip("/root/reference absent and tests/cxx/_build/cuda_main_* not built")
+    r = subprocess.run(["make", "-C", CXX_DIR, "cuda"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert all(os.path.exists(e) for e in exes)
+    # no copy of the reference's text is left in the tree (the recipe pipes it to the compiler)
+    assert not [f for f in os.listdir(os.path.join(CXX_DIR, "_build")) if f.endswith(".cpp")]
+
+
+_VARIANT_CALLER = r'''
+#include <cstdio>
+#include <stdexcept>
+#include <functions.h>
+int main() {
+    vector<double> x0(8, 0.5);
+    try { LBFGS_CUDA(rosenbrock, rosenbrock_grad, x0, 10, 5, 1e-1); }
+    catch (const std::invalid_argument& e) { std::printf("INVALID %s\n", e.what()); }
+    catch (const std::runtime_error& e) { std::printf("RUNTIME\n"); }
+    return 0;
+}
+'''
+
+
+@pytest.mark.parametrize("how", ["macro", "env"])
+def test_cuda_variant_selection_unknown_name(tmp_path, how):
+    """The string-less LBFGS_CUDA names its line search through -DLBFGS_CUDA_VARIANT (compile time)
+    or LBFGS_CUDA_VARIANT (environment); an unknown name throws std::invalid_argument with the
+    reference's message (lbfgs.cpp:69, L-BFGS.cu:151) before any device work (runs on CPU)."""
+    src = tmp_path / "v.cpp"
+    src.write_text(_VARIANT_CALLER)
+    exe = tmp_path / "v"
+    cmd = ["g++", "-std=c++17", "-O2", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe),
+           "-L", PKG, "-l:liblbfgs_hip.so", "-Wl,-rpath," + PKG]
+    if how == "macro":
+        cmd.insert(3, '-DLBFGS_CUDA_VARIANT="bogus"')
+    subprocess.run(cmd, check=True, capture_output=True)
+    env = dict(os.environ, LBFGS_CUDA_VARIANT="bogus") if how == "env" else None
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60, env=env)
+    assert r.returncode == 0, r.stderr
+    assert "INVALID Unknown line search method: bogus" in r.stdout
+
+
+def _rosen_seq(x):  # functions.cpp:26-36, left to right
+    s = 0.0
+    v = x.tolist()
+    for i in range(len(v) - 1):
+        s += 100 * (v[i + 1] - v[i] * v[i]) ** 2 + (1 - v[i]) ** 2
+    return s
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cu", list(CUDA_MAINS))
+def test_cuda_path_main_on_gpu(cu):
+    """The unchanged main() of each CUDA-path file on the GPU: the variant's line search with the
+    CUDA path's constants (constants.h, C2 = 0.7). Its printed solution (cout, 6 significant
+    digits) and "Optimum value" equal the C ABI's run of the same problem (rosenbrock, m = 10,
+    tol 1e-1, x0 ~ U(-2,2) from mt19937(42)); at n = 5 (L-BFGS.cu) also the canonical oracle's."""
+    tag, ls, n = CUDA_MAINS[cu]
+    exe = _cuda_exe(tag)
+    if not os.path.exists(exe):
+        pytest.skip("tests/cxx/_build/cuda_main_* not built (needs /root/reference where it is built)")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    lines = r.stdout.splitlines()
+    sol = [ln for ln in lines if ln.startswith("Found solution: ")]
+    opt = [ln for ln in lines if ln.startswith("Optimum value: ")]
+    assert len(sol) == 1 and len(opt) == 1
+    x0 = O.x0_uniform(n, 42, -2.0, 2.0)
+    first = [ln for ln in lines if ln.startswith("First x: ")][0]
+    assert first.split()[2:5] == ["%g" % v for v in x0[:3]]
+    import sys
+
+    if PKG not in sys.path:
+        sys.path.insert(0, PKG)
+    import lbfgs_amd as LA
+
+    with LA.Context(n, 10, device=0) as ctx:
+        res = ctx.minimize("rosenbrock", x0, ls, 50000, tolerance=1e-1, consts=LA.constants("cuda"))
+    x = res["x"]
+    assert sol[0].split()[2:] == ["%g" % v for v in x]
+    assert opt[0] == "Optimum value: %g" % _rosen_seq(x)
+    if n == 5:
+        o = O.lbfgs("rosenbrock", x0, ls, 10, 50000, 1e-1, mode=O.CANON, consts=dict(c2=0.7))
+        assert np.array_equal(x.view(np.uint64), o["x"].view(np.uint64))
