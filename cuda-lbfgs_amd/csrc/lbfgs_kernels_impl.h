@@ -560,6 +560,24 @@ __device__ __forceinline__ void stream_pipelined(const Op& op, const Seg& s, dou
 #define LBK_PIPELINE 0
 #endif
 
+// Rows per load group on full segments. A pass with few load streams per row (k_mid: q and y0)
+// keeps fewer bytes in flight per wave at 4 rows; op_unroll widens its groups. The groups only
+// decide when loads are issued: rows are still applied, and accumulated, in ascending order, so
+// every unroll gives the same bits.
+#ifndef LBK_MID_UNROLL
+#define LBK_MID_UNROLL 8
+#endif
+template <class Op>
+struct op_unroll {
+    static constexpr int value = 4;
+};
+template <bool NT>
+struct OpMid;
+template <bool NT>
+struct op_unroll<OpMid<NT>> {
+    static constexpr int value = LBK_MID_UNROLL;
+};
+
 template <int K, class Op>
 __device__ __forceinline__ void stream(const Op& op, const Seg& s, const Geo& geo, double (&acc)[K]) {
     int u0 = 0;
@@ -568,6 +586,9 @@ __device__ __forceinline__ void stream(const Op& op, const Seg& s, const Geo& ge
         return;
     }
     if (s.len == geo.L) {
+        constexpr int U = op_unroll<Op>::value;
+        if constexpr (U > 4)
+            for (; u0 + U <= s.nrows; u0 += U) rows<false, U>(op, s, u0, acc);
         for (; u0 + 4 <= s.nrows; u0 += 4) rows<false, 4>(op, s, u0, acc);
         if (u0 + 2 <= s.nrows) {
             rows<false, 2>(op, s, u0, acc);
