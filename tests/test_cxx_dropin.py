@@ -219,6 +219,7 @@ _VARIANT_CALLER = r'''
 #include <cstdio>
 #include <stdexcept>
 #include <functions.h>
+#include <benchmark.h>  // both objective headers in one unit (same declarations)
 int main() {
     vector<double> x0(8, 0.5);
     try { LBFGS_CUDA(rosenbrock, rosenbrock_grad, x0, 10, 5, 1e-1); }
@@ -237,8 +238,8 @@ def test_cuda_variant_selection_unknown_name(tmp_path, how):
     src = tmp_path / "v.cpp"
     src.write_text(_VARIANT_CALLER)
     exe = tmp_path / "v"
-    cmd = ["g++", "-std=c++17", "-O2", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe),
-           "-L", PKG, "-l:liblbfgs_hip.so", "-Wl,-rpath," + PKG]
+    cmd = ["g++", "-std=c++17", "-O2", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), str(src), "-o",
+           str(exe), "-L", PKG, "-l:liblbfgs_hip.so", "-Wl,-rpath," + PKG]
     if how == "macro":
         cmd.insert(3, '-DLBFGS_CUDA_VARIANT="bogus"')
     subprocess.run(cmd, check=True, capture_output=True)
