@@ -4,6 +4,7 @@
 // parallel-implementation/L-BFGS.cu:105-112) and run on the GPU. The benchmark objectives are
 // recognised through std::function::target and evaluated by the device kernels; any other
 // callable is driven through the host-callback objective.
+#include <cmath>
 #include <cstdint>
 #include <cstdlib>
 #include <limits>
@@ -14,6 +15,7 @@
 #include <vector>
 
 #include <cstdio>
+#include <iostream>
 #include <numeric>
 
 #include "benchmark.h"
@@ -282,8 +284,33 @@ double line_search(int ls, const vector<double>& x, const vector<double>& d, con
     return alpha;
 }
 
+// LBFGS_CUDA with LBFGS_CUDA_PROGRESS=1: the CUDA path's progress lines (L-BFGS.cu:115, 297,
+// 307, 350-355) printed after the solve from the device trace (entry k: f and |g| at the top of
+// iteration k, the step iteration k took) instead of the sequential driver's messages; no host
+// f evaluation per iteration. The convergence line uses the CUDA path's <= test (:353).
+void print_cuda_progress(lbfgs_ctx* c, double tolerance) {
+    const int len = lbfgs_trace_len(c);
+    if (len <= 0) return;
+    vector<double> tf(len), tg(len), ta(len);
+    lbfgs_trace_get(c, tf.data(), tg.data(), ta.data(), nullptr, nullptr, len);
+    for (int k = 0; k < len && !std::isnan(ta[k]); ++k) {
+        if (ta[k] < 1e-10) {
+            std::cout << "Warning: Line search failed at iteration " << k << std::endl;
+            break;
+        }
+        std::cout << "alpha: " << ta[k] << std::endl;
+        if (k + 1 >= len) break;
+        std::cout << "Iteration " << k << ": norm_g = " << tg[k + 1] << std::endl;
+        std::cout << "Optimum value: " << tf[k + 1] << std::endl;
+        if (tg[k + 1] <= tolerance) {
+            std::cout << "Convergence achieved at iteration " << k << std::endl;
+            break;
+        }
+    }
+}
+
 vector<double> run(const FnF& f, const FnG& grad, const vector<double>& x0, int ls, int max_iterations,
-                   int m, double tolerance, bool verbose, const lbfgs_constants& k) {
+                   int m, double tolerance, bool verbose, const lbfgs_constants& k, bool cuda_progress = false) {
     const int64_t n = (int64_t)x0.size();
     if (n < 1) throw std::invalid_argument("x0 must not be empty");
     const int obj = identify(f, grad, (int)n);
@@ -310,10 +337,15 @@ vector<double> run(const FnF& f, const FnG& grad, const vector<double>& x0, int 
         if (lbfgs_set_dense_quadratic(c, df->A->data(), df->b->data()) != 0)
             throw std::runtime_error(std::string("lbfgs_set_dense_quadratic failed: ") + lbfgs_last_error(c));
     }
+    if (cuda_progress) {
+        flags |= LBFGS_FLAG_TRACE | LBFGS_FLAG_QUIET;
+        std::cout << "Starting" << std::endl;
+    }
     int rc = lbfgs_minimize(c, obj, obj == LBFGS_OBJ_HOST ? &cb : nullptr, ls, &k, x0.data(), x.data(),
                             max_iterations, tolerance, flags, &res);
     if (!hf.error.empty()) throw std::runtime_error("objective callback failed: " + hf.error);
     if (rc < 0) throw std::runtime_error(std::string("LBFGS failed: ") + lbfgs_last_error(c));
+    if (cuda_progress) print_cuda_progress(c, tolerance);
     return x;
 }
 
@@ -332,7 +364,8 @@ vector<double> LBFGS_CUDA(const FnF f, const FnG grad, const vector<double> x0, 
     const int ls = line_search_id(line_search_method);
     lbfgs_constants k;
     lbfgs_constants_cuda(&k);  // parallel-implementation/constants.h (C2 = 0.7)
-    return run(f, grad, x0, ls, max_iterations, m, tolerance, false, k);
+    const char* p = std::getenv("LBFGS_CUDA_PROGRESS");
+    return run(f, grad, x0, ls, max_iterations, m, tolerance, false, k, p && std::atoi(p) != 0);
 }
 
 vector<double> LBFGS_CUDA(const FnF f, const FnG grad, const vector<double> x0, const int max_iterations,

@@ -291,3 +291,52 @@ def test_cuda_path_main_on_gpu(cu):
     if n == 5:
         o = O.lbfgs("rosenbrock", x0, ls, 10, 50000, 1e-1, mode=O.CANON, consts=dict(c2=0.7))
         assert np.array_equal(x.view(np.uint64), o["x"].view(np.uint64))
+
+
+_PROGRESS_CALLER = r'''
+#include <functions.h>
+#include <random>
+int main() {
+    std::mt19937 gen(42);
+    std::uniform_real_distribution<> dis(-2, 2);
+    std::vector<double> x0(1000);
+    for (double& v : x0) v = dis(gen);
+    std::vector<double> x = LBFGS_CUDA(rosenbrock, rosenbrock_grad, x0, "backtracking", 40, 5, 1e-5);
+    cout << "END " << x.size() << endl;
+    return 0;
+}
+'''
+
+
+@pytest.mark.gpu
+def test_cuda_progress_lines(tmp_path):
+    """LBFGS_CUDA_PROGRESS=1: LBFGS_CUDA prints the CUDA path's progress lines (L-BFGS.cu:115,
+    307, 350-351: "Starting", then per iteration "alpha", "Iteration k: norm_g", "Optimum value")
+    from the device trace, equal to the C ABI trace of the same solve; without it, none."""
+    src = tmp_path / "p.cpp"
+    src.write_text(_PROGRESS_CALLER)
+    exe = tmp_path / "p"
+    subprocess.run(["g++", "-std=c++17", "-O2", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe),
+                    "-L", PKG, "-l:liblbfgs_hip.so", "-Wl,-rpath," + PKG], check=True, capture_output=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, LBFGS_CUDA_PROGRESS="1"))
+    assert r.returncode == 0, r.stderr
+    lines = r.stdout.splitlines()
+    import sys
+
+    if PKG not in sys.path:
+        sys.path.insert(0, PKG)
+    import lbfgs_amd as LA
+
+    x0 = O.x0_uniform(1000, 42, -2.0, 2.0)
+    with LA.Context(1000, 5, device=0) as ctx:
+        t = ctx.minimize("rosenbrock", x0, "backtracking", 40, tolerance=1e-5, trace=True,
+                         consts=LA.constants("cuda"))
+    want = ["Starting"]
+    for k in range(len(t["tr_f"]) - 1):
+        want += ["alpha: %g" % t["tr_alpha"][k], "Iteration %d: norm_g = %g" % (k, t["tr_gnorm"][k + 1]),
+                 "Optimum value: %g" % t["tr_f"][k + 1]]
+    assert lines[:-1] == want and lines[-1] == "END 1000"
+    assert len(want) == 1 + 3 * 40
+    r0 = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert r0.returncode == 0 and "Starting" not in r0.stdout and "alpha: " not in r0.stdout
