@@ -177,11 +177,17 @@ class CpuBaseline:
                 out.append(dict(n=r["n"], error=f"rc={p.returncode} {p.stderr.read().decode()[-200:]}"))
                 continue
             g = np.fromfile(r["pre"] + ".g.bin", dtype=np.uint64).reshape(-1, 5)
+            fcalls = np.fromfile(r["pre"] + ".f.bin", dtype=np.float64)
             t = g[:, 3].copy().view(np.float64)
             dt = np.diff(t)  # dt[k] = time of iteration k (grad call k -> k+1)
             steady = dt[r["m"]:]  # iterations with h = m
+            # the reference's trajectory: grad call k is made at x_k (lbfgs.cpp:30,171; backtracking
+            # calls grad nowhere else), right after f(x_k) (:29,160), the nf-th f call
+            nf = g[:, 4].astype(np.int64)
+            traj = dict(f=fcalls[nf - 1], gnorm=g[:, 2].copy().view(np.float64), c1=g[:, 0].copy(),
+                        c2=g[:, 1].copy())
             out.append(dict(n=r["n"], per_iter_s=float(np.mean(steady)), iters_timed=len(steady),
-                            total_s=float(t[-1]), pinned=r["pinned"], core=r["core"]))
+                            total_s=float(t[-1]), pinned=r["pinned"], core=r["core"], trajectory=traj))
         for r in self.runs:
             if r["proc"].stderr:
                 r["proc"].stderr.close()
@@ -260,11 +266,17 @@ def measure(a, D, n, x0, dev, rank, world, uid, unfused=False, vector_free=False
                 print(f"exchange auto: xgmi {tx:.2f} us, rccl {tr:.2f} us -> {ctx.backend}", file=sys.stderr,
                       flush=True)
     backend = ctx.backend
-    ctx.init(a.objective, x0, a.line_search, tolerance=1e-5, unfused=unfused, vector_free=vector_free)
+    # the untimed history fill and warm-up record the trajectory (f, |g|, alpha, x checksums at
+    # the top of every iteration) for reference_parity; the timed steps run untraced
+    trace = not vector_free
+    ctx.init(a.objective, x0, a.line_search, tolerance=1e-5, unfused=unfused, vector_free=vector_free,
+             trace=trace)
     # history fill (untimed, not counted as warm-up): m iterations store m pairs, so every later
     # step uses h = m whatever --warmup is (B_iter grows with h)
     fill = ctx.step(a.history)
     ctx.step(a.warmup)
+    if trace:
+        ctx.trace_enable(False)
     ctx.sync()
     D.barrier()
     ctx.sync()
@@ -282,13 +294,24 @@ def measure(a, D, n, x0, dev, rank, world, uid, unfused=False, vector_free=False
     if not a.no_prof and res["status"] == "running":
         ctx.prof_reset()
         ctx.prof_enable(True)
+        tp = time.perf_counter()
         ctx.step(min(a.steps, 20))
         ctx.sync()
+        prof_wall_ms = (time.perf_counter() - tp) * 1e3
         ctx.prof_enable(False)
         for kname in L.KERNELS:
             p = ctx.prof_get(kname)
             if p["launches"]:
                 prof[kname] = p
+        if world > 1:
+            # the share of the (instrumented) iterations this rank spent in reduction exchanges,
+            # waiting for its peers included; the max over ranks is reported
+            ex = prof.get("exchange", {"ms": 0.0, "launches": 0})
+            share = D.allreduce(ex["ms"] / max(prof_wall_ms, 1e-9), "max")
+            prof["_exchange_share"] = {"share_max_over_ranks": round(share, 4),
+                                       "rank0_ms": round(ex["ms"], 3), "rank0_exchanges": ex["launches"],
+                                       "rank0_wall_ms": round(prof_wall_ms, 3),
+                                       "iterations": min(a.steps, 20)}
     # sharded: the cost of one reduction exchange on this machine, per backend available on
     # every rank (collective calls, same sequence everywhere): the two-loop issues ~2h + 3 of
     # them per iteration, each on the critical path
@@ -299,6 +322,8 @@ def measure(a, D, n, x0, dev, rank, world, uid, unfused=False, vector_free=False
         for b in backends:
             for k in (8, 96):
                 lat[f"{b}_{k * 8}doubles"] = round(ctx.exchange_latency(b, k, 200), 2)
+    if trace:
+        res["trajectory"] = ctx.trace()
     ctx.close()
     res["history_fill"] = fill["iterations"]
     done_steps = a.steps if res["status"] == "running" else max(res["iterations"] - a.warmup - fill["iterations"], 1)
@@ -336,8 +361,11 @@ def config4(a, D, dev, rank, world):
     """BASELINE configs[4]: Rosenbrock n = 1e9, m = 10, sharded over 8 GPUs, default mode, the
     xGMI peer exchange (no RCCL communicator: a rank that fails early cannot strand the others in
     a collective init). Every rank generates the full x0 (std::mt19937(42), as everywhere) and
-    uploads its slice. Each step that can fail is followed by a gloo vote, so all ranks skip
-    together."""
+    uploads its slice. Like the headline, m untimed iterations fill the history before the
+    warm-up, so every timed step has h = m. Each step that can fail is followed by a gloo vote,
+    so all ranks skip together. Then rank 0 repeats the solve on its GPU alone (n = 1e9 is 240 GB
+    resident, which fits one MI355X) and compares f, |g| and the iteration count bit for bit
+    (`shard_check`, as for the n = 1e8 line)."""
     n9 = 10 ** 9
     t0 = time.perf_counter()
     try:
@@ -360,10 +388,10 @@ def config4(a, D, dev, rank, world):
     if not ok:
         ctx.close()
         return {"skipped": f"xGMI peer exchange unavailable ({msg})"}
-    res, T, err = None, None, None
+    res, T, err, fill = None, None, None, None
     try:
         ctx.init(a.objective, x0, a.line_search, tolerance=1e-5)
-        del x0
+        fill = ctx.step(a.history)
         ctx.step(a.warmup)
         ctx.sync()
     except L.LbfgsError as e:
@@ -381,22 +409,105 @@ def config4(a, D, dev, rank, world):
         T = D.allreduce(t_local, "max")
         bytes_all = D.allreduce(res["bytes"] if res else 0.0, "sum")
     ok = D.all_ok(err is None and res is not None)
-    ctx.close()
+    ctx.close()  # every rank frees its shard before rank 0's one-GPU check
     if not ok:
         return {"skipped": f"solve failed on a rank ({err})"}
-    steps = a.steps if res["status"] == "running" else max(res["iterations"] - a.warmup, 1)
+    D.barrier()
+    if rank != 0:
+        del x0
+    check = shard_check(a, D, n9, x0 if rank == 0 else None, dev, rank, world, res)
+    fill_n = fill["iterations"] if fill else 0
+    steps = a.steps if res["status"] == "running" else max(res["iterations"] - a.warmup - fill_n, 1)
     return {"workload": f"{a.objective} n=1e9 m={a.history} {a.line_search}, sharded over {world} GPUs "
                         "(BASELINE configs[4])",
             "value": round(steps / T, 4), "unit": "iters/s", "steps": steps, "warmup": a.warmup,
+            "history_fill": fill_n, "h_min": res.get("h_min", -1), "h_max": res.get("h_max", -1),
+            "steady_state": res.get("h_min", -1) == a.history,
             "ms_per_step": round(T / steps * 1e3, 4), "achieved_hbm_gbps": round(bytes_all / T / 1e9, 1),
             "exchange": "xgmi", "x0_generation_s": round(gen_s, 1),
-            "solver": {"status": res["status"], "f": res["f"], "gnorm": res["gnorm"]}}
+            "solver": {"status": res["status"], "f": res["f"], "gnorm": res["gnorm"]},
+            "shard_check": check}
+
+
+FULLSIZE = os.path.join(ROOT, "tests", "golden", "fullsize")
+PARITY_TOL = 1e-10  # BASELINE.json north star: within 1e-10 relative on fp64
+
+
+def fullsize_fixture(a, n):
+    """The committed full-size fixture of this workload (tests/golden/make_fullsize.py: the
+    reference's own trace and the canonical-order oracle's, generated where the reference
+    lives), or (None, None). Data only: nothing under oracle/ is loaded here."""
+    import glob
+
+    for fn in sorted(glob.glob(os.path.join(FULLSIZE, "*.json"))):
+        try:
+            d = json.load(open(fn))
+        except (OSError, ValueError):
+            continue
+        if (d["objective"], d["n"], d["m"], d["method"], d["seed"], d["lo"], d["hi"]) == \
+                (a.objective, n, a.history, a.line_search, 42, -2.0, 2.0):
+            return d, os.path.relpath(fn, ROOT)
+    return None, None
+
+
+def reference_parity(traj, live, fixture, fsrc):
+    """The measured run's own trajectory (the traced history fill and warm-up: f, |g|, alpha and
+    the x checksums at the top of every iteration) against
+      * the reference: the live run of the CPU baseline on this host (N = 1), else the
+        fixture's trace of the reference itself; f and |g| within 1e-10 relative
+        (lbfgs.cpp:72-199 on benchmark.cpp:58-81), and the first k where that fails;
+      * the canonical-order oracle (the fixture): bit for bit."""
+    if traj is None or (live is None and fixture is None):
+        return None
+    gf, gg = np.asarray(traj["tr_f"]), np.asarray(traj["tr_gnorm"])
+    out = {"tolerance": PARITY_TOL, "gpu_iterations_traced": int(len(gf))}
+    u64 = lambda xs: np.array([int(v) for v in xs], dtype=np.uint64)  # noqa: E731
+    f64 = lambda hs: np.array([int(h, 16) for h in hs], dtype=np.uint64).view(np.float64)  # noqa: E731
+    if live is not None:
+        rf, rg, rc1, rc2 = live["f"], live["gnorm"], live["c1"], live["c2"]
+        out["reference"] = "live: oracle/_ref/ref_lbfgs (the reference's sources) on this host, the CPU baseline run"
+        if fixture is not None:  # the box's build of the reference against the committed trace of it
+            fr = fixture["reference"]
+            k = min(len(fr["grad_norm"]), len(rg))
+            out["live_reference_matches_fixture"] = bool(
+                np.array_equal(f64(fr["grad_norm"])[:k].view(np.uint64), rg[:k].view(np.uint64))
+                and np.array_equal(u64(fr["grad_c1"])[:k], rc1[:k]))
+    else:
+        s = fixture["seq"]
+        rf, rg, rc1, rc2 = f64(s["f"]), f64(s["gnorm"]), u64(s["c1"]), u64(s["c2"])
+        out["reference"] = f"fixture: {fsrc} (the reference's own trace, tests/golden/make_fullsize.py)"
+    k = min(len(gf), len(rf))
+    rel_f = np.abs(gf[:k] - rf[:k]) / np.maximum(np.abs(rf[:k]), 1e-300)
+    rel_g = np.abs(gg[:k] - rg[:k]) / np.maximum(np.abs(rg[:k]), 1e-300)
+    bad = np.nonzero((rel_f > PARITY_TOL) | (rel_g > PARITY_TOL))[0]
+    same_x = np.nonzero((np.asarray(traj["tr_c1"])[:k] != rc1[:k]) | (np.asarray(traj["tr_c2"])[:k] != rc2[:k]))[0]
+    out.update(iterations_compared=int(k), max_rel_f=float(rel_f.max()) if k else None,
+               max_rel_gnorm=float(rel_g.max()) if k else None,
+               first_divergent_k=int(bad[0]) if len(bad) else None,
+               x_bit_identical_iterations=int(same_x[0]) if len(same_x) else int(k))
+    ok = k > 0 and not len(bad)
+    if fixture is not None:
+        c = fixture["canon"]
+        kc = min(len(gf), len(c["f"]))
+        ta = np.asarray(traj["tr_alpha"])[:kc - 1]  # the canonical trace's last entry has no step
+        exact = bool(np.array_equal(gf[:kc].view(np.uint64), f64(c["f"])[:kc].view(np.uint64))
+                     and np.array_equal(gg[:kc].view(np.uint64), f64(c["gnorm"])[:kc].view(np.uint64))
+                     and np.array_equal(ta.view(np.uint64), f64(c["alpha"])[:kc - 1].view(np.uint64))
+                     and np.array_equal(np.asarray(traj["tr_c1"])[:kc], u64(c["c1"])[:kc])
+                     and np.array_equal(np.asarray(traj["tr_c2"])[:kc], u64(c["c2"])[:kc]))
+        out["canonical"] = {"fixture": fsrc, "iterations_compared": int(kc), "bit_exact": exact,
+                            "horizons_vs_reference": fixture.get("horizons")}
+        ok = ok and exact
+    out["ok"] = bool(ok)
+    return out
 
 
 def roofline(prof, n, world):
-    if not prof:
+    prof = {k: v for k, v in (prof or {}).items() if not k.startswith("_")}
+    streaming = [k for k in prof if prof[k]["bytes"] > 0]  # not the stage-2 / exchange launches
+    if not streaming:
         return None
-    dom = max(prof, key=lambda k: prof[k]["ms"])
+    dom = max(streaming, key=lambda k: prof[k]["ms"])
     p = prof[dom]
     avg_s = p["ms"] / p["launches"] / 1e3
     per_launch = p["bytes"] / p["launches"]  # this rank's algorithmic bytes per launch
@@ -463,7 +574,7 @@ def main():
     if rank == 0:
         value = done_steps / T
         roof = roofline(prof, n, world)
-        cpu = None
+        cpu, cbs = None, None
         if cpu_runs is not None:
             cbs = cpu_runs.collect()
             main_cb = cbs[0] if cbs else None
@@ -484,6 +595,12 @@ def main():
                                            error=c.get("error")) for c in cbs[1:]])
             elif cbs:
                 cpu = {"error": cbs[0].get("error", "no result")}
+        live = None
+        if cpu_runs is not None and cbs and "trajectory" in cbs[0] and cbs[0]["n"] == n and \
+                a.objective == "rosenbrock" and a.line_search == "backtracking":
+            live = cbs[0]["trajectory"]
+        fixture, fsrc = fullsize_fixture(a, n)
+        parity = reference_parity(res.get("trajectory"), live, fixture, fsrc)
         h_min, h_max = res.get("h_min", -1), res.get("h_max", -1)
         out = {
             "metric": f"L-BFGS iters/sec (n={ntag(n)} {a.objective.capitalize()}, m={a.history}, fp64)",
@@ -515,7 +632,9 @@ def main():
             "bytes_per_step": bytes_all / max(done_steps, 1),
             "roofline": roof,
             "exchange_latency_us": xlat,
+            "exchange_share": prof.get("_exchange_share"),
             "cpu_baseline": cpu,
+            "reference_parity": parity,
             "solver": {"status": res["status"], "f": res["f"], "gnorm": res["gnorm"],
                        "trials_f": res["trials_f"], "commits": res["commits"],
                        "passes": res["passes"]},

@@ -4,8 +4,12 @@
 // parallel-implementation/L-BFGS.cu:105-112) and run on the GPU. The benchmark objectives are
 // recognised through std::function::target and evaluated by the device kernels; any other
 // callable is driven through the host-callback objective.
+#include <dlfcn.h>
+#include <link.h>
+
 #include <cmath>
 #include <cstdint>
+#include <cstring>
 #include <cstdlib>
 #include <limits>
 #include <algorithm>
@@ -146,12 +150,35 @@ const lbfgs_amd::DenseQuadF* dense_f(const FnF& f) {
     return wf ? wf->target<lbfgs_amd::DenseQuadF>() : f.target<lbfgs_amd::DenseQuadF>();
 }
 
+// Is the function pointer p this library's function `own`? Either p is its address as the
+// library sees it, or p is the canonical PLT entry a non-PIE caller (g++ -fno-pic -no-pie) made
+// for it: the address of an UNDEFINED symbol of the caller's module with our function's name,
+// which the dynamic linker binds to this library (protected visibility keeps the library's own
+// references local, so the two addresses differ). A caller that defines its own function of the
+// same name has a defined symbol there and is not ours.
+bool same_function(const void* p, const void* own) {
+    if (p == own) return true;
+    Dl_info mine, theirs;
+    ElfW(Sym)* sym = nullptr;
+    if (!dladdr(own, &mine) || !mine.dli_sname) return false;
+    if (!dladdr1(p, &theirs, reinterpret_cast<void**>(&sym), RTLD_DL_SYMENT) || !sym || !theirs.dli_sname)
+        return false;
+    return sym->st_shndx == SHN_UNDEF && theirs.dli_saddr == p && std::strcmp(theirs.dli_sname, mine.dli_sname) == 0 &&
+           dlsym(RTLD_DEFAULT, mine.dli_sname) == p;
+}
+
 int identify(const FnF& f, const FnG& g, int n) {
     const PlainF* pf = f.target<PlainF>();
     const PlainG* pg = g.target<PlainG>();
     if (pf && pg) {
-        if (*pf == &rosenbrock && *pg == &rosenbrock_grad) return LBFGS_OBJ_ROSENBROCK;
-        if (*pf == &quadratic && *pg == &quadratic_grad) return LBFGS_OBJ_QUAD_SEPARABLE;
+        const void* vf = reinterpret_cast<const void*>(*pf);
+        const void* vg = reinterpret_cast<const void*>(*pg);
+        if (same_function(vf, reinterpret_cast<const void*>(&rosenbrock)) &&
+            same_function(vg, reinterpret_cast<const void*>(&rosenbrock_grad)))
+            return LBFGS_OBJ_ROSENBROCK;
+        if (same_function(vf, reinterpret_cast<const void*>(&quadratic)) &&
+            same_function(vg, reinterpret_cast<const void*>(&quadratic_grad)))
+            return LBFGS_OBJ_QUAD_SEPARABLE;
     }
     const FnFc* wf = f.target<FnFc>();
     const FnGc* wg = g.target<FnGc>();
@@ -287,8 +314,9 @@ double line_search(int ls, const vector<double>& x, const vector<double>& d, con
 // LBFGS_CUDA with LBFGS_CUDA_PROGRESS=1: the CUDA path's progress lines (L-BFGS.cu:115, 297,
 // 307, 350-355) printed after the solve from the device trace (entry k: f and |g| at the top of
 // iteration k, the step iteration k took) instead of the sequential driver's messages; no host
-// f evaluation per iteration. The convergence line uses the CUDA path's <= test (:353).
-void print_cuda_progress(lbfgs_ctx* c, double tolerance) {
+// f evaluation per iteration. The convergence line follows the solver's status (the sequential
+// test, lbfgs.cpp:80), printed where the CUDA path prints it (:353-357).
+void print_cuda_progress(lbfgs_ctx* c, int status) {
     const int len = lbfgs_trace_len(c);
     if (len <= 0) return;
     vector<double> tf(len), tg(len), ta(len);
@@ -302,7 +330,9 @@ void print_cuda_progress(lbfgs_ctx* c, double tolerance) {
         if (k + 1 >= len) break;
         std::cout << "Iteration " << k << ": norm_g = " << tg[k + 1] << std::endl;
         std::cout << "Optimum value: " << tf[k + 1] << std::endl;
-        if (tg[k + 1] <= tolerance) {
+        // the solver's own outcome decides the line: it converged at the top of the trace's last
+        // iteration (a separate comparison with the tolerance could disagree with it at |g| = tol)
+        if (status == LBFGS_STATUS_CONVERGED && k + 1 == len - 1) {
             std::cout << "Convergence achieved at iteration " << k << std::endl;
             break;
         }
@@ -345,7 +375,7 @@ vector<double> run(const FnF& f, const FnG& grad, const vector<double>& x0, int 
                             max_iterations, tolerance, flags, &res);
     if (!hf.error.empty()) throw std::runtime_error("objective callback failed: " + hf.error);
     if (rc < 0) throw std::runtime_error(std::string("LBFGS failed: ") + lbfgs_last_error(c));
-    if (cuda_progress) print_cuda_progress(c, tolerance);
+    if (cuda_progress) print_cuda_progress(c, res.status);
     return x;
 }
 

@@ -81,7 +81,8 @@ extern "C" {
 enum {
     LBK_K_DOT = 0, LBK_K_AXPY_DOT, LBK_K_MID, LBK_K_AXPY2_DOT, LBK_K_LAST, LBK_K_NEGDOT,
     LBK_K_EVAL, LBK_K_TRIAL_F, LBK_K_TRIAL_FG, LBK_K_COMMIT, LBK_K_POINT, LBK_K_CHECKSUM,
-    LBK_K_UPDATE, LBK_K_VF_COMMIT, LBK_K_VF_DIR, LBK_K_SMALL_ITER, LBK_K_GROUP_REDUCE, LBK_K_COUNT
+    LBK_K_UPDATE, LBK_K_VF_COMMIT, LBK_K_VF_DIR, LBK_K_SMALL_ITER, LBK_K_GROUP_REDUCE,
+    LBK_K_EXCHANGE /* sharded: a reduction exchange (mailbox kernel or RCCL all-gather) */, LBK_K_COUNT
 };
 
 typedef struct {

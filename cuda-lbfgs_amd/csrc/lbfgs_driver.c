@@ -257,8 +257,11 @@ int lbfgs_spec_stats(const lbfgs_ctx* c, int64_t* adopted, int64_t* dropped) {
     return 0;
 }
 
+#ifndef LBFGS_ARCH
+#define LBFGS_ARCH "unknown"
+#endif
 const char* lbfgs_build_info(void) {
-    return "src=" LBFGS_SRC_HASH " built=" __DATE__ " " __TIME__ " arch=gfx950";
+    return "src=" LBFGS_SRC_HASH " built=" __DATE__ " " __TIME__ " arch=" LBFGS_ARCH;
 }
 
 int lbfgs_unique_id(void* out128) { return lbk_unique_id(out128) == 0 ? 0 : LBFGS_ERR_RCCL; }
@@ -1834,6 +1837,15 @@ int lbfgs_messages(const lbfgs_ctx* c, char* buf, int cap) {
 }
 
 int lbfgs_trace_len(const lbfgs_ctx* c) { return c ? c->tr_len : 0; }
+
+int lbfgs_trace_enable(lbfgs_ctx* c, int on) {
+    if (!c || !c->inited) return LBFGS_ERR_STATE;
+    if (on)
+        c->flags |= LBFGS_FLAG_TRACE;
+    else
+        c->flags &= ~LBFGS_FLAG_TRACE;
+    return 0;
+}
 
 int lbfgs_trace_get(const lbfgs_ctx* c, double* f, double* gnorm, double* alpha, uint64_t* c1,
                     uint64_t* c2, int cap) {

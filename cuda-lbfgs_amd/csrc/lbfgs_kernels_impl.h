@@ -2470,6 +2470,23 @@ int exchange_slot(lbk_ctx* c, int slot, int K = 1, bool host_read = true) {
     return rc;
 }
 
+// exchange_slot bracketed by events when profiling (LBK_K_EXCHANGE: bench.py's exchange_share)
+int exchange_timed(lbk_ctx* c, int slot, int K = 1, bool host_read = true) {
+    hipEvent_t a = nullptr, b = nullptr;
+    if (c->prof_on) {
+        if (c->pending.size() > 4096 && prof_flush(c) != 0) return -2;
+        a = ev_get(c);
+        b = ev_get(c);
+        if (a) HIPCHK(c, hipEventRecord(a, c->stream));
+    }
+    const int rc = exchange_slot(c, slot, K, host_read);
+    if (a && b) {
+        HIPCHK(c, hipEventRecord(b, c->stream));
+        c->pending.push_back({LBK_K_EXCHANGE, a, b, 0.0});
+    }
+    return rc;
+}
+
 // Deferred partials live in the two highest components of the partials array: a consuming launch
 // reads them while its own workgroups store their partials (components 0..K-1, K <= 87), and a
 // deferred producer and its consumer alternate between the two.
@@ -2570,7 +2587,7 @@ int launch(lbk_ctx* c, int kind, double vec_passes, int slot, F&& fn, int K = 1,
         HIPCHK(c, hipEventRecord(b, c->stream));
         c->pending.push_back({kind, a, b, 0.0});
     }
-    if (exchange && (c->geo.world > 1 || c->comm) && slot >= 0) return exchange_slot(c, slot, K);
+    if (exchange && (c->geo.world > 1 || c->comm) && slot >= 0) return exchange_timed(c, slot, K);
     return 0;
 }
 

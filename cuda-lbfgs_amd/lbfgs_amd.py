@@ -23,7 +23,7 @@ FLAG_VERBOSE, FLAG_QUIET, FLAG_TRACE, FLAG_UNFUSED, FLAG_VECTOR_FREE = 1, 2, 4, 
 FLAG_REFERENCE_CALLS = 32
 KERNELS = ["dot", "axpy_dot", "mid", "axpy2_dot", "last", "negdot", "eval", "trial_f",
            "trial_fg", "commit", "point", "checksum", "update", "vf_commit", "vf_dir", "small_iter",
-           "group_reduce"]
+           "group_reduce", "exchange"]
 
 
 class LbfgsError(RuntimeError):
@@ -100,6 +100,7 @@ def lib():
     L.lbfgs_sync.argtypes = [vp]
     L.lbfgs_messages.argtypes = [vp, C.c_char_p, C.c_int]
     L.lbfgs_trace_len.argtypes = [vp]
+    L.lbfgs_trace_enable.argtypes = [vp, C.c_int]
     L.lbfgs_trace_get.argtypes = [vp, dp, dp, dp, np.ctypeslib.ndpointer(dtype=np.uint64),
                                   np.ctypeslib.ndpointer(dtype=np.uint64), C.c_int]
     L.lbfgs_dev_dot.argtypes = [vp, dp, dp, C.POINTER(C.c_double)]
@@ -131,6 +132,7 @@ EXPORTED_SYMBOLS = [
     "lbfgs_host_group_destroy", "lbfgs_ctx_create_emulated", "lbfgs_ctx_destroy", "lbfgs_last_error",
     "lbfgs_local_range", "lbfgs_shard_range", "lbfgs_minimize", "lbfgs_solver_init", "lbfgs_solver_step",
     "lbfgs_get_x", "lbfgs_sync", "lbfgs_messages", "lbfgs_trace_len", "lbfgs_trace_get",
+    "lbfgs_trace_enable",
     "lbfgs_dev_dot", "lbfgs_dev_norm", "lbfgs_dev_objective", "lbfgs_dev_trial",
     "lbfgs_dev_twoloop", "lbfgs_dev_elementwise", "lbfgs_line_search", "lbfgs_prof_enable",
     "lbfgs_prof_reset", "lbfgs_prof_get", "lbfgs_peer_handle", "lbfgs_peer_connect", "lbfgs_peer_enable",
@@ -413,6 +415,12 @@ class Context:
         buf = C.create_string_buffer(1 << 20)
         lib().lbfgs_messages(self.h, buf, len(buf))
         return buf.value.decode()
+
+    def trace_enable(self, on=True):
+        """Record (or stop recording) the per-iteration trace between step() calls."""
+        rc = lib().lbfgs_trace_enable(self.h, 1 if on else 0)
+        if rc != 0:
+            self._err("lbfgs_trace_enable", rc)
 
     def trace(self):
         n = lib().lbfgs_trace_len(self.h)

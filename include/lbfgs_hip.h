@@ -229,6 +229,11 @@ int lbfgs_messages(const lbfgs_ctx* ctx, char* buf, int cap);
 int lbfgs_trace_len(const lbfgs_ctx* ctx);
 int lbfgs_trace_get(const lbfgs_ctx* ctx, double* f, double* gnorm, double* alpha,
                     uint64_t* c1, uint64_t* c2, int cap);
+/* switch the trace on or off between lbfgs_solver_step calls of an initialised solve (entries
+ * recorded so far are kept): bench.py traces the untimed history fill and warm-up, whose f / |g|
+ * it checks against the reference, and times the steps after it untraced (the x checksums are
+ * extra passes) */
+int lbfgs_trace_enable(lbfgs_ctx* ctx, int on);
 
 /* ---- line search alone (line_search.h:10-26 on the GPU) -------------------------------- */
 /* Step size along d from x (gradient g at x) by one of the four line searches, every trial on
@@ -262,6 +267,9 @@ enum {
     LBFGS_KERNEL_TRIAL_FG, LBFGS_KERNEL_COMMIT, LBFGS_KERNEL_POINT, LBFGS_KERNEL_CHECKSUM,
     LBFGS_KERNEL_UPDATE, LBFGS_KERNEL_VF_COMMIT, LBFGS_KERNEL_VF_DIR,
     LBFGS_KERNEL_SMALL_ITER, LBFGS_KERNEL_GROUP_REDUCE /* stage 2 of the reductions */,
+    /* sharded runs: each reduction's exchange between ranks (the xGMI mailbox kernel, waiting
+     * for the peers included, or the RCCL all-gather); bytes 0 */
+    LBFGS_KERNEL_EXCHANGE,
     LBFGS_KERNEL_COUNT
 };
 void lbfgs_prof_enable(lbfgs_ctx* ctx, int on);

@@ -59,3 +59,59 @@ def test_cpu_baseline_runner(bench):
     assert [o["n"] for o in out] == [3000, 1000]
     for o in out:
         assert o["per_iter_s"] > 0 and o["iters_timed"] == 2 and isinstance(o["pinned"], bool)
+
+
+def test_roofline_ignores_exchange_and_stage2(bench):
+    """The dominant kernel is the streaming pass with the most time: a long exchange wait (bytes 0)
+    or a stage-2 launch never becomes the roofline kernel."""
+    prof = {"axpy_dot": {"ms": 560.0, "launches": 1000, "bytes": 3.2e12},
+            "exchange": {"ms": 5000.0, "launches": 2000, "bytes": 0.0},
+            "group_reduce": {"ms": 900.0, "launches": 900, "bytes": 0.0},
+            "_exchange_share": {"share_max_over_ranks": 0.5}}
+    assert bench.roofline(prof, 10 ** 8, 8)["kernel"] == "axpy_dot"
+
+
+def _trajectory(o):
+    return dict(tr_f=o["f"], tr_gnorm=o["gnorm"], tr_alpha=o["alpha"], tr_c1=o["c1"], tr_c2=o["c2"])
+
+
+def test_reference_parity_live_and_fixture(bench):
+    """reference_parity: the trajectory of the measured run (here the canonical-order oracle, which
+    the GPU reproduces bit for bit) against the reference's live CPU-baseline run, and against a
+    fixture of the canonical order (bit for bit; one flipped bit is caught)."""
+    import numpy as np
+
+    import oracle_lib as O
+
+    if not os.path.exists(os.path.join(ROOT, "oracle", "_ref", "ref_lbfgs")):
+        pytest.skip("oracle/_ref not built (needs /root/reference)")
+    n, m = 3000, 3
+    aff = os.sched_getaffinity(0)
+    try:
+        live = bench.CpuBaseline([n], m).collect(timeout=120)[0]["trajectory"]
+    finally:
+        os.sched_setaffinity(0, aff)
+    x0 = O.x0_uniform(n, 42, -2.0, 2.0)
+    can = O.lbfgs("rosenbrock", x0, "backtracking", m, 2 * m + 2, 1e-5, mode=O.CANON)
+    traj = _trajectory(can)
+    p = bench.reference_parity(traj, live, None, None)
+    assert p["ok"] and p["iterations_compared"] == m + 3 and p["first_divergent_k"] is None
+    assert p["max_rel_f"] <= 1e-10 and p["x_bit_identical_iterations"] >= 2  # x_0, x_1 = x_0 - g_0
+    hexes = lambda a: [f"{int(u):016x}" for u in np.asarray(a, np.float64).view(np.uint64)]  # noqa: E731
+    seq = O.lbfgs("rosenbrock", x0, "backtracking", m, m + 2, 1e-5, mode=O.SEQ)
+    canon_short = O.lbfgs("rosenbrock", x0, "backtracking", m, m + 2, 1e-5, mode=O.CANON)
+    fx = {"reference": {"grad_norm": hexes(live["gnorm"]), "grad_c1": [str(int(v)) for v in live["c1"]]},
+          "seq": {"f": hexes(seq["f"]), "gnorm": hexes(seq["gnorm"]), "c1": [str(int(v)) for v in seq["c1"]],
+                  "c2": [str(int(v)) for v in seq["c2"]]},
+          "canon": {"f": hexes(canon_short["f"]), "gnorm": hexes(canon_short["gnorm"]),
+                    "alpha": hexes(canon_short["alpha"]), "c1": [str(int(v)) for v in canon_short["c1"]],
+                    "c2": [str(int(v)) for v in canon_short["c2"]]},
+          "horizons": {"ref": [m + 3, m + 3]}}
+    p = bench.reference_parity(traj, live, fx, "fixture.json")
+    assert p["ok"] and p["canonical"]["bit_exact"] and p["live_reference_matches_fixture"]
+    p = bench.reference_parity(traj, None, fx, "fixture.json")  # sharded lines: the fixture's reference
+    assert p["ok"] and p["reference"].startswith("fixture")
+    bad = dict(traj, tr_f=traj["tr_f"].copy())
+    bad["tr_f"][2] = np.nextafter(bad["tr_f"][2], np.inf)
+    p = bench.reference_parity(bad, live, fx, "fixture.json")
+    assert not p["canonical"]["bit_exact"] and not p["ok"]

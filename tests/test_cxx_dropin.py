@@ -115,11 +115,14 @@ def test_reference_main_compiles_unchanged():
     assert os.path.exists(REF_MAIN_EXE)
 
 
-def test_caller_defined_objective_is_not_replaced(tmp_path):
+@pytest.mark.parametrize("link", [[], ["-fno-pic", "-no-pie"]], ids=["pie", "no-pie"])
+def test_caller_defined_objective_is_not_replaced(tmp_path, link):
     """identify() only maps THIS library's rosenbrock / quadratic / generate_quadratic_* to device
     kernels (protected symbols). A caller's own function of the same name (main.cpp:7-21 defines
     quadratic) stays the caller's and runs as a host callback. Without a GPU the solve throws after
-    the objective has been classified; with one it runs (n = 50)."""
+    the objective has been classified; with one it runs (n = 50). A non-PIE caller takes the
+    library's rosenbrock through a canonical PLT entry of its own (a different address from the
+    library's protected one), which identify() recognises by the undefined symbol behind it."""
     src = tmp_path / "own.cpp"
     src.write_text(r'''
 #include <cstdio>
@@ -140,8 +143,8 @@ int main() {
 }
 ''')
     exe = tmp_path / "own"
-    subprocess.run(["g++", "-std=c++17", "-O2", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe),
-                    "-L", PKG, "-l:liblbfgs_hip.so", "-Wl,-rpath," + PKG], check=True, capture_output=True)
+    subprocess.run(["g++", "-std=c++17", "-O2", *link, "-I", os.path.join(ROOT, "include"), str(src), "-o",
+                    str(exe), "-L", PKG, "-l:liblbfgs_hip.so", "-Wl,-rpath," + PKG], check=True, capture_output=True)
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     line = [ln for ln in r.stdout.splitlines() if ln.startswith("IDS ")][0]
@@ -316,8 +319,8 @@ def test_cuda_progress_lines(tmp_path):
     src = tmp_path / "p.cpp"
     src.write_text(_PROGRESS_CALLER)
     exe = tmp_path / "p"
-    subprocess.run(["g++", "-std=c++17", "-O2", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe),
-                    "-L", PKG, "-l:liblbfgs_hip.so", "-Wl,-rpath," + PKG], check=True, capture_output=True)
+    subprocess.run(["g++", "-std=c++17", "-O2", *link, "-I", os.path.join(ROOT, "include"), str(src), "-o",
+                    str(exe), "-L", PKG, "-l:liblbfgs_hip.so", "-Wl,-rpath," + PKG], check=True, capture_output=True)
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120,
                        env=dict(os.environ, LBFGS_CUDA_PROGRESS="1"))
     assert r.returncode == 0, r.stderr

@@ -1,0 +1,123 @@
+"""Parity at the BASELINE configs' own sizes.
+
+* configs[2] — Rosenbrock n = 1e8, m = 10, backtracking, the 12 iterations the bench's CPU
+  baseline runs — and configs[3] — tridiagonal quadratic n = 1e8, m = 20, Wolfe, to convergence:
+  the GPU trajectory is bit-exact with the canonical-order oracle at full size, and within 1e-10
+  relative of the reference itself over the reference's own order-sensitivity horizon
+  (tests/golden/fullsize/*.json, made by tests/golden/make_fullsize.py from oracle/_ref/ref_lbfgs
+  — the reference's sequential sources — and the oracle, which reproduces that run call for call).
+* configs[4]'s exchange exactly as bench.py's config4() runs it: 8 processes, no RCCL
+  communicator (the xGMI peer mailboxes alone), the ticket stage 2 of segments >= 8192 elements
+  (n = 8192^2 + 1, the smallest such n, L = 8320), m = 10, backtracking and Wolfe, plus the
+  vector-free mode: bit-identical with the one-GPU run. The box has one GPU, so the 8 ranks share
+  it; the mailboxes, wire format, epochs and bootstrap are those of the cross-GPU case.
+"""
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "cuda-lbfgs_amd"))
+import lbfgs_amd as L  # noqa: E402
+from test_gpu_xgmi import run_ranks  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+FULLSIZE = os.path.join(ROOT, "tests", "golden", "fullsize")
+TOL = 1e-10
+
+
+def bits(a):
+    return np.ascontiguousarray(a, np.float64).view(np.uint64)
+
+
+def f64(hexes):
+    return np.array([int(h, 16) for h in hexes], dtype=np.uint64).view(np.float64)
+
+
+def u64(decs):
+    return np.array([int(v) for v in decs], dtype=np.uint64)
+
+
+def np_checksum(x):
+    u = np.ascontiguousarray(x, np.float64).view(np.uint64)
+    with np.errstate(over="ignore"):
+        return str(int(u.sum(dtype=np.uint64))), str(int((u * np.arange(1, len(u) + 1, dtype=np.uint64)).sum(dtype=np.uint64)))
+
+
+def horizon(a, b):
+    k = min(len(a), len(b))
+    r = np.abs(a[:k] - b[:k]) / np.maximum(np.abs(b[:k]), 1e-300)
+    bad = np.nonzero(r > TOL)[0]
+    return int(bad[0]) if len(bad) else int(k)
+
+
+@pytest.mark.parametrize("name", ["config2_n1e8", "config3_n1e8"])
+def test_fullsize_parity(name):
+    fx = json.load(open(os.path.join(FULLSIZE, name + ".json")))
+    n, m = fx["n"], fx["m"]
+    x0 = L.x0_uniform(n, fx["seed"], fx["lo"], fx["hi"])
+    with L.Context(n, m) as c:
+        r = c.minimize(fx["objective"], x0, fx["method"], fx["maxit"], tolerance=fx["tol"], trace=True)
+    del x0
+    # bit for bit with the canonical-order oracle, whole run
+    can = fx["canon"]
+    assert r["status"] == can["status"] and r["iterations"] == can["iterations"]
+    assert np.array_equal(bits(r["tr_f"]), bits(f64(can["f"])))
+    assert np.array_equal(bits(r["tr_gnorm"]), bits(f64(can["gnorm"])))
+    ta, ca = r["tr_alpha"], f64(can["alpha"])
+    assert np.array_equal(np.isnan(ta), np.isnan(ca)) and np.array_equal(bits(ta[~np.isnan(ta)]), bits(ca[~np.isnan(ca)]))
+    assert np.array_equal(r["tr_c1"], u64(can["c1"])) and np.array_equal(r["tr_c2"], u64(can["c2"]))
+    assert r["messages"] == can["messages"]
+    assert list(np_checksum(r["x"])) == can["x_checksum"]
+    # against the reference itself: f and |g| within 1e-10 relative at least as far as the
+    # reference agrees with itself under another summation order, and the same outcome
+    seq = fx["seq"]
+    rf, rg = f64(seq["f"]), f64(seq["gnorm"])
+    kf, kg = fx["horizons"]["ref"]
+    assert horizon(r["tr_f"], rf) >= kf and horizon(r["tr_gnorm"], rg) >= kg, (
+        horizon(r["tr_f"], rf), horizon(r["tr_gnorm"], rg), fx["horizons"])
+    assert r["status"] == seq["status"]
+    assert r["messages"].strip().splitlines()[-1] == fx["reference"]["stdout"].strip().splitlines()[-1]
+    if r["status"] == "converged":
+        assert r["gnorm"] < fx["tol"]
+    # backtracking takes the unit steepest-descent step first: x_1 = x_0 - g_0 involves no
+    # reduction, so it has the reference's bits (the checksum of its grad() argument)
+    if fx["method"] == "backtracking":
+        assert r["tr_c1"][1] == int(fx["reference"]["grad_c1"][1])
+        assert r["tr_c2"][1] == int(fx["reference"]["grad_c2"][1])
+
+
+N4 = 8192 * 8192 + 1
+_one_gpu = {}
+
+
+def _single(ls, iters, vf):
+    key = (ls, iters, vf)
+    if key not in _one_gpu:
+        x0 = L.x0_uniform(N4, 42, -2.0, 2.0)
+        with L.Context(N4, 10) as c:
+            _one_gpu[key] = c.minimize("rosenbrock", x0, ls, iters, trace=True, vector_free=vf)
+    return _one_gpu[key]
+
+
+@pytest.mark.parametrize("ls,mode", [("backtracking", "default"), ("wolfe", "default"),
+                                     ("backtracking", "vf")])
+def test_config4_mailboxes_8_processes(tmp_path, ls, mode):
+    iters = 13  # h reaches m = 10 (the ring full) for the last iterations
+    ref = _single(ls, iters, mode == "vf")
+    # the library's own stage-2 and mirror choices, as bench.py runs it
+    outs = run_ranks(tmp_path, 8, N4, 10, "rosenbrock", ls, iters, mode,
+                     unset=("LBFGS_TICKET", "LBFGS_XGMI_MIRROR"))
+    x = np.zeros(N4)
+    for r, o in enumerate(outs):
+        for key in ("tr_f", "tr_gnorm", "tr_alpha"):
+            assert np.array_equal(bits(o[key]), bits(ref[key])), (r, key)
+        assert np.array_equal(o["tr_c1"], ref["tr_c1"]) and np.array_equal(o["tr_c2"], ref["tr_c2"]), r
+        assert str(o["messages"]) == ref["messages"]
+        lo = int(o["lo"])
+        x[lo:lo + len(o["x"])] = o["x"]
+    assert np.array_equal(bits(x), bits(ref["x"]))
+    assert ref["h_max"] == 10

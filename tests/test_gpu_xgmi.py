@@ -24,8 +24,8 @@ def bits(a):
     return np.asarray(a, dtype=np.float64).view(np.uint64)
 
 
-def run_ranks(tmp_path, world, n, m, obj, ls, iters, mode, env=None):
-    e = dict(os.environ)
+def run_ranks(tmp_path, world, n, m, obj, ls, iters, mode, env=None, unset=()):
+    e = {k: v for k, v in os.environ.items() if k not in unset}
     e.update(env or {})
     procs = [subprocess.Popen([sys.executable, WORKER, str(tmp_path), str(r), str(world), str(n), str(m), obj, ls,
                                str(iters), mode], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=e)

@@ -29,35 +29,49 @@ import numpy as np  # noqa: E402
 
 
 def timed_steps(n, m, obj, ls, warm, steps, tol=1e-5, unfused=False, vector_free=False):
+    """m untimed iterations fill the history first (as bench.py), so every timed step has h = m;
+    h_min / h_max of the timed steps are reported"""
     x0 = L.x0_uniform(n, 42, -2.0, 2.0)
     with L.Context(n, m) as c:
         c.init(obj, x0, ls, tolerance=tol, unfused=unfused, vector_free=vector_free)
         del x0
+        fill = c.step(m)
         c.step(warm)
         c.sync()
         t0 = time.perf_counter()
         r = c.step(steps)
         c.sync()
         dt = time.perf_counter() - t0
-    done = steps if r["status"] == "running" else max(r["iterations"] - warm, 1)
+    done = steps if r["status"] == "running" else max(r["iterations"] - warm - fill["iterations"], 1)
     return dict(n=n, m=m, objective=obj, line_search=ls,
                 kernels="unfused" if unfused else "vector_free" if vector_free else "fused",
-                warmup=warm, steps=done, seconds=dt,
+                history_fill=fill["iterations"], warmup=warm, steps=done, h_min=r["h_min"], h_max=r["h_max"],
+                steady_state=r["h_min"] == m, seconds=dt,
                 iters_per_s=done / dt, ms_per_iter=1e3 * dt / done, gbps=r["bytes"] / dt / 1e9,
                 status=r["status"], f=r["f"], gnorm=r["gnorm"])
 
 
 def to_solution(n, m, obj, ls, maxit, tol=1e-5, vector_free=False):
+    """time to solution through lbfgs_minimize (x0 upload and x download included), and the same
+    solve with x0 already resident (lbfgs_solver_init untimed, then the steps)"""
     x0 = L.x0_uniform(n, 42, -2.0, 2.0)
     with L.Context(n, m) as c:
         t0 = time.perf_counter()
         r = c.minimize(obj, x0, ls, maxit, tolerance=tol, vector_free=vector_free)
         dt = time.perf_counter() - t0
+        c.init(obj, x0, ls, tolerance=tol, vector_free=vector_free)
+        c.sync()
+        t1 = time.perf_counter()
+        r2 = c.step(maxit)
+        c.sync()
+        dt2 = time.perf_counter() - t1
     return dict(n=n, m=m, objective=obj, line_search=ls, kernels="vector_free" if vector_free else "fused",
-                seconds=dt, iterations=r["iterations"],
+                seconds=dt, seconds_x0_resident=dt2, iterations=r["iterations"],
                 status=r["status"], f=r["f"], gnorm=r["gnorm"], trials_f=r["trials_f"],
                 trials_fg=r["trials_fg"], gbps=r["bytes"] / dt / 1e9,
-                note="includes x0 upload and result download")
+                same_result_resident=(r2["iterations"] == r["iterations"] and r2["f"] == r["f"]),
+                note="seconds: lbfgs_minimize incl. x0 upload and result download; seconds_x0_resident: "
+                     "the solve alone (init untimed, no download)")
 
 
 def cpu_reference(n, m, iters):
