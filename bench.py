@@ -479,13 +479,27 @@ def reference_parity(traj, live, fixture, fsrc):
     k = min(len(gf), len(rf))
     rel_f = np.abs(gf[:k] - rf[:k]) / np.maximum(np.abs(rf[:k]), 1e-300)
     rel_g = np.abs(gg[:k] - rg[:k]) / np.maximum(np.abs(rg[:k]), 1e-300)
-    bad = np.nonzero((rel_f > PARITY_TOL) | (rel_g > PARITY_TOL))[0]
+    bad_f, bad_g = np.nonzero(rel_f > PARITY_TOL)[0], np.nonzero(rel_g > PARITY_TOL)[0]
+    hf = int(bad_f[0]) if len(bad_f) else int(k)  # leading iterations within tolerance
+    hg = int(bad_g[0]) if len(bad_g) else int(k)
     same_x = np.nonzero((np.asarray(traj["tr_c1"])[:k] != rc1[:k]) | (np.asarray(traj["tr_c2"])[:k] != rc2[:k]))[0]
     out.update(iterations_compared=int(k), max_rel_f=float(rel_f.max()) if k else None,
                max_rel_gnorm=float(rel_g.max()) if k else None,
-               first_divergent_k=int(bad[0]) if len(bad) else None,
+               first_divergent_k=min(hf, hg) if min(hf, hg) < k else None,
+               within_tolerance_iterations={"f": hf, "gnorm": hg},
                x_bit_identical_iterations=int(same_x[0]) if len(same_x) else int(k))
-    ok = k > 0 and not len(bad)
+    # The bar: no parallel summation order can match the reference's left-to-right sums
+    # indefinitely; the fixture records how many leading iterations the
+    # reference itself keeps within 1e-10 under another equally valid order (K_ref). The run
+    # passes when its own horizon reaches K_ref (capped at the iterations compared); without a
+    # fixture every compared iteration must be within tolerance.
+    kref = (fixture or {}).get("horizons", {}).get("ref")
+    if kref:
+        need_f, need_g = min(int(kref[0]), k), min(int(kref[1]), k)
+        out["reference_self_horizon"] = {"f": int(kref[0]), "gnorm": int(kref[1])}
+    else:
+        need_f = need_g = k
+    ok = k > 0 and hf >= need_f and hg >= need_g
     if fixture is not None:
         c = fixture["canon"]
         kc = min(len(gf), len(c["f"]))
@@ -495,8 +509,7 @@ def reference_parity(traj, live, fixture, fsrc):
                      and np.array_equal(ta.view(np.uint64), f64(c["alpha"])[:kc - 1].view(np.uint64))
                      and np.array_equal(np.asarray(traj["tr_c1"])[:kc], u64(c["c1"])[:kc])
                      and np.array_equal(np.asarray(traj["tr_c2"])[:kc], u64(c["c2"])[:kc]))
-        out["canonical"] = {"fixture": fsrc, "iterations_compared": int(kc), "bit_exact": exact,
-                            "horizons_vs_reference": fixture.get("horizons")}
+        out["canonical"] = {"fixture": fsrc, "iterations_compared": int(kc), "bit_exact": exact}
         ok = ok and exact
     out["ok"] = bool(ok)
     return out

@@ -125,6 +125,9 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
     c->coop_max = 256;
     if (const char* e = getenv("LBFGS_COOP")) c->coop_max = std::min(atoi(e), LBK_COOP_SEGMAX);  // max segments
     c->pend_slot = -1;
+    c->xf_slot = -1;
+    c->fold_env = 1;  // folded exchanges over the mailboxes; LBFGS_XGMI_FOLD=0: off
+    if (const char* e = getenv("LBFGS_XGMI_FOLD")) c->fold_env = atoi(e) != 0;
     // measured (profiles/r01/defer_ab.txt): +21..32 % at n = 3e5 (586 segments); -14 % at 1954
     // segments and worse beyond, where every workgroup forms two or more group trees
     c->defer_max = LBK_SEG_PER_GROUP;
@@ -199,7 +202,25 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
         CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, k_coop_iter<LBK_OBJ_QUAD_SEPARABLE>, LB_BLOCK, 0));
         occ = std::min(occ, o);
         c->coop_max = (int)std::min<int64_t>(c->coop_max, (int64_t)occ * cus);
+        // the persistent iteration (LBFGS_PERSIST=1): every workgroup of its grid resident, at most
+        // 4 per CU. The occupancy answer is VGPR-bound here (165 VGPRs: 3 per CU), where the API and
+        // the hardware agree; MI355X_MICROARCH.md's one-short case is SGPR-bound (82-98 SGPRs at
+        // 7-8 per CU). A grid that does not fit still ends: every flagged wait times out (2 s).
+        int po = 1 << 30;
+        CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, (k_persist_iter<LBK_OBJ_ROSENBROCK, true>), LB_BLOCK, 0));
+        po = std::min(po, o);
+        CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, (k_persist_iter<LBK_OBJ_QUAD_TRIDIAG, true>), LB_BLOCK, 0));
+        po = std::min(po, o);
+        CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, (k_persist_iter<LBK_OBJ_QUAD_SEPARABLE, true>), LB_BLOCK, 0));
+        po = std::min(po, o);
+        c->persist_gmax = std::min(po, 4) * cus;
     }
+    c->persist_on = 0;
+    if (const char* e = getenv("LBFGS_PERSIST")) c->persist_on = atoi(e) != 0;
+    CK(hipMalloc(&c->persist_cnt, sizeof(unsigned long long) * LBK_GROUPS));
+    CK(hipMemset(c->persist_cnt, 0, sizeof(unsigned long long) * LBK_GROUPS));
+    CK(hipMalloc(&c->persist_gflag, sizeof(unsigned long long) * 2 * 8 * 8 * 2));
+    CK(hipMemset(c->persist_gflag, 0, sizeof(unsigned long long) * 2 * 8 * 8 * 2));
     CK(hipDeviceSynchronize());
 #undef CK
     if (world > 1 && !grp) {
@@ -252,6 +273,8 @@ void lbk_destroy(lbk_ctx* c) {
     if (c->d_ckslot) (void)hipFree(c->d_ckslot);
     (void)hipFree(c->partials);
     (void)hipFree(c->coop_ll);
+    (void)hipFree(c->persist_cnt);
+    (void)hipFree(c->persist_gflag);
     if (c->coop_err_h) (void)hipHostFree(c->coop_err_h);
     if (c->sp_h) (void)hipHostFree(c->sp_h);
     if (c->sp_vd) (void)hipFree(c->sp_vd);
@@ -362,8 +385,12 @@ int lbk_copy(lbk_ctx* c, double* dst, const double* src) {
 int lbk_dot(lbk_ctx* c, const double* a, const double* b, int slot) {
     Geo g = kgeo(c);
     Red r = kred_deferrable(c, slot);
+    fold_producer(c, r, false);
     return launch(c, LBK_K_DOT, 2, slot, [&] {
-        NT_DISPATCH(c, hipLaunchKernelGGL(k_dot<NT_>, dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, a, b, g, r));
+        if (r.fp.peers)
+            NT_DISPATCH(c, hipLaunchKernelGGL((k_dot<NT_, true>), dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, a, b, g, r));
+        else
+            NT_DISPATCH(c, hipLaunchKernelGGL(k_dot<NT_>, dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, a, b, g, r));
     });
 }
 
@@ -371,10 +398,15 @@ int lbk_axpy_dot(lbk_ctx* c, double* qout, const double* qin, const double* y, c
                  int ref_alpha, int slot) {
     Geo g = kgeo(c);
     g.ppart = take_pending(c, ref_alpha);
+    const FoldSrc fs = take_fold(c, ref_alpha);
     Red r = kred_deferrable(c, slot);
+    fold_producer(c, r, false);
     const double* pa = sref(c, ref_alpha);
     return launch(c, LBK_K_AXPY_DOT, 4, slot, [&] {
-        NT_DISPATCH(c, hipLaunchKernelGGL(k_axpy_dot<NT_>, dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, qout, qin, y, s, rho, pa, g, r));
+        if (r.fp.peers || fs.mbx)
+            NT_DISPATCH(c, hipLaunchKernelGGL((k_axpy_dot<NT_, true>), dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, qout, qin, y, s, rho, pa, g, r, fs));
+        else
+            NT_DISPATCH(c, hipLaunchKernelGGL(k_axpy_dot<NT_>, dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, qout, qin, y, s, rho, pa, g, r, fs));
     });
 }
 
@@ -382,11 +414,16 @@ int lbk_mid(lbk_ctx* c, double* rout, const double* qin, const double* y0, doubl
             int ref_alpha, int slot) {
     Geo g = kgeo(c);
     g.ppart = take_pending(c, ref_alpha);
+    const FoldSrc fs = take_fold(c, ref_alpha);
     Red r = kred_deferrable(c, slot);
+    fold_producer(c, r, true);
     const double* pa = sref(c, ref_alpha);
     if (c->geo.world > 1) g.edge_slot = r.slot;
     return launch(c, LBK_K_MID, 3, slot, [&] {
-        NT_DISPATCH(c, hipLaunchKernelGGL(k_mid<NT_>, dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, rout, qin, y0, rho0, gamma, pa, g, r));
+        if (r.fp.peers || fs.mbx)
+            NT_DISPATCH(c, hipLaunchKernelGGL((k_mid<NT_, true>), dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, rout, qin, y0, rho0, gamma, pa, g, r, fs));
+        else
+            NT_DISPATCH(c, hipLaunchKernelGGL(k_mid<NT_>, dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, rout, qin, y0, rho0, gamma, pa, g, r, fs));
     });
 }
 
@@ -394,12 +431,17 @@ int lbk_axpy2_dot(lbk_ctx* c, double* rr, const double* rin, const double* s, co
                   int ref_beta, int ref_alpha, int slot) {
     Geo g = kgeo(c);
     g.ppart = take_pending(c, ref_beta);
+    const FoldSrc fs = take_fold(c, ref_beta);
     Red r = kred_deferrable(c, slot);
+    fold_producer(c, r, true);
     const double* pb = sref(c, ref_beta);
     const double* pa = sref(c, ref_alpha);
     if (c->geo.world > 1) g.edge_slot = r.slot;
     return launch(c, LBK_K_AXPY2_DOT, 4, slot, [&] {
-        NT_DISPATCH(c, hipLaunchKernelGGL(k_axpy2_dot<NT_>, dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, rr, rin, s, ynext, rho, pb, pa, g, r));
+        if (r.fp.peers || fs.mbx)
+            NT_DISPATCH(c, hipLaunchKernelGGL((k_axpy2_dot<NT_, true>), dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, rr, rin, s, ynext, rho, pb, pa, g, r, fs));
+        else
+            NT_DISPATCH(c, hipLaunchKernelGGL(k_axpy2_dot<NT_>, dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, rr, rin, s, ynext, rho, pb, pa, g, r, fs));
     });
 }
 
@@ -508,6 +550,15 @@ int lbk_elementwise(lbk_ctx* c, int op, double* out, const double* a, const doub
 }
 
 // ---- vector-free mode -------------------------------------------------------------------
+// the persistent iteration's segments per workgroup (1..16, dividing a group's 1024) for this n,
+// or 0 when it is off or the grid would not be resident
+static int persist_fits(const lbk_ctx* c) {
+    if (!c->persist_on || c->geo.world != 1 || c->comm || !c->direct || c->geo.nseg <= c->coop_max) return 0;
+    for (int spw = 1; spw <= 16; spw *= 2)
+        if ((c->geo.nseg + spw - 1) / spw <= c->persist_gmax) return spw;
+    return 0;
+}
+
 int lbk_small_iter(lbk_ctx* c, int obj, int h, const double* g, double* q, double* r, const double* const* S,
                    const double* const* Y, const double* rho, double gamma, int p0_ref, double a0, const double* x,
                    double* xn, double* gn, double* so, double* yo, int slot_p0, int slot_a0, int slot_b0,
@@ -551,7 +602,8 @@ int lbk_small_iter(lbk_ctx* c, int obj, int h, const double* g, double* q, doubl
     // algorithmic bytes: the multi-launch sequence's passes (P0 dot if computed, 4 per pair
     // pass, 3 for mid, 8 for the commit)
     const double vec = (p0_ref >= 0 ? 0.0 : 2.0) + 4.0 * (h - 1) + 3.0 + 4.0 * (h - 1) + 8.0;
-    if (c->coop_max > 0 && c->geo.nseg <= c->coop_max) {
+    const int persist = persist_fits(c);
+    if ((c->coop_max > 0 && c->geo.nseg <= c->coop_max) || persist) {
         // passes of this launch (sequence numbers it tags): [P0] + (h-1) first-loop + mid + (h-1)
         // second-loop + commit
         const int passes = (p0_ref >= 0 ? 0 : 1) + 2 * h;
@@ -586,6 +638,20 @@ int lbk_small_iter(lbk_ctx* c, int obj, int h, const double* g, double* q, doubl
         }
         c->coop_base += (unsigned long long)passes;
         geo.rev = 0;
+        if (persist) {
+            a.spw = persist;
+            a.partials = c->partials;
+            a.pcnt = c->persist_cnt;
+            a.gflag = c->persist_gflag;
+            const int nb = (int)((c->geo.nseg + persist - 1) / persist);
+            return launch(c, LBK_K_SMALL_ITER, vec, -1, [&] {
+                NT_DISPATCH(c, switch (obj) {
+                    case LBK_OBJ_ROSENBROCK: hipLaunchKernelGGL((k_persist_iter<LBK_OBJ_ROSENBROCK, NT_>), dim3(nb), dim3(LB_BLOCK), 0, c->stream, a, geo); break;
+                    case LBK_OBJ_QUAD_TRIDIAG: hipLaunchKernelGGL((k_persist_iter<LBK_OBJ_QUAD_TRIDIAG, NT_>), dim3(nb), dim3(LB_BLOCK), 0, c->stream, a, geo); break;
+                    default: hipLaunchKernelGGL((k_persist_iter<LBK_OBJ_QUAD_SEPARABLE, NT_>), dim3(nb), dim3(LB_BLOCK), 0, c->stream, a, geo); break;
+                });
+            });
+        }
         const int nb = (int)c->geo.nseg;
         return launch(c, LBK_K_SMALL_ITER, vec, -1, [&] {
             switch (obj) {
@@ -704,6 +770,7 @@ int lbk_fetch_marked(lbk_ctx* c, int slot, int ncomp, double* totals) {
 int lbk_small_ok(const lbk_ctx* c, int h) {
     if (c->geo.world != 1 || c->comm || h < 1 || h > LBK_SMALL_HMAX) return 0;
     if (c->coop_max > 0 && c->geo.nseg <= c->coop_max) return 1;
+    if (persist_fits(c)) return 1;
     return c->small_seg_max > 0 && c->geo.nseg <= c->small_seg_max && c->geo.nseg <= LBK_SMALL_SEGMAX;
 }
 
@@ -751,6 +818,8 @@ int lbk_checksum(lbk_ctx* c, const double* x, uint64_t* c1, uint64_t* c2) {
     }
     if (c->geo.world > 1 && !c->grp && c->xg_on) {
         // integer sums: gather every rank's pair through the peer mailboxes, add on the host
+        const int frc = flush_fold(c);  // epochs in order
+        if (frc) return frc;
         uint64_t w[LBK_GROUPS * 2];
         HIPCHK(c, hipMemsetAsync(c->d_ckslot, 0, sizeof w, c->stream));
         HIPCHK(c, hipMemcpyAsync(c->d_ckslot + 2 * c->geo.g_lo, c->d_ck, 2 * sizeof(uint64_t), hipMemcpyDeviceToDevice,
@@ -870,7 +939,13 @@ int lbk_peer_connect(lbk_ctx* c, const void* handles) {
 int lbk_peer_enable(lbk_ctx* c, int on) {
     if (on && !lbk_xgmi_connected(c->xg)) return -5;
     if (!on && !c->comm && !c->grp) return -5;  // nothing else to exchange through
+    if (!on) {  // a folded exchange in flight is collected through the mailboxes first
+        const int rc = flush_fold(c);
+        if (rc) return rc;
+    }
     c->xg_on = on ? 1 : 0;
+    c->xf_on = 0;
+    if (on && c->fold_env && c->geo.world > 1 && !c->grp && lbk_xgmi_fold_info(c->xg, &c->xf) == 0) c->xf_on = 1;
     return 0;
 }
 
@@ -879,6 +954,10 @@ int lbk_exchange_bench(lbk_ctx* c, int backend, int ks, int iters, double* us) {
     if (backend == 2 && !lbk_xgmi_connected(c->xg)) return -5;
     if (backend == 1 && !c->comm) return -5;
     if (backend != 1 && backend != 2) return -1;
+    {
+        const int rc = flush_fold(c);
+        if (rc) return rc;
+    }
     const int saved = c->xg_on;
     c->xg_on = backend == 2;
     double* buf = nullptr;

@@ -63,6 +63,38 @@ struct Geo {
     double* edge_slot;  // sharded: where d[0] / d[n_loc-1] of this rank are published
 };
 
+// Folded exchange, consumer side (sharded over the xGMI mailboxes): the other
+// ranks' group values of this launch's first source arrive in this rank's mailbox (parity of
+// mepoch applied), pushed there by the producing pass itself; src_total polls them. A separate
+// kernel argument of the fold-capable passes, so the other kernels' Geo stays as it was.
+struct FoldSrc {
+    const unsigned long long* mbx;  // nullptr: the source is an ordinary slot
+    unsigned mepoch;
+    unsigned* merr;
+    unsigned long long mtmo;
+};
+
+// Folded exchange, producer side: where a pass pushes its group values (stage 2's last arriver,
+// or k_group_reduce) and its rank-edge values (publish_edges) - every peer's mailbox at `epoch`,
+// in the exchange kernel's wire format (lbfgs_xgmi.h). peers == nullptr: no push.
+struct FoldPush {
+    unsigned long long* const* peers;
+    int positions, world, rank;
+    unsigned epoch;
+};
+
+__device__ __forceinline__ void fold_push(const FoldPush& fp, int pos, double v) {
+    const size_t par = (size_t)(fp.epoch & 1u) * (size_t)fp.positions * 2;
+    const unsigned long long tag = (unsigned long long)fp.epoch << 32;
+    const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+    for (int p = 0; p < fp.world; ++p) {
+        if (p == fp.rank) continue;
+        unsigned long long* dst = fp.peers[p] + par + 2 * (size_t)pos;
+        __hip_atomic_store(dst, tag | (u & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(dst + 1, tag | (u >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
 struct Red {
     double* partials;  // [LBK_KW][LBK_SEGS], local segment index
     unsigned* cnt;     // [LBK_GROUPS] tickets
@@ -74,6 +106,7 @@ struct Red {
     // after the slot's mirror, so the host waits on it instead of synchronising the stream
     unsigned long long* done;
     unsigned long long epoch;
+    FoldPush fp;  // folded exchange: the last arriver pushes the group value (K == 1)
 };
 
 // Streaming loads/stores; NT = non-temporal (the vectors are touched once per pass and, at
@@ -155,7 +188,7 @@ __device__ __forceinline__ double bitsd(unsigned long long u) {
 // store is single-copy atomic, so a reader that sees both tags has both halves: no separate
 // arrival counter, no drain between the data and the flag. Agent-scope (sc1) stores and loads,
 // coherent across the XCDs' L2s.
-#define LBK_LL_SEGS 512   // == LBK_COOP_SEGMAX
+#define LBK_LL_SEGS 8192  // >= LBK_COOP_SEGMAX; every segment for the persistent iteration (LBFGS_PERSIST)
 #define LBK_LL_COMPS 10   // up to 8 reduction components + the 2 edge values of an r pass
 __device__ __forceinline__ void ll_store(unsigned long long* p, double v, unsigned seq) {
     const unsigned long long u = dbits(v), tag = (unsigned long long)seq << 32;
@@ -309,7 +342,7 @@ __device__ __forceinline__ void group_tree(const double* partials, int64_t lbase
 //                ticket's vmcnt(0) has to wait for all the wave's outstanding row stores, which
 //                costs ~2x on short segments (n = 1e7: 3.0 vs 4.7+ TB/s, profiles/r01).
 // Both give the same bits.
-template <int K>
+template <int K, bool FOLD = false>
 __device__ __forceinline__ void reduce_publish(double (&acc)[K], const Geo& geo, const Red& red) {
     __shared__ double lds[4][K];
     __shared__ int last_flag;
@@ -352,6 +385,8 @@ __device__ __forceinline__ void reduce_publish(double (&acc)[K], const Geo& geo,
     const int64_t gseg0 = (int64_t)g * geo.spg;
     group_tree<K, true>(red.partials, gseg0 - geo.seg_lo, gseg0, geo.nseg, geo.spg, red.slot + g * red.kstride,
                         red.hslot ? red.hslot + g * red.kstride : nullptr, lds);
+    // folded exchange: thread 0 stored the group value (K == 1) itself; it goes to every peer now
+    if (FOLD && K == 1 && red.fp.peers && t == 0) fold_push(red.fp, g * red.kstride, red.slot[g * red.kstride]);
     if (t == 0) __hip_atomic_store(red.cnt + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (red.done) {  // every wave's mirror stores complete before the word
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
@@ -363,12 +398,14 @@ __device__ __forceinline__ void reduce_publish(double (&acc)[K], const Geo& geo,
 // Reduce-kernel mode: one workgroup per group of this rank (stage 2 after the boundary).
 template <int K>
 __global__ __launch_bounds__(LB_BLOCK) void k_group_reduce(const double* __restrict__ partials, Geo geo,
-                                                           double* __restrict__ slot, double* hslot, int kstride) {
+                                                           double* __restrict__ slot, double* hslot, int kstride,
+                                                           FoldPush fp) {
     __shared__ double lds[4][K];
     const int g = geo.g_lo + (int)blockIdx.x;
     const int64_t gseg0 = (int64_t)g * geo.spg;
     group_tree<K, false>(partials, gseg0 - geo.seg_lo, gseg0, geo.nseg, geo.spg, slot + g * kstride,
                          hslot ? hslot + g * kstride : nullptr, lds);
+    if (K == 1 && fp.peers && threadIdx.x == 0) fold_push(fp, g * kstride, slot[g * kstride]);
 }
 
 // The same stage 2 for a runtime number of components (wide slots): blockIdx.y takes
@@ -411,6 +448,45 @@ __global__ __launch_bounds__(LB_BLOCK) void k_group_reduce_wide(const double* __
 // the group trees from the producer's partials itself - the same trees, so the same bits - and
 // workgroup 0 stores the group values into the slot for later readers. One kernel boundary and
 // the stage-2 launch per pass disappear; the price is each workgroup reading <= 2048 partials.
+// Folded exchange, consumer side: the rank's own groups from the slot (its producer's stage 2,
+// before this launch's boundary), every other group's value from the mailbox once both words carry
+// the exchange's epoch (a wait past the timeout sets *merr and gives NaN, as the exchange kernel);
+// workgroup 0 completes the slot for later readers. Same eight values, same fixed-order sum.
+__device__ __forceinline__ double src_total_mailbox(const double* slot, const Geo& geo, const FoldSrc& fs) {
+    __shared__ double gv[LBK_GROUPS];
+    const int t = threadIdx.x;
+    if (t < LBK_GROUPS) {
+        double v;
+        if (t >= geo.g_lo && t < geo.g_hi) {
+            v = slot[t * LBK_KMAX];
+        } else {
+            const unsigned long long* p = fs.mbx + 2 * (size_t)(t * LBK_KMAX);
+            unsigned long long a, b;
+            const unsigned long long t0 = wall_clock64();
+            for (;;) {
+                a = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                b = __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                if ((unsigned)(a >> 32) == fs.mepoch && (unsigned)(b >> 32) == fs.mepoch) break;
+                if (wall_clock64() - t0 > fs.mtmo) {
+                    __hip_atomic_store(fs.merr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    a = 0;
+                    b = 0x7ff80000ull;  // quiet NaN
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            v = bitsd((a & 0xffffffffull) | ((b & 0xffffffffull) << 32));
+            if (blockIdx.x == 0) const_cast<double*>(slot)[t * LBK_KMAX] = v;
+        }
+        gv[t] = v;
+    }
+    __syncthreads();
+    double tt = gv[0];
+#pragma unroll
+    for (int g = 1; g < LBK_GROUPS; ++g) tt = tt + gv[g];
+    return tt;
+}
+
 __device__ __forceinline__ double src_total(const double* slot, const Geo& geo) {
     if (!geo.ppart) return slot_total(slot);
     __shared__ double gv[LBK_GROUPS];
@@ -868,14 +944,33 @@ struct OpNegDot {  // d = -g;  acc += g . d                          (:90, :151-
     }
 };
 
-template <class Op, int K>
+// Folded exchange of an r pass (sharded): the workgroup holding the rank's first or last element
+// pushes that edge value, which one of its waves stored into the slot during the stream, to the
+// peers once its waves are past the stream (a workgroup-scope hand-off on one CU).
+__device__ __forceinline__ void fold_push_edges(const Geo& geo, const Seg& s, const FoldPush& fp) {
+    const bool first = s.lb == 0, last = s.lb + s.len == geo.n_loc;
+    if (!first && !last) return;  // uniform over the workgroup
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    if (threadIdx.x == 0) {
+        const volatile double* e = geo.edge_slot;
+        if (first) fold_push(fp, geo.g_lo * LBK_KMAX + 1, e[geo.g_lo * LBK_KMAX + 1]);
+        if (last) fold_push(fp, (geo.g_hi - 1) * LBK_KMAX + 2, e[(geo.g_hi - 1) * LBK_KMAX + 2]);
+    }
+}
+
+// FOLD: a folded exchange's producer (sharded, the mailboxes; the kernels of every other run are
+// compiled without its code, which costs the pass kernels registers)
+template <class Op, int K, bool FOLD = false>
 __device__ __forceinline__ void run_pass(const Op& op, const Geo& geo, const Red& red) {
     const Seg s = seg_setup(geo);
     double acc[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) acc[k] = 0.0;
     stream(op, s, geo, acc);
-    reduce_publish<K>(acc, geo, red);
+    if (FOLD && red.fp.peers && geo.edge_slot) fold_push_edges(geo, s, red.fp);
+    reduce_publish<K, FOLD>(acc, geo, red);
 }
 
 template <class Op, int K>
@@ -888,39 +983,42 @@ __device__ __forceinline__ void run_pass_halo(const Op& op, const Geo& geo, cons
     reduce_publish<K>(acc, geo, red);
 }
 
-template <bool NT>
+template <bool NT, bool FOLD = false>
 __global__ __launch_bounds__(LB_BLOCK) void k_dot(const double* __restrict__ a, const double* __restrict__ b,
                                                   Geo geo, Red red) {
-    run_pass<OpDot<NT>, 1>(OpDot<NT>{a, b}, geo, red);
+    run_pass<OpDot<NT>, 1, FOLD>(OpDot<NT>{a, b}, geo, red);
 }
 
 // alpha = rho * total(prev)
-template <bool NT>
+// FOLD: sharded over the mailboxes, the source arrives folded (src_total polls) and the result is
+// pushed folded. A folded producer whose source came through a slot (or the reverse) does not
+// occur: the two-loop's passes fold as a chain.
+template <bool NT, bool FOLD = false>
 __global__ __launch_bounds__(LB_BLOCK) void k_axpy_dot(double* qout, const double* qin, const double* __restrict__ y,
                                                        const double* __restrict__ sv, double rho,
-                                                       const double* __restrict__ prev, Geo geo, Red red) {
-    const double alpha = rho * src_total(prev, geo);
-    run_pass<OpAxpyDot<NT>, 1>(OpAxpyDot<NT>{qout, qin, y, sv, alpha}, geo, red);
+                                                       const double* __restrict__ prev, Geo geo, Red red, FoldSrc fs) {
+    const double alpha = rho * ((FOLD && fs.mbx) ? src_total_mailbox(prev, geo, fs) : src_total(prev, geo));
+    run_pass<OpAxpyDot<NT>, 1, FOLD>(OpAxpyDot<NT>{qout, qin, y, sv, alpha}, geo, red);
 }
 
-template <bool NT>
+template <bool NT, bool FOLD = false>
 __global__ __launch_bounds__(LB_BLOCK) void k_mid(double* __restrict__ rout, const double* __restrict__ qin,
                                                   const double* __restrict__ y0, double rho0, double gamma,
-                                                  const double* __restrict__ prev, Geo geo, Red red) {
-    const double alpha = rho0 * src_total(prev, geo);
-    run_pass<OpMid<NT>, 1>(OpMid<NT>{rout, qin, y0, alpha, gamma, geo.edge_slot, geo.n_loc, geo.g_lo, geo.g_hi}, geo,
-                           red);
+                                                  const double* __restrict__ prev, Geo geo, Red red, FoldSrc fs) {
+    const double alpha = rho0 * ((FOLD && fs.mbx) ? src_total_mailbox(prev, geo, fs) : src_total(prev, geo));
+    run_pass<OpMid<NT>, 1, FOLD>(OpMid<NT>{rout, qin, y0, alpha, gamma, geo.edge_slot, geo.n_loc, geo.g_lo, geo.g_hi},
+                                 geo, red);
 }
 
 // beta = rho * total(pb), alpha = rho * total(pa)
-template <bool NT>
+template <bool NT, bool FOLD = false>
 __global__ __launch_bounds__(LB_BLOCK) void k_axpy2_dot(double* r, const double* rin, const double* __restrict__ sv,
                                                         const double* __restrict__ yn, double rho,
                                                         const double* __restrict__ pb, const double* __restrict__ pa,
-                                                        Geo geo, Red red) {
-    const double beta = rho * src_total(pb, geo);
+                                                        Geo geo, Red red, FoldSrc fs) {
+    const double beta = rho * ((FOLD && fs.mbx) ? src_total_mailbox(pb, geo, fs) : src_total(pb, geo));
     const double alpha = rho * slot_total(pa);
-    run_pass<OpAxpy2Dot<NT>, 1>(
+    run_pass<OpAxpy2Dot<NT>, 1, FOLD>(
         OpAxpy2Dot<NT>{r, rin, sv, yn, alpha - beta, geo.edge_slot, geo.n_loc, geo.g_lo, geo.g_hi}, geo, red);
 }
 
@@ -1034,7 +1132,7 @@ __device__ __forceinline__ double halo_z(const double* __restrict__ x, const Dir
 }
 
 // (x, d) at local element hi (-1 <= hi <= n_loc; zeros outside), d per DMODE: halo operands
-template <int DMODE>
+template <int DMODE, bool REDGE = false>
 __device__ __forceinline__ double2 xd_at(const double* __restrict__ x, const DirArgs& da, int64_t hi, int64_t n_loc) {
     if (hi < -1 || hi > n_loc) return make_double2(0.0, 0.0);
     double dh;
@@ -1042,7 +1140,15 @@ __device__ __forceinline__ double2 xd_at(const double* __restrict__ x, const Dir
         dh = ghost_d(da, hi, n_loc);
     else if (DMODE == LBK_D_TWOLOOP && da.ghost && (hi == -1 || hi == n_loc))
         dh = -(ghost_d(da, hi, n_loc) + da.s[hi] * da.coef);
-    else
+    else if (REDGE && DMODE == LBK_D_TWOLOOP && da.redge && hi >= 0 && hi < n_loc &&
+             (hi == (hi / da.L) * da.L || hi == (hi / da.L) * da.L + da.L - 1)) {
+        // persistent iteration (stencil walk): a segment edge's r, written in this launch by the
+        // workgroup that owns that segment - its published edge word (as halo_z)
+        const int64_t sg = hi / da.L;
+        const double rv = ll_load(da.redge + ((hi == sg * da.L ? 1 : 2) * LBK_LL_SEGS + sg) * 2, da.redge_seq,
+                                  da.err, da.tmo);
+        dh = -(rv + da.s[hi] * da.coef);
+    } else
         dh = load_dir1<DMODE>(da, hi);
     return make_double2(x[hi], dh);
 }
@@ -1153,7 +1259,9 @@ __global__ __launch_bounds__(LB_BLOCK) void k_objective(const double* __restrict
 //   [GD] g.d  [F] f  [SY] s.y  [YY] y.y  [GG] g_new.g_new  [SG] s.g_new  [DPHI] g_new.d
 // CAND: also f(x + cand d) at the line search's next backtracking step [FC] (no extra bytes:
 // x and d are in registers), so a rejected first step needs no trial pass for the second.
-template <int OBJ, int DMODE, bool NT, bool CAND = false>
+// REDGE: the persistent iteration's commit (k_persist_iter), whose stencil halos at segment edges
+// come from the published edge words
+template <int OBJ, int DMODE, bool NT, bool CAND = false, bool REDGE = false>
 struct OpCommit {
     static constexpr int K = CAND ? 8 : 7;
     const double* __restrict__ x;
@@ -1178,7 +1286,7 @@ struct OpCommit {
         r.z.x = r.x.x + alpha * r.d.x;
         r.z.y = r.x.y + alpha * r.d.y;
     }
-    __device__ double2 halo_mem(int64_t hi) const { return xd_at<DMODE>(x, da, hi, n_loc); }
+    __device__ double2 halo_mem(int64_t hi) const { return xd_at<DMODE, REDGE>(x, da, hi, n_loc); }
     __device__ double2 edge_first(const Row& r) const { return make_double2(r.x.x, r.d.x); }
     __device__ double2 edge_last(const Row& r) const { return make_double2(r.x.y, r.d.y); }
     __device__ void set_halo(Row& r, double2 xd) const {
@@ -1728,6 +1836,13 @@ struct SmallArgs {
     unsigned long long* vd;             // device verdict word of this launch ((epoch << 1) | went)
     const unsigned long long* chain;    // the previous speculative launch's verdict word, or nullptr
     unsigned long long chain_want;
+    // persistent form (k_persist_iter) only: segments per workgroup, the canonical stage 2's
+    // partials and per-group arrival counters (monotonic over passes), the group values as
+    // flagged words [pass parity][component][group][2]
+    int spw;
+    double* partials;
+    unsigned long long* pcnt;
+    unsigned long long* gflag;
 };
 
 __device__ __forceinline__ Seg seg_at(const Geo& geo, int64_t sidx, int tq) {
@@ -1870,7 +1985,7 @@ __global__ __launch_bounds__(LBK_SMALL_THREADS) void k_small_iter(SmallArgs a, G
 // A barrier that waits past its timeout sets *err (pinned host memory) instead of hanging.
 // ---------------------------------------------------------------------------------------
 #define LBK_COOP_SEGMAX 512  // one group; resident at 2 workgroups per CU
-static_assert(LBK_COOP_SEGMAX == LBK_LL_SEGS, "flagged partials cover every cooperative segment");
+static_assert(LBK_COOP_SEGMAX <= LBK_LL_SEGS, "flagged partials cover every cooperative segment");
 
 // component k of a slot: group 0 holds the total's tree, groups 1..7 are empty (+0.0), written
 // explicitly so that every reader - the host's fixed-order sum of the mirror, slot_total() of a
@@ -2087,6 +2202,164 @@ __global__ __launch_bounds__(LB_BLOCK) void k_coop_iter(SmallArgs a, Geo geo) {
 }
 #undef SL
 
+// ---------------------------------------------------------------------------------------
+// Persistent iteration for large n (LBFGS_PERSIST=1; VERDICT r02 item 8, SURVEY §7 step 5 at
+// configs[2]'s size): the cooperative iteration above with one resident grid of G workgroups
+// instead of one workgroup per segment. Workgroup b walks the contiguous canonical segments
+// [b spw, (b+1) spw) of every pass (spw | 1024, so they lie in one group) exactly as the pass
+// kernels do, storing each segment partial write-through; then one agent-scope ticket per
+// workgroup on its group's counter (monotonic: the last arriver of pass seq sees
+// seq * workgroups-in-group), and the group's last arriver forms the canonical stage-2 tree
+// (group_tree, the same bits as k_group_reduce) and publishes the group values as flagged words.
+// Every workgroup then waits for the 8 group words of each component and forms the fixed-order
+// total. One launch per iteration: the pass boundaries and stage-2 launches of the launch
+// sequence become one ticket round trip plus one flagged hop per pass.
+// ---------------------------------------------------------------------------------------
+template <int K, bool HALO, class Op>
+__device__ __forceinline__ void persist_pass(const Op& op, const Geo& geo, const SmallArgs& a, int pass, double* slot,
+                                             double* hslot, const double* rvec, double (&tot)[K],
+                                             double (&lds)[4][8], double (&gv)[8][8], int& last_flag) {
+    static_assert(K + 2 <= LBK_LL_COMPS && K <= 8, "flagged components");
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int64_t s0 = (int64_t)blockIdx.x * a.spw, s1 = min(s0 + a.spw, geo.nseg);
+    const unsigned seq = a.seq_base + (unsigned)pass + 1u;
+    unsigned long long* P = a.ll + (size_t)(pass & 1) * LBK_LL_COMPS * LBK_LL_SEGS * 2;
+    for (int64_t sidx = s0; sidx < s1; ++sidx) {
+        const Seg s = seg_at(geo, sidx, t);
+        double acc[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) acc[k] = 0.0;
+        if constexpr (HALO)
+            stream_halo(op, s, geo, acc);
+        else
+            stream(op, s, geo, acc);
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const double v = wave_sum(acc[k]);
+            if (lane == 0) lds[w][k] = v;
+        }
+        // this segment's vector stores are read by other waves of the workgroup (its edge r below,
+        // the next pass)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __syncthreads();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        if (t == 0) {
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+                __hip_atomic_store(reinterpret_cast<unsigned long long*>(a.partials + (int64_t)k * LBK_SEGS + sidx),
+                                   dbits((lds[0][k] + lds[1][k]) + (lds[2][k] + lds[3][k])), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            if (rvec) {  // the segment's first / last r for the commit's halo across segments
+                ll_store(P + ((int64_t)K * LBK_LL_SEGS + sidx) * 2, rvec[s.lb], seq);
+                ll_store(P + ((int64_t)(K + 1) * LBK_LL_SEGS + sidx) * 2, rvec[s.lb + s.len - 1], seq);
+            }
+        }
+        __syncthreads();  // lds reuse
+    }
+    const int g = (int)(s0 / LBK_SEG_PER_GROUP);
+    if (t == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int64_t gend = min(geo.nseg, (int64_t)(g + 1) * LBK_SEG_PER_GROUP);
+        const unsigned long long nwg = (unsigned long long)((gend - (int64_t)g * LBK_SEG_PER_GROUP + a.spw - 1) / a.spw);
+        const unsigned long long old =
+            __hip_atomic_fetch_add(a.pcnt + g, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last_flag = (old + 1ull == (unsigned long long)seq * nwg);
+    }
+    __syncthreads();
+    if (last_flag) {  // stage 2 of group g, then its values as flagged words
+        __shared__ double glds[4][K];
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        double* sg = slot + g * LBK_KMAX;
+        group_tree<K, true>(a.partials, (int64_t)g * LBK_SEG_PER_GROUP, (int64_t)g * LBK_SEG_PER_GROUP, geo.nseg,
+                            LBK_SEG_PER_GROUP, sg, hslot ? hslot + g * LBK_KMAX : nullptr, glds);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __syncthreads();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        if (t < K) ll_store(a.gflag + ((size_t)((pass & 1) * 8 + t) * 8 + g) * 2, sg[t], seq);
+    }
+    // every workgroup: the group values (groups without segments are the slot's 0.0), then the
+    // fixed-order total of slot_total()
+    const int ng = (int)((geo.nseg + LBK_SEG_PER_GROUP - 1) / LBK_SEG_PER_GROUP);
+    if (t < K * 8) {
+        const int k = t >> 3, gg = t & 7;
+        gv[k][gg] = gg < ng ? ll_load(a.gflag + ((size_t)((pass & 1) * 8 + k) * 8 + gg) * 2, seq, a.err, a.timeout)
+                            : 0.0;
+    }
+    __syncthreads();
+    if (t < K) {
+        double tt = gv[t][0];
+#pragma unroll
+        for (int q = 1; q < LBK_GROUPS; ++q) tt = tt + gv[t][q];
+        if (blockIdx.x == 0) {
+#pragma unroll
+            for (int q = 0; q < LBK_GROUPS; ++q) {
+                slot[q * LBK_KMAX + t] = gv[t][q];
+                if (hslot) hslot[q * LBK_KMAX + t] = gv[t][q];
+            }
+        }
+        lds[0][t] = tt;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < K; ++k) tot[k] = lds[0][k];
+    __syncthreads();  // lds / gv reuse by the next pass
+}
+
+#define SL(sl) (a.slots + (int64_t)(sl) * LBK_SLOT)
+template <int OBJ, bool NT>
+__global__ __launch_bounds__(LB_BLOCK) void k_persist_iter(SmallArgs a, Geo geo) {
+    __shared__ double lds[4][8];
+    __shared__ double gv[8][8];
+    __shared__ double TA[LBK_SMALL_HMAX], TB[LBK_SMALL_HMAX];
+    __shared__ int last_flag;
+    const int h = a.h;
+    int pass = 0;
+    double t1[1];
+    const double rho_top = a.rho[h - 1], gamma = a.gamma;
+    if (a.p0_from_slot)
+        t1[0] = slot_total(a.p0_slot);
+    else
+        persist_pass<1, false>(OpDot<NT>{a.S[h - 1], a.g}, geo, a, pass++, SL(a.slot_p0), nullptr, nullptr, t1, lds,
+                               gv, last_flag);
+    if (threadIdx.x == 0) TA[h - 1] = t1[0];
+    double alpha = rho_top * t1[0];
+    const double* qsrc = a.g;
+    for (int i = h - 2; i >= 0; --i) {  // q = q - alpha_{i+1} y_{i+1};  s_i . q
+        persist_pass<1, false>(OpAxpyDot<NT>{a.q, qsrc, a.Y[i + 1], a.S[i], alpha}, geo, a, pass++, SL(a.slot_a0 + i),
+                               nullptr, nullptr, t1, lds, gv, last_flag);
+        if (threadIdx.x == 0) TA[i] = t1[0];
+        alpha = a.rho[i] * t1[0];
+        qsrc = a.q;
+    }
+    persist_pass<1, false>(OpMid<NT>{a.r, qsrc, a.Y[0], alpha, gamma}, geo, a, pass++, SL(a.slot_b0), nullptr,
+                           h == 1 ? a.r : nullptr, t1, lds, gv, last_flag);
+    if (threadIdx.x == 0) TB[0] = t1[0];
+    __syncthreads();
+    for (int i = 0; i + 1 < h; ++i) {  // r += s_i (alpha_i - beta_i);  y_{i+1} . r
+        const double beta = a.rho[i] * TB[i];
+        const double alph = a.rho[i] * TA[i];
+        persist_pass<1, false>(OpAxpy2Dot<NT>{a.r, a.r, a.S[i], a.Y[i + 1], alph - beta}, geo, a, pass++,
+                               SL(a.slot_b0 + i + 1), nullptr, i + 2 == h ? a.r : nullptr, t1, lds, gv, last_flag);
+        if (threadIdx.x == 0) TB[i + 1] = t1[0];
+        __syncthreads();
+    }
+    const int rp = pass - 1;
+    DirArgs da = {a.r, a.S[h - 1], a.g, 0.0, nullptr, nullptr, rho_top, nullptr, geo.g_lo, geo.g_hi,
+                  a.ll + (size_t)(rp & 1) * LBK_LL_COMPS * LBK_LL_SEGS * 2, geo.L, a.seq_base + (unsigned)rp + 1u, a.err,
+                  a.timeout};
+    {
+        const double beta = rho_top * TB[h - 1];
+        const double alph = rho_top * TA[h - 1];
+        da.coef = alph - beta;
+    }
+    double t8[8];
+    persist_pass<8, true>(OpCommit<OBJ, LBK_D_TWOLOOP, NT, true, true>{a.x, da, a.a0, a.xn, a.gn, a.so, a.yo, geo.n,
+                                                                       geo.n_loc, a.cand},
+                          geo, a, pass++, SL(a.slot_c), HS(a.slot_c), nullptr, t8, lds, gv, last_flag);
+    coop_publish(a, 1, rho_top, gamma);
+}
+#undef SL
+
 // z = x + alpha d over the whole local range incl. ghosts (host-callback objectives)
 __global__ void k_point(double* __restrict__ z, const double* __restrict__ x, const double* __restrict__ d,
                         double alpha, int64_t lo, int64_t hi) {
@@ -2258,6 +2531,11 @@ struct lbk_ctx {
     int pend_taken;       // the launch in progress consumes it
     // cooperative small-n iteration (k_coop_iter): nseg <= coop_max (0: off)
     int coop_max;
+    // persistent iteration for large n (LBFGS_PERSIST=1, opt-in A/B): resident workgroups, their
+    // segments per pass, stage-2 counters and flagged group values
+    int persist_on, persist_gmax;
+    unsigned long long *persist_cnt, *persist_gflag;
+    unsigned long long coop_ll_bytes;
     unsigned long long* coop_ll;   // flagged partials (SmallArgs::ll)
     unsigned long long coop_base;  // passes tagged so far (the next launch's sequence base)
     unsigned* coop_err_h;          // pinned: barrier timeout
@@ -2279,6 +2557,18 @@ struct lbk_ctx {
     unsigned long long s2_epoch;
     unsigned long long slot_s2[LBK_NSLOTS + LBK_NWSLOTS];
     double *dq_A, *dq_b, *dq_t;  // dense quadratic objective (lbk_dense_set): A (n x n), b, terms
+    // folded exchanges (sharded over the mailboxes; LBFGS_XGMI_FOLD=0: off): the two-loop's
+    // single-component reductions travel from the producing pass straight into the consuming pass
+    int fold_env;          // LBFGS_XGMI_FOLD (default 1)
+    int xf_on;             // peers connected and enabled, fold on
+    lbk_xgmi_fold xf;
+    int xf_slot;           // slot of the last folded exchange not yet consumed (-1: none)
+    unsigned xf_epoch;
+    int xf_edges;          // ... whose producer also pushed its rank edges
+    int xf_taken;          // the launch in progress consumes it (src_total polls the mailbox)
+    int fold_now;          // the launch in progress pushes its reduction (epoch fold_epoch)
+    unsigned fold_epoch;
+    int fold_edges;
 };
 
 namespace {
@@ -2376,6 +2666,7 @@ Red kred(lbk_ctx* c, int slot, int K = 1) {
     r.ticket = c->ticket;
     r.done = nullptr;
     r.epoch = 0;
+    r.fp = FoldPush{nullptr, 0, 0, 0, 0u};
     const int si = slot < LBK_NSLOTS ? slot : LBK_NSLOTS + slot - LBK_WSLOT0;
     c->slot_s2[si] = 0;
     if (r.ticket && r.hslot && c->geo.world == 1 && !c->comm && !c->grp && c->sp_dh) {
@@ -2426,8 +2717,13 @@ int prof_flush(lbk_ctx* c) {
 // Sharded runs: each rank owns groups [g_lo, g_hi) of every result slot; gather them so
 // every rank holds all 8 (one RCCL all-gather of (8/world) x KMAX doubles per reduction, in
 // place, on the solver stream), or through the host group for emulated ranks.
+int flush_fold(lbk_ctx* c);
 int exchange_buf(lbk_ctx* c, double* base, int ks, double* host_mirror = nullptr) {
     const int per = (c->geo.g_hi - c->geo.g_lo) * ks;
+    if (c->xg_on) {  // a folded exchange's epoch is collected before the next one is issued
+        const int rc = flush_fold(c);
+        if (rc) return rc;
+    }
     if (c->grp) {
         lbk_group* G = c->grp;
         HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -2492,15 +2788,69 @@ int exchange_timed(lbk_ctx* c, int slot, int K = 1, bool host_read = true) {
 // deferred producer and its consumer alternate between the two.
 double* defer_part(const lbk_ctx* c, int region) { return c->partials + (int64_t)(LBK_KW - 2 + region) * LBK_SEGS; }
 
-// a pending (deferred) stage 2 that no consumer took: run it as the reduce kernel now
+// A folded exchange that no pass consumed (the next launch is not its consumer, or the host reads
+// the slot): wait for the peers' pushes with the collect kernel (timed as an exchange). Every new
+// exchange epoch is issued behind this in stream order, so a rank never pushes epoch e + 1 before
+// it holds every peer's e (the mailbox parity rule).
+int flush_fold(lbk_ctx* c) {
+    if (c->xf_slot < 0 || c->xf_taken) return 0;
+    hipEvent_t a = nullptr, b = nullptr;
+    if (c->prof_on) {
+        a = ev_get(c);
+        b = ev_get(c);
+        if (a) HIPCHK(c, hipEventRecord(a, c->stream));
+    }
+    const int rc = lbk_xgmi_collect(c->xg, c->stream, slot_base(c, c->xf_slot), slot_stride(c->xf_slot), c->geo.g_lo,
+                                    c->geo.g_hi, c->xf_epoch, c->xf_edges);
+    c->xf_slot = -1;
+    if (rc) {
+        snprintf(c->err, sizeof c->err, "xgmi collect launch failed");
+        return -3;
+    }
+    if (a && b) {
+        HIPCHK(c, hipEventRecord(b, c->stream));
+        c->pending.push_back({LBK_K_EXCHANGE, a, b, 0.0});
+    }
+    return 0;
+}
+
+// a pending (deferred) stage 2 that no consumer took: run it as the reduce kernel now; the same
+// for a folded exchange
 int flush_pending(lbk_ctx* c) {
+    {
+        const int rc = flush_fold(c);
+        if (rc) return rc;
+    }
     if (c->pend_slot < 0) return 0;
     const Geo g = kgeo(c);
     hipLaunchKernelGGL(k_group_reduce<1>, dim3(c->geo.g_hi - c->geo.g_lo), dim3(LB_BLOCK), 0, c->stream, c->pend_part,
-                       g, slot_base(c, c->pend_slot), (double*)nullptr, LBK_KMAX);
+                       g, slot_base(c, c->pend_slot), (double*)nullptr, LBK_KMAX, FoldPush{nullptr, 0, 0, 0, 0u});
     HIPCHK(c, hipGetLastError());
     c->pend_slot = -1;
     return 0;
+}
+
+// Folded exchange, producer: this launch's single-component reduction into `slot` (and, for an r
+// pass, the rank-edge values) is pushed to the peers from inside the pass; set up its Red.
+void fold_producer(lbk_ctx* c, Red& r, bool edges) {
+    if (!c->xf_on) return;
+    r.fp = FoldPush{c->xf.peers, c->xf.positions, c->xf.world, c->xf.rank, lbk_xgmi_next_epoch(c->xg)};
+    c->fold_now = 1;
+    c->fold_epoch = r.fp.epoch;
+    c->fold_edges = edges ? 1 : 0;
+}
+
+// Folded exchange, consumer: a launch whose first source (src_total) is the pending folded slot
+// polls the mailbox for it in its prologue
+FoldSrc take_fold(lbk_ctx* c, int ref) {
+    FoldSrc f{nullptr, 0u, nullptr, 0ull};
+    if (c->xf_slot < 0 || ref % LBK_KMAX != 0 || c->xf_slot != ref / LBK_KMAX) return f;
+    f.mbx = c->xf.own + (size_t)(c->xf_epoch & 1u) * (size_t)c->xf.positions * 2;
+    f.mepoch = c->xf_epoch;
+    f.merr = c->xf.err;
+    f.mtmo = c->xf.timeout;
+    c->xf_taken = 1;
+    return f;
 }
 
 // A single-component reduction into `slot` may leave its stage 2 to the next pass (returns the
@@ -2526,6 +2876,10 @@ const double* take_pending(lbk_ctx* c, int ref) {
 template <class F>
 int launch(lbk_ctx* c, int kind, double vec_passes, int slot, F&& fn, int K = 1, bool exchange = true,
            const Geo* gv = nullptr) {
+    if (c->xf_slot >= 0 && !c->xf_taken) {
+        const int rc = flush_fold(c);
+        if (rc) return rc;
+    }
     if (c->pend_slot >= 0 && !c->pend_taken) {
         const int rc = flush_pending(c);
         if (rc) return rc;
@@ -2560,6 +2914,13 @@ int launch(lbk_ctx* c, int kind, double vec_passes, int slot, F&& fn, int K = 1,
         c->pend_slot = -1;
         c->pend_taken = 0;
     }
+    if (c->xf_taken) {  // ... and the folded slot's other groups, from the mailbox
+        c->xf_slot = -1;
+        c->xf_taken = 0;
+    }
+    FoldPush fp{nullptr, 0, 0, 0, 0u};
+    if (c->fold_now && !c->ticket)  // the reduce kernel's workgroups push the group values
+        fp = FoldPush{c->xf.peers, c->xf.positions, c->xf.world, c->xf.rank, c->fold_epoch};
     if (c->defer_now) {
         c->pend_slot = slot;
         c->pend_part = defer_part(c, c->defer_region);
@@ -2572,10 +2933,10 @@ int launch(lbk_ctx* c, int kind, double vec_passes, int slot, F&& fn, int K = 1,
         const int ks = slot_stride(slot);
         const dim3 grid(c->geo.g_hi - c->geo.g_lo), blk(LB_BLOCK);
         switch (K) {
-            case 1: hipLaunchKernelGGL(k_group_reduce<1>, grid, blk, 0, c->stream, c->partials, g, sl, hs, ks); break;
-            case 2: hipLaunchKernelGGL(k_group_reduce<2>, grid, blk, 0, c->stream, c->partials, g, sl, hs, ks); break;
-            case 7: hipLaunchKernelGGL(k_group_reduce<7>, grid, blk, 0, c->stream, c->partials, g, sl, hs, ks); break;
-            case 8: hipLaunchKernelGGL(k_group_reduce<8>, grid, blk, 0, c->stream, c->partials, g, sl, hs, ks); break;
+            case 1: hipLaunchKernelGGL(k_group_reduce<1>, grid, blk, 0, c->stream, c->partials, g, sl, hs, ks, fp); break;
+            case 2: hipLaunchKernelGGL(k_group_reduce<2>, grid, blk, 0, c->stream, c->partials, g, sl, hs, ks, fp); break;
+            case 7: hipLaunchKernelGGL(k_group_reduce<7>, grid, blk, 0, c->stream, c->partials, g, sl, hs, ks, fp); break;
+            case 8: hipLaunchKernelGGL(k_group_reduce<8>, grid, blk, 0, c->stream, c->partials, g, sl, hs, ks, fp); break;
             default:
                 hipLaunchKernelGGL(k_group_reduce_wide, dim3(c->geo.g_hi - c->geo.g_lo, (K + 7) / 8), blk, 0, c->stream,
                                    c->partials, g, sl, hs, K, ks);
@@ -2586,6 +2947,14 @@ int launch(lbk_ctx* c, int kind, double vec_passes, int slot, F&& fn, int K = 1,
     if (c->prof_on && a && b) {
         HIPCHK(c, hipEventRecord(b, c->stream));
         c->pending.push_back({kind, a, b, 0.0});
+    }
+    if (c->fold_now) {  // pushed by the pass (or its reduce kernel): no exchange launch
+        c->xf_slot = slot;
+        c->xf_epoch = c->fold_epoch;
+        c->xf_edges = c->fold_edges;
+        c->xf_taken = 0;
+        c->fold_now = 0;
+        return 0;
     }
     if (exchange && (c->geo.world > 1 || c->comm) && slot >= 0) return exchange_timed(c, slot, K);
     return 0;

@@ -43,4 +43,25 @@ int lbk_xgmi_exchange_u64(lbk_xgmi* x, hipStream_t stream, uint64_t* slot, int k
 // nonzero once an exchange timed out waiting for a peer (the slot then holds NaN)
 int lbk_xgmi_failed(const lbk_xgmi* x);
 
+// ---- the exchange folded into the passes ----------------------------------------
+// A pass kernel pushes its own group values (and a rank-edge value) into the peers' mailboxes
+// itself, in the wire format above, and the consuming pass's prologue polls its own mailbox: no
+// exchange kernel and no extra kernel boundary between the two passes. What the kernels need:
+struct lbk_xgmi_fold {
+    unsigned long long* const* peers;  // device array [world]: every rank's mailbox as mapped here
+    const unsigned long long* own;     // this rank's mailbox
+    unsigned* err;                     // pinned: set by a poll that timed out
+    unsigned long long timeout;        // wall-clock ticks
+    int positions;                     // doubles per parity (the mailbox's [2][positions][2] layout)
+    int rank, world;
+};
+int lbk_xgmi_fold_info(const lbk_xgmi* x, lbk_xgmi_fold* out);  // -5 before a successful connect
+// the epoch of the next exchange (the counter the exchange kernel advances, shared)
+unsigned lbk_xgmi_next_epoch(lbk_xgmi* x);
+// the fallback when no pass consumes a folded exchange: wait for the peers' pushes of `epoch`
+// (component 0 of every other rank's groups, and with `edges` their rank-edge components 1 / 2)
+// and write them into the slot
+int lbk_xgmi_collect(lbk_xgmi* x, hipStream_t stream, double* slot, int ks, int g_lo, int g_hi, unsigned epoch,
+                     int edges);
+
 #endif

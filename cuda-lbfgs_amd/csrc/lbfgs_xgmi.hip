@@ -34,6 +34,7 @@ struct lbk_xgmi {
     double wall_khz;
     int connected;
     std::vector<unsigned long long*> opened;  // peer mappings to close
+    unsigned long long** peers_dev;           // device copy of peers.mb (folded exchanges)
 };
 
 namespace {
@@ -85,6 +86,38 @@ __global__ __launch_bounds__(256) void k_xgmi_exchange(unsigned long long* __res
     }
 }
 
+// Folded exchanges (lbk_xgmi_fold): wait for the positions the peers' passes pushed for `epoch`
+// (component 0 of every group of the other ranks; with `edges`, the rank-edge components 1 of each
+// rank's first group and 2 of its last) and write them into the slot.
+__global__ __launch_bounds__(64) void k_xgmi_collect(unsigned long long* __restrict__ slot, int ks, int g_lo,
+                                                     int g_hi, const unsigned long long* mine, int world,
+                                                     unsigned epoch, int edges, unsigned* err,
+                                                     unsigned long long timeout) {
+    const int per = XG_GROUPS / world;
+    const int j = threadIdx.x;  // 0..7 group values, 8..15 first-group edges, 16..23 last-group edges
+    if (j >= 3 * XG_GROUPS || (j >= XG_GROUPS && !edges)) return;
+    const int g = j % XG_GROUPS, kind = j / XG_GROUPS;
+    if (g >= g_lo && g < g_hi) return;
+    if (kind == 1 && g % per != 0) return;
+    if (kind == 2 && g % per != per - 1) return;
+    const int pos = g * ks + kind;
+    unsigned long long a, b;
+    const unsigned long long t0 = wall_clock64();
+    for (;;) {
+        a = __hip_atomic_load(mine + 2 * (size_t)pos, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        b = __hip_atomic_load(mine + 2 * (size_t)pos + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if ((unsigned)(a >> 32) == epoch && (unsigned)(b >> 32) == epoch) break;
+        if (wall_clock64() - t0 > timeout) {
+            __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            a = 0;
+            b = 0x7ff80000ull;
+            break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+    slot[pos] = (a & 0xffffffffull) | ((b & 0xffffffffull) << 32);
+}
+
 unsigned long long ticks(const lbk_xgmi* x, double seconds) {
     return (unsigned long long)(seconds * x->wall_khz * 1e3);
 }
@@ -92,8 +125,7 @@ unsigned long long ticks(const lbk_xgmi* x, double seconds) {
 int launch(lbk_xgmi* x, hipStream_t s, unsigned long long* slot, int ks, int g_lo, int g_hi,
            unsigned long long timeout, unsigned long long* hm = nullptr) {
     if (ks < 1 || XG_GROUPS * ks > x->positions || g_lo < 0 || g_hi > XG_GROUPS || g_lo >= g_hi) return -1;
-    ++x->epoch;
-    if (x->epoch == 0) ++x->epoch;  // 0 marks an empty mailbox word
+    lbk_xgmi_next_epoch(x);
     hipLaunchKernelGGL(k_xgmi_exchange, dim3(1), dim3(256), 0, s, slot, ks, g_lo, g_hi, x->peers, x->rank,
                        x->world, x->positions, x->epoch, x->err_d, timeout, hm);
     return hipGetLastError() == hipSuccess ? 0 : -2;
@@ -157,6 +189,7 @@ void lbk_xgmi_destroy(lbk_xgmi* x) {
     (void)hipSetDevice(x->device);
     (void)hipDeviceSynchronize();
     for (auto* p : x->opened) (void)hipIpcCloseMemHandle(p);
+    if (x->peers_dev) (void)hipFree(x->peers_dev);
     if (x->mb) (void)hipFree(x->mb);
     if (x->err_h) (void)hipHostFree(x->err_h);
     delete x;
@@ -229,8 +262,44 @@ int lbk_xgmi_connect(lbk_xgmi* x, const void* handles, hipStream_t stream, char*
         }
     }
     (void)hipFree(d);
+    if (rc == 0 && !x->peers_dev) {  // the mapped mailboxes for the passes that push themselves
+        hipError_t e = hipMalloc((void**)&x->peers_dev, sizeof(unsigned long long*) * XG_MAXW);
+        if (e == hipSuccess)
+            e = hipMemcpy(x->peers_dev, x->peers.mb, sizeof(unsigned long long*) * XG_MAXW, hipMemcpyHostToDevice);
+        if (e != hipSuccess) {
+            snprintf(err, cap, "xgmi: peer table: %s", hipGetErrorString(e));
+            rc = -2;
+        }
+    }
     if (rc == 0) x->connected = 1;
     return rc;
+}
+
+int lbk_xgmi_fold_info(const lbk_xgmi* x, lbk_xgmi_fold* out) {
+    if (!x || !x->connected || !x->peers_dev) return -5;
+    out->peers = x->peers_dev;
+    out->own = x->mb;
+    out->err = x->err_d;
+    out->timeout = x->timeout_ticks;
+    out->positions = x->positions;
+    out->rank = x->rank;
+    out->world = x->world;
+    return 0;
+}
+
+unsigned lbk_xgmi_next_epoch(lbk_xgmi* x) {
+    ++x->epoch;
+    if (x->epoch == 0) ++x->epoch;  // 0 marks an empty mailbox word
+    return x->epoch;
+}
+
+int lbk_xgmi_collect(lbk_xgmi* x, hipStream_t stream, double* slot, int ks, int g_lo, int g_hi, unsigned epoch,
+                     int edges) {
+    if (!x->connected) return -5;
+    const unsigned long long* mine = x->mb + (size_t)(epoch & 1u) * (size_t)x->positions * 2;
+    hipLaunchKernelGGL(k_xgmi_collect, dim3(1), dim3(64), 0, stream, reinterpret_cast<unsigned long long*>(slot), ks,
+                       g_lo, g_hi, mine, x->world, epoch, edges, x->err_d, x->timeout_ticks);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
 int lbk_xgmi_exchange(lbk_xgmi* x, hipStream_t stream, double* slot, int ks, int g_lo, int g_hi,

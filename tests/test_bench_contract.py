@@ -115,3 +115,12 @@ def test_reference_parity_live_and_fixture(bench):
     bad["tr_f"][2] = np.nextafter(bad["tr_f"][2], np.inf)
     p = bench.reference_parity(bad, live, fx, "fixture.json")
     assert not p["canonical"]["bit_exact"] and not p["ok"]
+    # past the reference's own horizon a divergence is reported, not failed; before it, it fails
+    far = dict(traj, tr_gnorm=traj["tr_gnorm"].copy())
+    far["tr_gnorm"][m + 2] *= 1.0 + 1e-8
+    fx2 = dict(fx, horizons={"ref": [m + 3, m + 2]})
+    fx2["canon"] = dict(fx["canon"], gnorm=hexes(np.concatenate([canon_short["gnorm"][:m + 2], far["tr_gnorm"][m + 2:m + 3]])))
+    p = bench.reference_parity(far, live, fx2, "fixture.json")
+    assert p["first_divergent_k"] == m + 2 and p["within_tolerance_iterations"]["gnorm"] == m + 2 and p["ok"]
+    p = bench.reference_parity(far, live, dict(fx2, horizons={"ref": [m + 3, m + 3]}), "fixture.json")
+    assert not p["ok"]

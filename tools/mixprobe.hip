@@ -1,0 +1,168 @@
+// tools/mixprobe.hip — the HBM ceiling of each read/write mix the solver's passes stream, measured
+// in the passes' OWN access pattern (is k_commit's 4R + 4W, k_vf_commit's
+// 22R + 4W or k_mid's 2R + 1W at the chip's ceiling for that mix, or is there headroom?).
+//
+// Geometry exactly as the product's pass kernels (lbfgs_kernels_impl.h stream()): one 256-thread
+// workgroup per canonical segment of L elements, wave w visits rows 4u + w of 128 elements, lane l
+// the two elements 2l, 2l + 1 (one 16-B load per vector), U rows of every vector loaded before the
+// first use, no masks (n a multiple of 128 here). Per element: the NR loaded values are summed, one
+// product goes into a dot accumulator (so no load is dead), and NW distinct values are stored.
+// Policies per operand class: non-temporal (nt) or default, for loads and stores separately; the
+// store order (all stores of a row together, or interleaved with the next row's loads) is a variant.
+//
+// Reports algorithmic GB/s = (NR + NW) * 8 * n / kernel time (HIP events, median of 15 reps, one
+// warm-up), n = 1e8 (configs[2]: 800 MB per vector, far beyond the 256 MiB Infinity Cache).
+// Build: hipcc --offload-arch=gfx950 -O3 -o tools/mixprobe tools/mixprobe.hip
+// Run:   tools/mixprobe [n]
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x)                                                                       \
+    do {                                                                            \
+        hipError_t e = (x);                                                         \
+        if (e != hipSuccess) {                                                      \
+            fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e)); \
+            exit(1);                                                                \
+        }                                                                           \
+    } while (0)
+
+#define MAXV 24
+struct Vecs {
+    const double* in[MAXV];
+    double* out[MAXV];
+};
+
+typedef double dvec2 __attribute__((ext_vector_type(2)));
+template <bool NT>
+__device__ __forceinline__ dvec2 ld(const double* p) {
+    if (NT) return __builtin_nontemporal_load(reinterpret_cast<const dvec2*>(p));
+    return *reinterpret_cast<const dvec2*>(p);
+}
+template <bool NT>
+__device__ __forceinline__ void st(double* p, dvec2 v) {
+    if (NT)
+        __builtin_nontemporal_store(v, reinterpret_cast<dvec2*>(p));
+    else
+        *reinterpret_cast<dvec2*>(p) = v;
+}
+
+// LNT / SNT: nt loads / stores; the first TWL inputs and the first TWS outputs (the "work"
+// vectors q / r / d of the product) keep the default policy; INPL: output 0 is input 0 (in place,
+// as the two-loop's q)
+template <int NR, int NW, int U, bool LNT, bool SNT, int TWL, int TWS, bool INPL>
+__global__ __launch_bounds__(256) void k_mix(Vecs v, int64_t n, int64_t L, double* sink) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t sbeg = (int64_t)blockIdx.x * L;
+    const int64_t len = min(L, n - sbeg);
+    const int nrows = (int)(len / 128);
+    const int myrows = nrows > w ? (nrows - w + 3) / 4 : 0;
+    double acc = 0.0;
+    for (int u0 = 0; u0 < myrows; u0 += U) {
+        dvec2 a[U][NR];
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            if (u0 + j >= myrows) break;
+            const int64_t off = sbeg + (int64_t)(4 * (u0 + j) + w) * 128 + 2 * lane;
+#pragma unroll
+            for (int k = 0; k < NR; ++k)
+                a[j][k] = (k < TWL) ? ld<false>(v.in[k] + off) : ld<LNT>(v.in[k] + off);
+        }
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            if (u0 + j >= myrows) break;
+            const int64_t off = sbeg + (int64_t)(4 * (u0 + j) + w) * 128 + 2 * lane;
+            dvec2 s = a[j][0];
+#pragma unroll
+            for (int k = 1; k < NR; ++k) s = s + a[j][k];
+            acc = fma(s.x, a[j][0].x, fma(s.y, a[j][0].y, acc));
+#pragma unroll
+            for (int k = 0; k < NW; ++k) {
+                const dvec2 o = s + (double)(k + 1);
+                double* dst = (INPL && k == 0) ? const_cast<double*>(v.in[0]) : v.out[k];
+                if (k < TWS)
+                    st<false>(dst + off, o);
+                else
+                    st<SNT>(dst + off, o);
+            }
+        }
+    }
+    if (acc == 1234.5678) sink[0] = acc;
+}
+
+struct Case {
+    const char* name;
+    int nr, nw;
+    void (*launch)(Vecs, int64_t, int64_t, int, double*);
+};
+
+template <int NR, int NW, int U, bool LNT, bool SNT, int TWL, int TWS, bool INPL>
+void launch(Vecs v, int64_t n, int64_t L, int nseg, double* sink) {
+    hipLaunchKernelGGL((k_mix<NR, NW, U, LNT, SNT, TWL, TWS, INPL>), dim3(nseg), dim3(256), 0, 0, v, n, L, sink);
+}
+
+int main(int argc, char** argv) {
+    const int64_t n = argc > 1 ? (int64_t)atof(argv[1]) : 100000000;
+    // the canonical segment length at this n: roundup(ceil(n / 8192), 128)
+    const int64_t L = std::max<int64_t>(512, ((n + 8191) / 8192 + 127) / 128 * 128);
+    const int nseg = (int)((n + L - 1) / L);
+    const int64_t npad = (int64_t)nseg * L;
+    std::vector<double*> bufs(MAXV + 4);
+    for (auto& b : bufs) {
+        CK(hipMalloc(&b, sizeof(double) * npad));
+        CK(hipMemset(b, 0, sizeof(double) * npad));
+    }
+    double* sink;
+    CK(hipMalloc(&sink, 64));
+    Vecs v;
+    for (int k = 0; k < MAXV; ++k) v.in[k] = bufs[k];
+    for (int k = 0; k < MAXV; ++k) v.out[k] = bufs[MAXV + 3 - (k % 4)];  // outputs disjoint from the inputs (NW <= 4)
+    // names: <R>r<W>w_u<U>_<load policy><store policy>  (nt / df = default); "work" operands as the
+    // product's kernels: k_mid q (df) + y -> r (df); k_axpy_dot q (df) + y + s -> q (df, in place);
+    // k_commit r (df) + x + s + g -> x' + g' + s + y; k_vf_commit 22 nt -> 4 nt
+    Case cases[] = {
+        {"1r0w_u4_nt", 1, 0, launch<1, 0, 4, true, true, 0, 0, false>},
+        {"1r1w_u4_ntnt", 1, 1, launch<1, 1, 4, true, true, 0, 0, false>},
+        {"mid_2r1w_u4", 2, 1, launch<2, 1, 4, true, true, 1, 1, false>},
+        {"mid_2r1w_u8", 2, 1, launch<2, 1, 8, true, true, 1, 1, false>},
+        {"axpy_3r1w_u4", 3, 1, launch<3, 1, 4, true, true, 1, 1, true>},
+        {"3r1w_u4_allnt", 3, 1, launch<3, 1, 4, true, true, 0, 0, false>},
+        {"commit_4r4w_u4", 4, 4, launch<4, 4, 4, true, true, 1, 0, false>},
+        {"commit_4r4w_u2", 4, 4, launch<4, 4, 2, true, true, 1, 0, false>},
+        {"commit_4r4w_u8", 4, 4, launch<4, 4, 8, true, true, 1, 0, false>},
+        {"4r4w_u4_ntld_dfst", 4, 4, launch<4, 4, 4, true, false, 1, 0, false>},
+        {"4r4w_u4_alldf", 4, 4, launch<4, 4, 4, false, false, 0, 0, false>},
+        {"4r2w_u4", 4, 2, launch<4, 2, 4, true, true, 1, 0, false>},
+        {"4r0w_u4", 4, 0, launch<4, 0, 4, true, true, 1, 0, false>},
+        {"vf_22r4w_u1", 22, 4, launch<22, 4, 1, true, true, 0, 0, false>},
+        {"vf_22r4w_u2", 22, 4, launch<22, 4, 2, true, true, 0, 0, false>},
+        {"22r4w_u1_ntld_dfst", 22, 4, launch<22, 4, 1, true, false, 0, 0, false>},
+        {"22r0w_u1", 22, 0, launch<22, 0, 1, true, true, 0, 0, false>},
+    };
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    printf("n=%lld L=%lld segments=%d (one 256-thread workgroup each)\n", (long long)n, (long long)L, nseg);
+    for (const Case& c : cases) {
+        std::vector<float> ms;
+        for (int r = 0; r < 16; ++r) {
+            CK(hipEventRecord(e0, 0));
+            c.launch(v, n, L, nseg, sink);
+            CK(hipEventRecord(e1, 0));
+            CK(hipEventSynchronize(e1));
+            float t;
+            CK(hipEventElapsedTime(&t, e0, e1));
+            if (r) ms.push_back(t);
+        }
+        std::sort(ms.begin(), ms.end());
+        const double med = ms[ms.size() / 2];
+        const double gbs = (double)(c.nr + c.nw) * 8.0 * (double)n / (med * 1e-3) / 1e9;
+        printf("%-22s %2dR %2dW  %9.1f us  %7.1f GB/s  (min %.1f us)\n", c.name, c.nr, c.nw, med * 1e3, gbs,
+               ms.front() * 1e3);
+    }
+    for (auto b : bufs) CK(hipFree(b));
+    return 0;
+}
