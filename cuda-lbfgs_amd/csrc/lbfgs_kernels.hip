@@ -2,7 +2,11 @@
 // results, exchange, profiling (kernels and helpers: lbfgs_kernels_impl.h).
 #include "lbfgs_kernels_impl.h"
 
+#include <thread>
+
 extern "C" {
+
+void xfer_pool_free(lbk_ctx* c);  // staged transfers' pinned pool (below)
 
 int lbk_device_count(void) {
     int n = 0;
@@ -217,6 +221,8 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
     }
     c->persist_on = 0;
     if (const char* e = getenv("LBFGS_PERSIST")) c->persist_on = atoi(e) != 0;
+    CK(hipMalloc(&c->fold_wait, sizeof(unsigned long long)));
+    CK(hipMemset(c->fold_wait, 0, sizeof(unsigned long long)));
     CK(hipMalloc(&c->persist_cnt, sizeof(unsigned long long) * LBK_GROUPS));
     CK(hipMemset(c->persist_cnt, 0, sizeof(unsigned long long) * LBK_GROUPS));
     CK(hipMalloc(&c->persist_gflag, sizeof(unsigned long long) * 2 * 8 * 8 * 2));
@@ -273,7 +279,9 @@ void lbk_destroy(lbk_ctx* c) {
     if (c->d_ckslot) (void)hipFree(c->d_ckslot);
     (void)hipFree(c->partials);
     (void)hipFree(c->coop_ll);
+    xfer_pool_free(c);
     (void)hipFree(c->persist_cnt);
+    (void)hipFree(c->fold_wait);
     (void)hipFree(c->persist_gflag);
     if (c->coop_err_h) (void)hipHostFree(c->coop_err_h);
     if (c->sp_h) (void)hipHostFree(c->sp_h);
@@ -320,15 +328,152 @@ void lbk_host_free(void* p) {
     if (p) (void)hipHostFree(p);
 }
 
+// ---- whole-vector copies between the caller's (pageable) memory and HBM: x0 in, x out ----------
+// (configs[3]'s time to solution pays both; parallel-implementation/L-BFGS.cu:176, 360-365 too).
+// LBFGS_XFER selects how a copy of >= 16 MB travels:
+//   pageable  one hipMemcpyAsync from / to the caller's buffer (the runtime stages it)
+//   register  the caller's pages pinned for the copy (hipHostRegister), one DMA, unpinned
+//   staged    LBFGS_XFER_THREADS host threads, each with its own stream and two pinned 8 MB
+//             buffers, copy their slice through them while the DMA engines move the previous chunk
+// (tools/xferprobe.hip measures the three on the box; the default is the measured best).
+namespace {
+constexpr size_t kXferMin = 16u << 20, kXferChunk = 8u << 20;
+
+struct XferPool {
+    int threads = 0;
+    std::vector<hipStream_t> st;
+    std::vector<char*> buf;        // 2 per thread
+    std::vector<hipEvent_t> ev;    // 2 per thread
+};
+XferPool* xfer_pool(lbk_ctx* c) {
+    if (c->xfer_pool) return static_cast<XferPool*>(c->xfer_pool);
+    XferPool* P = new (std::nothrow) XferPool();
+    if (!P) return nullptr;
+    int T = 8;
+    if (const char* e = getenv("LBFGS_XFER_THREADS")) T = std::max(1, std::min(32, atoi(e)));
+    P->threads = T;
+    P->st.resize(T);
+    P->buf.resize(2 * T);
+    P->ev.resize(2 * T);
+    bool ok = true;
+    for (int t = 0; t < T && ok; ++t) {
+        ok = hipStreamCreateWithFlags(&P->st[t], hipStreamNonBlocking) == hipSuccess;
+        for (int b = 0; b < 2 && ok; ++b) {
+            ok = hipHostMalloc((void**)&P->buf[2 * t + b], kXferChunk, hipHostMallocDefault) == hipSuccess &&
+                 hipEventCreateWithFlags(&P->ev[2 * t + b], hipEventDisableTiming) == hipSuccess;
+        }
+    }
+    c->xfer_pool = P;  // freed by xfer_pool_free (also a partial one)
+    return ok ? P : nullptr;
+}
+
+// one worker: its slice [off, off + len) of the copy, through its two pinned buffers
+int xfer_slice(lbk_ctx* c, XferPool* P, int t, char* dst, const char* src, size_t len, bool h2d) {
+    if (hipSetDevice(c->device) != hipSuccess) return -2;
+    hipStream_t s = P->st[t];
+    const size_t nch = (len + kXferChunk - 1) / kXferChunk;
+    if (h2d) {
+        for (size_t i = 0; i < nch; ++i) {
+            const int b = (int)(i & 1);
+            const size_t o = i * kXferChunk, l = std::min(kXferChunk, len - o);
+            if (i >= 2 && hipEventSynchronize(P->ev[2 * t + b]) != hipSuccess) return -2;  // the DMA that read it
+            memcpy(P->buf[2 * t + b], src + o, l);
+            if (hipMemcpyAsync(dst + o, P->buf[2 * t + b], l, hipMemcpyHostToDevice, s) != hipSuccess ||
+                hipEventRecord(P->ev[2 * t + b], s) != hipSuccess)
+                return -2;
+        }
+    } else {
+        auto issue = [&](size_t i) {
+            const int b = (int)(i & 1);
+            const size_t o = i * kXferChunk, l = std::min(kXferChunk, len - o);
+            return hipMemcpyAsync(P->buf[2 * t + b], src + o, l, hipMemcpyDeviceToHost, s) == hipSuccess &&
+                   hipEventRecord(P->ev[2 * t + b], s) == hipSuccess;
+        };
+        if (nch > 0 && !issue(0)) return -2;
+        for (size_t i = 0; i < nch; ++i) {
+            const int b = (int)(i & 1);
+            if (hipEventSynchronize(P->ev[2 * t + b]) != hipSuccess) return -2;
+            if (i + 1 < nch && !issue(i + 1)) return -2;  // the other buffer, freed one step ago
+            const size_t o = i * kXferChunk, l = std::min(kXferChunk, len - o);
+            memcpy(dst + o, P->buf[2 * t + b], l);
+        }
+    }
+    return hipStreamSynchronize(s) == hipSuccess ? 0 : -2;
+}
+
+int xfer_mode() {  // read per copy (two getenv calls per solve): tests and tools switch it in-process
+    int mode = 0;
+    if (const char* e = getenv("LBFGS_XFER")) {
+        if (!strcmp(e, "register")) mode = 1;
+        else if (!strcmp(e, "staged")) mode = 2;
+    }
+    return mode;
+}
+
+// dst / src: one device, one host pointer; bytes; h2d direction
+int xfer(lbk_ctx* c, void* dst, const void* src, size_t bytes, bool h2d) {
+    const int mode = bytes >= kXferMin ? xfer_mode() : 0;
+    if (mode == 1) {  // pin the caller's pages for this copy
+        void* host = h2d ? const_cast<void*>(src) : dst;
+        const uintptr_t a = (uintptr_t)host & ~(uintptr_t)4095;
+        const size_t len = (((uintptr_t)host + bytes + 4095) & ~(uintptr_t)4095) - a;
+        if (hipHostRegister((void*)a, len, hipHostRegisterDefault) == hipSuccess) {
+            hipError_t e = hipMemcpyAsync(dst, src, bytes, h2d ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost, c->stream);
+            if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+            (void)hipHostUnregister((void*)a);
+            HIPCHK(c, e);
+            return 0;
+        }
+        (void)hipGetLastError();  // not registrable (already pinned, ...): the pageable copy
+    } else if (mode == 2) {
+        XferPool* P = xfer_pool(c);
+        if (P) {
+            HIPCHK(c, hipStreamSynchronize(c->stream));  // the solver stream's work on the vector is done
+            const int T = P->threads;
+            const size_t per = ((bytes / T) + 4095) & ~(size_t)4095;
+            std::vector<std::thread> th;
+            std::vector<int> rc(T, 0);
+            for (int t = 0; t < T; ++t) {
+                const size_t o = std::min(bytes, per * t), l = std::min(bytes, per * (t + 1)) - o;
+                if (!l) continue;
+                th.emplace_back([=, &rc] {
+                    rc[t] = xfer_slice(c, P, t, (char*)dst + o, (const char*)src + o, l, h2d);
+                });
+            }
+            for (auto& x : th) x.join();
+            for (int t = 0; t < T; ++t)
+                if (rc[t]) {
+                    snprintf(c->err, sizeof c->err, "staged transfer failed (worker %d)", t);
+                    return -2;
+                }
+            return 0;
+        }
+    }
+    HIPCHK(c, hipMemcpyAsync(dst, src, bytes, h2d ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return 0;
+}
+}  // namespace
+
+void xfer_pool_free(lbk_ctx* c) {
+    XferPool* P = static_cast<XferPool*>(c->xfer_pool);
+    if (!P) return;
+    for (auto s : P->st)
+        if (s) (void)hipStreamDestroy(s);
+    for (auto b : P->buf)
+        if (b) (void)hipHostFree(b);
+    for (auto e : P->ev)
+        if (e) (void)hipEventDestroy(e);
+    delete P;
+    c->xfer_pool = nullptr;
+}
+
 int lbk_upload(lbk_ctx* c, double* dst, const double* host_global) {
     // local range plus the ghosts that exist globally
     const int64_t lo = c->geo.elem_lo > 0 ? c->geo.elem_lo - 1 : 0;
     const int64_t hi = std::min<int64_t>(c->geo.elem_lo + c->geo.n_loc + 1, c->geo.n);
     if (hi <= lo) return 0;
-    HIPCHK(c, hipMemcpyAsync(dst + (lo - c->geo.elem_lo), host_global + lo, sizeof(double) * (hi - lo),
-                             hipMemcpyHostToDevice, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    return 0;
+    return xfer(c, dst + (lo - c->geo.elem_lo), host_global + lo, sizeof(double) * (hi - lo), true);
 }
 
 int lbk_upload_local(lbk_ctx* c, double* dst, const double* host_local) {
@@ -370,9 +515,7 @@ int lbk_download(lbk_ctx* c, double* host_global, const double* src) {
 
 int lbk_download_local(lbk_ctx* c, double* host_local, const double* src) {
     if (c->geo.n_loc == 0) return 0;
-    HIPCHK(c, hipMemcpyAsync(host_local, src, sizeof(double) * c->geo.n_loc, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    return 0;
+    return xfer(c, host_local, src, sizeof(double) * c->geo.n_loc, false);
 }
 
 int lbk_copy(lbk_ctx* c, double* dst, const double* src) {
@@ -992,11 +1135,19 @@ int lbk_prof_get(lbk_ctx* c, int kind, double* ms, int64_t* launches, double* by
     *ms = c->prof_ms[kind];
     *launches = c->prof_n[kind];
     *bytes = c->prof_bytes[kind];
+    if (kind == LBK_K_EXCHANGE && c->fold_wait) {
+        // folded exchanges have no launch of their own: their wait, as the consuming pass's first
+        // workgroup measured it in its prologue, counts as exchange time
+        unsigned long long ticks = 0;
+        HIPCHK(c, hipMemcpy(&ticks, c->fold_wait, sizeof ticks, hipMemcpyDeviceToHost));
+        *ms += (double)ticks / c->wall_khz;
+    }
     return 0;
 }
 
 void lbk_prof_reset(lbk_ctx* c) {
     prof_flush(c);
+    if (c->fold_wait) (void)hipMemset(c->fold_wait, 0, sizeof(unsigned long long));
     for (int k = 0; k < LBK_K_COUNT; ++k) {
         c->prof_ms[k] = 0;
         c->prof_n[k] = 0;

@@ -72,6 +72,7 @@ struct FoldSrc {
     unsigned mepoch;
     unsigned* merr;
     unsigned long long mtmo;
+    unsigned long long* wait;  // profiling: workgroup 0 adds its prologue's wall-clock ticks here
 };
 
 // Folded exchange, producer side: where a pass pushes its group values (stage 2's last arriver,
@@ -455,6 +456,7 @@ __global__ __launch_bounds__(LB_BLOCK) void k_group_reduce_wide(const double* __
 __device__ __forceinline__ double src_total_mailbox(const double* slot, const Geo& geo, const FoldSrc& fs) {
     __shared__ double gv[LBK_GROUPS];
     const int t = threadIdx.x;
+    const unsigned long long w0 = (fs.wait && blockIdx.x == 0 && t == 0) ? wall_clock64() : 0ull;
     if (t < LBK_GROUPS) {
         double v;
         if (t >= geo.g_lo && t < geo.g_hi) {
@@ -481,6 +483,9 @@ __device__ __forceinline__ double src_total_mailbox(const double* slot, const Ge
         gv[t] = v;
     }
     __syncthreads();
+    // the time this launch's first workgroup spent waiting for the peers' values (exchange_share)
+    if (fs.wait && blockIdx.x == 0 && t == 0)
+        __hip_atomic_fetch_add(fs.wait, wall_clock64() - w0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     double tt = gv[0];
 #pragma unroll
     for (int g = 1; g < LBK_GROUPS; ++g) tt = tt + gv[g];
@@ -2566,6 +2571,8 @@ struct lbk_ctx {
     unsigned xf_epoch;
     int xf_edges;          // ... whose producer also pushed its rank edges
     int xf_taken;          // the launch in progress consumes it (src_total polls the mailbox)
+    unsigned long long* fold_wait;  // profiling: ticks the consumers' workgroup 0 waited (device)
+    void* xfer_pool;       // staged whole-vector transfers (LBFGS_XFER=staged), lazily
     int fold_now;          // the launch in progress pushes its reduction (epoch fold_epoch)
     unsigned fold_epoch;
     int fold_edges;
@@ -2843,12 +2850,13 @@ void fold_producer(lbk_ctx* c, Red& r, bool edges) {
 // Folded exchange, consumer: a launch whose first source (src_total) is the pending folded slot
 // polls the mailbox for it in its prologue
 FoldSrc take_fold(lbk_ctx* c, int ref) {
-    FoldSrc f{nullptr, 0u, nullptr, 0ull};
+    FoldSrc f{nullptr, 0u, nullptr, 0ull, nullptr};
     if (c->xf_slot < 0 || ref % LBK_KMAX != 0 || c->xf_slot != ref / LBK_KMAX) return f;
     f.mbx = c->xf.own + (size_t)(c->xf_epoch & 1u) * (size_t)c->xf.positions * 2;
     f.mepoch = c->xf_epoch;
     f.merr = c->xf.err;
     f.mtmo = c->xf.timeout;
+    f.wait = c->prof_on ? c->fold_wait : nullptr;
     c->xf_taken = 1;
     return f;
 }

@@ -15,6 +15,8 @@ import os
 import sys
 import time
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "cuda-lbfgs_amd"))
 import lbfgs_amd as L  # noqa: E402
@@ -60,10 +62,32 @@ def solve(n, m, batch, prof):
     return out
 
 
+def to_solution(n, m, mode, reps=3):
+    """lbfgs_minimize end to end (x0 upload from the caller's pageable buffer, the solve, x
+    download) with LBFGS_XFER=mode; median of reps, the context created beforehand"""
+    os.environ["LBFGS_BATCH"] = "1"
+    os.environ["LBFGS_XFER"] = mode
+    x0 = L.x0_uniform(n, 42, -2.0, 2.0)
+    times, r = [], None
+    with L.Context(n, m) as c:
+        for _ in range(reps + 1):
+            t0 = time.perf_counter()
+            r = c.minimize("quad_tridiag", x0, "wolfe", 1000, tolerance=1e-5)
+            times.append(time.perf_counter() - t0)
+    times = sorted(times[1:])
+    return dict(mode=mode, seconds=times[len(times) // 2], seconds_all=times, iterations=r["iterations"],
+                status=r["status"], f=r["f"], x_checksum=int(r["x"].view(np.uint64).sum(dtype=np.uint64)))
+
+
 def main():
     n = int(float(sys.argv[sys.argv.index("--n") + 1])) if "--n" in sys.argv else 10**8
     outp = sys.argv[1] if len(sys.argv) > 1 and not sys.argv[1].startswith("--") else None
     res = dict(config="configs[3]: quad_tridiag n=%d m=20 wolfe, tol 1e-5, x0 ~ U(-2,2) seed 42" % n)
+    # time to solution including the caller's transfers, per transfer mode (VERDICT r02 item 5)
+    res["with_transfers"] = [to_solution(n, 20, mode) for mode in ("pageable", "register", "staged")]
+    for row in res["with_transfers"]:
+        print("with_transfers", json.dumps(row), flush=True)
+    os.environ.pop("LBFGS_XFER", None)
     for batch in (1, 0):
         key = "batched" if batch else "one_pass_per_step"
         solve(n, 20, batch, False)  # warm-up (first-touch, code objects)
