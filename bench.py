@@ -265,7 +265,7 @@ def measure(a, D, n, x0, dev, rank, world, uid, unfused=False, vector_free=False
             if rank == 0:
                 print(f"exchange auto: xgmi {tx:.2f} us, rccl {tr:.2f} us -> {ctx.backend}", file=sys.stderr,
                       flush=True)
-    backend = ctx.backend
+    backend = ctx.backend + ("+fold" if world > 1 and ctx.backend == "xgmi" and ctx.folded else "")
     # the untimed history fill and warm-up record the trajectory (f, |g|, alpha, x checksums at
     # the top of every iteration) for reference_parity; the timed steps run untraced
     trace = not vector_free
@@ -318,7 +318,7 @@ def measure(a, D, n, x0, dev, rank, world, uid, unfused=False, vector_free=False
     lat = None
     if world > 1 and not vector_free and not unfused:
         lat = {}
-        backends = (["xgmi"] if backend == "xgmi" else []) + (["rccl"] if uid is not None else [])
+        backends = (["xgmi"] if backend.startswith("xgmi") else []) + (["rccl"] if uid is not None else [])
         for b in backends:
             for k in (8, 96):
                 lat[f"{b}_{k * 8}doubles"] = round(ctx.exchange_latency(b, k, 200), 2)
@@ -388,6 +388,7 @@ def config4(a, D, dev, rank, world):
     if not ok:
         ctx.close()
         return {"skipped": f"xGMI peer exchange unavailable ({msg})"}
+    folded = ctx.folded
     res, T, err, fill = None, None, None, None
     try:
         ctx.init(a.objective, x0, a.line_search, tolerance=1e-5)
@@ -424,7 +425,7 @@ def config4(a, D, dev, rank, world):
             "history_fill": fill_n, "h_min": res.get("h_min", -1), "h_max": res.get("h_max", -1),
             "steady_state": res.get("h_min", -1) == a.history,
             "ms_per_step": round(T / steps * 1e3, 4), "achieved_hbm_gbps": round(bytes_all / T / 1e9, 1),
-            "exchange": "xgmi", "x0_generation_s": round(gen_s, 1),
+            "exchange": "xgmi+fold" if folded else "xgmi", "x0_generation_s": round(gen_s, 1),
             "solver": {"status": res["status"], "f": res["f"], "gnorm": res["gnorm"]},
             "shard_check": check}
 

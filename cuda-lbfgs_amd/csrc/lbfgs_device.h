@@ -127,6 +127,7 @@ int lbk_peer_connect(lbk_ctx* c, const void* handles);
 int lbk_peer_enable(lbk_ctx* c, int on);
 /* 0 none (one rank), 1 RCCL, 2 xGMI peer mailboxes, 3 host group (emulated ranks) */
 int lbk_exchange_backend(const lbk_ctx* c);
+int lbk_exchange_fold(const lbk_ctx* c);
 /* collective: iters back-to-back exchanges of a ks-component slot through backend 1 or 2;
  * host wall time per exchange in microseconds */
 int lbk_exchange_bench(lbk_ctx* c, int backend, int ks, int iters, double* us);

@@ -435,6 +435,7 @@ int lbfgs_set_dense_quadratic(lbfgs_ctx* c, const double* A, const double* b) {
 }
 
 int lbfgs_exchange_backend(const lbfgs_ctx* c) { return c ? lbk_exchange_backend(c->dev) : LBFGS_ERR_BAD_ARG; }
+int lbfgs_exchange_fold(const lbfgs_ctx* c) { return c ? lbk_exchange_fold(c->dev) : LBFGS_ERR_BAD_ARG; }
 
 int lbfgs_exchange_latency(lbfgs_ctx* c, int backend, int components, int iters, double* us) {
     if (!c || !us) return LBFGS_ERR_BAD_ARG;

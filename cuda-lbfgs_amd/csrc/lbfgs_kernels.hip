@@ -130,8 +130,10 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
     if (const char* e = getenv("LBFGS_COOP")) c->coop_max = std::min(atoi(e), LBK_COOP_SEGMAX);  // max segments
     c->pend_slot = -1;
     c->xf_slot = -1;
-    c->fold_env = 1;  // folded exchanges over the mailboxes; LBFGS_XGMI_FOLD=0: off
-    if (const char* e = getenv("LBFGS_XGMI_FOLD")) c->fold_env = atoi(e) != 0;
+    // folded exchanges over the mailboxes: 1 (default) when every peer has a GPU of
+    // its own; 2 also for ranks sharing a GPU (tests on grids that fit beside each other); 0 off
+    c->fold_env = 1;
+    if (const char* e = getenv("LBFGS_XGMI_FOLD")) c->fold_env = atoi(e);
     // measured (profiles/r01/defer_ab.txt): +21..32 % at n = 3e5 (586 segments); -14 % at 1954
     // segments and worse beyond, where every workgroup forms two or more group trees
     c->defer_max = LBK_SEG_PER_GROUP;
@@ -1088,7 +1090,9 @@ int lbk_peer_enable(lbk_ctx* c, int on) {
     }
     c->xg_on = on ? 1 : 0;
     c->xf_on = 0;
-    if (on && c->fold_env && c->geo.world > 1 && !c->grp && lbk_xgmi_fold_info(c->xg, &c->xf) == 0) c->xf_on = 1;
+    if (on && c->fold_env && c->geo.world > 1 && !c->grp && lbk_xgmi_fold_info(c->xg, &c->xf) == 0 &&
+        (c->fold_env == 2 || !c->xf.shared_device))
+        c->xf_on = 1;
     return 0;
 }
 
@@ -1119,6 +1123,8 @@ int lbk_exchange_bench(lbk_ctx* c, int backend, int ks, int iters, double* us) {
     *us = ((double)(t1.tv_sec - t0.tv_sec) * 1e6 + (double)(t1.tv_nsec - t0.tv_nsec) * 1e-3) / iters;
     return rc;
 }
+
+int lbk_exchange_fold(const lbk_ctx* c) { return c->xf_on; }
 
 int lbk_exchange_backend(const lbk_ctx* c) {
     if (c->geo.world <= 1) return c->comm ? 1 : 0;

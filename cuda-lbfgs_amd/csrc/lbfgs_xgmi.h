@@ -54,6 +54,7 @@ struct lbk_xgmi_fold {
     unsigned long long timeout;        // wall-clock ticks
     int positions;                     // doubles per parity (the mailbox's [2][positions][2] layout)
     int rank, world;
+    int shared_device;  // some peer's mailbox lives on this rank's own GPU (ranks sharing a device)
 };
 int lbk_xgmi_fold_info(const lbk_xgmi* x, lbk_xgmi_fold* out);  // -5 before a successful connect
 // the epoch of the next exchange (the counter the exchange kernel advances, shared)

@@ -35,6 +35,7 @@ struct lbk_xgmi {
     int connected;
     std::vector<unsigned long long*> opened;  // peer mappings to close
     unsigned long long** peers_dev;           // device copy of peers.mb (folded exchanges)
+    int shared_device;                        // a peer's mailbox is on this GPU (or unknown)
 };
 
 namespace {
@@ -220,6 +221,12 @@ int lbk_xgmi_connect(lbk_xgmi* x, const void* handles, hipStream_t stream, char*
         }
         x->peers.mb[p] = static_cast<unsigned long long*>(ptr);
         x->opened.push_back(x->peers.mb[p]);
+        // which GPU holds the peer's mailbox: ranks sharing this GPU (one-card rehearsals and
+        // tests) must not fold their exchanges into the passes (a pass's spinning
+        // workgroups could hold every CU the peer's producing kernel needs)
+        hipPointerAttribute_t at;
+        if (hipPointerGetAttributes(&at, ptr) != hipSuccess || at.device == x->device) x->shared_device = 1;
+        (void)hipGetLastError();
     }
     // self-test: 4 exchanges (both mailbox parities twice) of the widest slot, checked bit for
     // bit on the host; a short timeout so that a broken path fails fast and the caller can
@@ -284,6 +291,7 @@ int lbk_xgmi_fold_info(const lbk_xgmi* x, lbk_xgmi_fold* out) {
     out->positions = x->positions;
     out->rank = x->rank;
     out->world = x->world;
+    out->shared_device = x->shared_device;
     return 0;
 }
 

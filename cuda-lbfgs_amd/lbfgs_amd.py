@@ -114,6 +114,7 @@ def lib():
     L.lbfgs_peer_connect.argtypes = [vp, C.c_char_p]
     L.lbfgs_peer_enable.argtypes = [vp, C.c_int]
     L.lbfgs_exchange_backend.argtypes = [vp]
+    L.lbfgs_exchange_fold.argtypes = [vp]
     L.lbfgs_exchange_latency.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_double)]
     L.lbfgs_spec_stats.argtypes = [vp, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
     L.lbfgs_prof_enable.argtypes = [vp, C.c_int]
@@ -136,7 +137,7 @@ EXPORTED_SYMBOLS = [
     "lbfgs_dev_dot", "lbfgs_dev_norm", "lbfgs_dev_objective", "lbfgs_dev_trial",
     "lbfgs_dev_twoloop", "lbfgs_dev_elementwise", "lbfgs_line_search", "lbfgs_prof_enable",
     "lbfgs_prof_reset", "lbfgs_prof_get", "lbfgs_peer_handle", "lbfgs_peer_connect", "lbfgs_peer_enable",
-    "lbfgs_exchange_backend", "lbfgs_exchange_latency", "lbfgs_device_count", "lbfgs_set_dense_quadratic", "lbfgs_build_info",
+    "lbfgs_exchange_backend", "lbfgs_exchange_fold", "lbfgs_exchange_latency", "lbfgs_device_count", "lbfgs_set_dense_quadratic", "lbfgs_build_info",
     "lbfgs_spec_stats",
 ]
 PEER_HANDLE_BYTES = 64
@@ -339,6 +340,11 @@ class Context:
     @property
     def backend(self):
         return BACKENDS.get(lib().lbfgs_exchange_backend(self.h), "unknown")
+
+    @property
+    def folded(self):
+        """the two-loop's mailbox exchanges ride inside the passes (lbfgs_exchange_fold)"""
+        return lib().lbfgs_exchange_fold(self.h) == 1
 
     def _err(self, what, rc):
         msg = lib().lbfgs_last_error(self.h)

@@ -187,6 +187,11 @@ int lbfgs_peer_connect(lbfgs_ctx* ctx, const void* handles /* world x LBFGS_PEER
 int lbfgs_peer_enable(lbfgs_ctx* ctx, int on);
 /* 0: one rank, 1: RCCL all-gathers, 2: xGMI peer mailboxes, 3: host group (emulated ranks) */
 int lbfgs_exchange_backend(const lbfgs_ctx* ctx);
+/* 1 when the mailbox exchanges of the two-loop are folded into the passes (the producing pass
+ * pushes its reduction to the peers, the consuming pass polls it: no exchange launch between
+ * them). On by default when every peer runs on a GPU of its own; LBFGS_XGMI_FOLD=2
+ * forces it for ranks sharing a GPU, 0 turns it off. */
+int lbfgs_exchange_fold(const lbfgs_ctx* ctx);
 /* collective diagnostic (every rank calls it with the same arguments): `iters` back-to-back
  * exchanges of a `components`-wide result slot (8 = a two-loop reduction, up to 96) through
  * backend 1 (RCCL) or 2 (xGMI mailboxes); *us = host wall time per exchange */

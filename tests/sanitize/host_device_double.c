@@ -121,6 +121,11 @@ int lbk_exchange_backend(const lbk_ctx* c) {
     (void)c;
     return 0;
 }
+
+int lbk_exchange_fold(const lbk_ctx* c) {
+    (void)c;
+    return 0;
+}
 int lbk_exchange_bench(lbk_ctx* c, int b, int ks, int it, double* us) {
     (void)c, (void)b, (void)ks, (void)it, (void)us;
     return -1;

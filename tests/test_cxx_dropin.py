@@ -319,7 +319,7 @@ def test_cuda_progress_lines(tmp_path):
     src = tmp_path / "p.cpp"
     src.write_text(_PROGRESS_CALLER)
     exe = tmp_path / "p"
-    subprocess.run(["g++", "-std=c++17", "-O2", *link, "-I", os.path.join(ROOT, "include"), str(src), "-o",
+    subprocess.run(["g++", "-std=c++17", "-O2", "-I", os.path.join(ROOT, "include"), str(src), "-o",
                     str(exe), "-L", PKG, "-l:liblbfgs_hip.so", "-Wl,-rpath," + PKG], check=True, capture_output=True)
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120,
                        env=dict(os.environ, LBFGS_CUDA_PROGRESS="1"))

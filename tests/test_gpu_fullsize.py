@@ -103,14 +103,19 @@ def _single(ls, iters, vf):
     return _one_gpu[key]
 
 
-@pytest.mark.parametrize("ls,mode", [("backtracking", "default"), ("wolfe", "default"),
-                                     ("backtracking", "vf")])
-def test_config4_mailboxes_8_processes(tmp_path, ls, mode):
+@pytest.mark.parametrize("ls,mode,fold", [("backtracking", "default", "2"), ("wolfe", "default", "2"),
+                                          ("backtracking", "default", "auto"), ("backtracking", "vf", "auto")])
+def test_config4_mailboxes_8_processes(tmp_path, ls, mode, fold):
+    """fold "2": the two-loop's exchanges folded into the passes, as 8 ranks on 8 GPUs run them
+    (forced here, where the 8 ranks share one GPU); "auto": this box's own choice (the exchange
+    kernel, the ranks sharing a GPU)."""
     iters = 13  # h reaches m = 10 (the ring full) for the last iterations
     ref = _single(ls, iters, mode == "vf")
     # the library's own stage-2 and mirror choices, as bench.py runs it
     outs = run_ranks(tmp_path, 8, N4, 10, "rosenbrock", ls, iters, mode,
-                     unset=("LBFGS_TICKET", "LBFGS_XGMI_MIRROR"))
+                     env={"LBFGS_XGMI_FOLD": "2"} if fold == "2" else None,
+                     unset=("LBFGS_TICKET", "LBFGS_XGMI_MIRROR", "LBFGS_XGMI_FOLD"))
+    assert all(bool(o["folded"]) == (fold == "2") for o in outs)
     x = np.zeros(N4)
     for r, o in enumerate(outs):
         for key in ("tr_f", "tr_gnorm", "tr_alpha"):

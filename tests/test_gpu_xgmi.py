@@ -24,8 +24,9 @@ def bits(a):
     return np.asarray(a, dtype=np.float64).view(np.uint64)
 
 
-def run_ranks(tmp_path, world, n, m, obj, ls, iters, mode, env=None, unset=()):
+def run_ranks(tmp_path, world, n, m, obj, ls, iters, mode, env=None, unset=(), timeout=150):
     e = {k: v for k, v in os.environ.items() if k not in unset}
+    e.setdefault("LBFGS_XGMI_TIMEOUT", "20")  # a lost exchange fails the test instead of hanging it
     e.update(env or {})
     procs = [subprocess.Popen([sys.executable, WORKER, str(tmp_path), str(r), str(world), str(n), str(m), obj, ls,
                                str(iters), mode], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=e)
@@ -33,7 +34,7 @@ def run_ranks(tmp_path, world, n, m, obj, ls, iters, mode, env=None, unset=()):
     outs = []
     for p in procs:
         try:
-            out, _ = p.communicate(timeout=240)
+            out, _ = p.communicate(timeout=timeout)
         except subprocess.TimeoutExpired:  # pragma: no cover
             for q in procs:
                 q.kill()
@@ -73,6 +74,42 @@ def test_xgmi_sharded_bit_exact(tmp_path, world, obj, ls, mode, ticket, mirror="
     assert np.array_equal(bits(x), bits(ref["x"]))
 
 
+@pytest.mark.parametrize("world,obj,ls,mode", [
+    (2, "rosenbrock", "backtracking", "default"),
+    (4, "quad_tridiag", "wolfe", "default"),
+    (8, "rosenbrock", "interpolation", "default"),
+    (2, "rosenbrock", "backtracking", "vf"),
+])
+def test_xgmi_folded_exchange_bit_exact(tmp_path, world, obj, ls, mode):
+    """The two-loop's exchanges folded into the passes (LBFGS_XGMI_FOLD=2 forces it for ranks
+    sharing this one GPU; it is the default when every rank has a GPU of its own): the producing
+    pass's stage 2 pushes its group value, an r pass its rank edges, straight into the peers'
+    mailboxes, and the consuming pass polls them in its prologue. In-launch (ticket) stage 2, as
+    every sharded run with segments >= 8192 elements uses. Bit-identical to one GPU."""
+    n, m, iters = 4_000_003, 5, 12
+    x0 = L.x0_uniform(n, 42, -2.0, 2.0)
+    with L.Context(n, m) as c:
+        ref = c.minimize(obj, x0, ls, iters, trace=True, vector_free=(mode == "vf"))
+    outs = run_ranks(tmp_path, world, n, m, obj, ls, iters, mode, env={"LBFGS_TICKET": "1", "LBFGS_XGMI_FOLD": "2"})
+    x = np.zeros(n)
+    for r, o in enumerate(outs):
+        assert bool(o["folded"])  # vector-free runs fold nothing but report the setting
+        for key in ("tr_f", "tr_gnorm", "tr_alpha"):
+            assert np.array_equal(bits(o[key]), bits(ref[key])), (r, key)
+        assert np.array_equal(o["tr_c1"], ref["tr_c1"]) and np.array_equal(o["tr_c2"], ref["tr_c2"]), r
+        lo = int(o["lo"])
+        x[lo:lo + len(o["x"])] = o["x"]
+        assert str(o["messages"]) == ref["messages"]
+    assert np.array_equal(bits(x), bits(ref["x"]))
+
+
+def test_xgmi_fold_off_on_a_shared_gpu(tmp_path):
+    """Ranks sharing one GPU do not fold by default (a pass's spinning workgroups could hold the CUs
+    the peer's producing kernel waits for); the exchange kernel carries their reductions."""
+    outs = run_ranks(tmp_path, 2, 4_000_003, 5, "rosenbrock", "backtracking", 3, "default", unset=("LBFGS_XGMI_FOLD",))
+    assert not any(bool(o["folded"]) for o in outs)
+
+
 @pytest.mark.parametrize("mode,ls,ticket", [("default", "wolfe", "1"), ("vf", "interpolation", "0")])
 def test_xgmi_host_mirror_bit_exact(tmp_path, mode, ls, ticket):
     """LBFGS_XGMI_MIRROR=1: the exchange kernel also fills the host mirror of the slots the host
@@ -89,7 +126,7 @@ def test_xgmi_soak_8_ranks_bit_exact(tmp_path):
     with L.Context(n, m) as c:
         ref = c.minimize("rosenbrock", x0, "backtracking", iters, trace=True)
     outs = run_ranks(tmp_path, 8, n, m, "rosenbrock", "backtracking", iters, "default",
-                     env={"LBFGS_TICKET": "1"})
+                     env={"LBFGS_TICKET": "1"}, timeout=280)
     x = np.zeros(n)
     for r, o in enumerate(outs):
         for key in ("tr_f", "tr_gnorm", "tr_alpha"):

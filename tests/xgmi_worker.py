@@ -63,6 +63,7 @@ def main():
         print(f"rank {rank}: peer connect failed: {msg}", flush=True)
         sys.exit(3)
     assert ctx.backend == "xgmi", ctx.backend
+    folded = ctx.folded
     if mode == "latency":  # lbfgs_exchange_latency through the mailboxes (collective)
         us8 = ctx.exchange_latency("xgmi", 8, 50)
         us96 = ctx.exchange_latency("xgmi", 96, 50)
@@ -74,7 +75,7 @@ def main():
     lo, nl = ctx.elem_lo, ctx.n_loc
     np.savez(os.path.join(d, f"out{rank}.npz"), tr_f=r["tr_f"], tr_gnorm=r["tr_gnorm"], tr_alpha=r["tr_alpha"],
              tr_c1=r["tr_c1"], tr_c2=r["tr_c2"], x=r["x"][lo:lo + nl], lo=lo, status=r["status"],
-             messages=r["messages"])
+             messages=r["messages"], folded=folded)
     ctx.close()
     print(f"rank {rank}: {r['status']} after {r['iterations']} iterations, f={r['f']!r}", flush=True)
 

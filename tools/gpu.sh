@@ -25,7 +25,14 @@ step_smoke() {
 step_suite() {
     local args=("$@"); [ ${#args[@]} -eq 0 ] && args=(tests)
     timeout -k 10 1000 python -u -m pytest "${args[@]}" -m gpu -v --timeout 300 --timeout-method thread \
-        > gpurun_out/pytest_gpu.log 2>&1
+        > gpurun_out/pytest_gpu.log 2>&1 &
+    local pid=$! n=0
+    # a progress line a minute (a multi-process test can run a few minutes without a result line)
+    while kill -0 $pid 2> /dev/null; do
+        sleep 5; n=$((n + 1))
+        [ $((n % 12)) -eq 0 ] && echo "suite running: $(grep -c -E 'PASSED|FAILED|ERROR' gpurun_out/pytest_gpu.log) results"
+    done
+    wait $pid
     local rc=$?; echo "suite rc=$rc"; tail -3 gpurun_out/pytest_gpu.log; return $rc
 }
 
