@@ -363,11 +363,15 @@ class Context:
 
     def minimize(self, objective, x0, line_search="backtracking", max_iterations=1000, m=None,
                  tolerance=1e-5, verbose=False, quiet=True, trace=False, consts=None,
-                 f=None, grad=None, unfused=False, vector_free=False, reference_calls=False):
+                 f=None, grad=None, unfused=False, vector_free=False, reference_calls=False, out=None):
+        """out: a caller-owned float64 buffer of n for the result (else a new array; a fresh
+        array's pages are first touched by the result's copy, which costs as much as the copy)"""
         assert m is None or m == self.m
         x0 = np.ascontiguousarray(x0, dtype=np.float64)
         assert x0.shape == (self.n,)
-        x = np.zeros(self.n)
+        if out is not None:
+            assert out.dtype == np.float64 and out.shape == (self.n,) and out.flags["C_CONTIGUOUS"]
+        x = out if out is not None else np.zeros(self.n)
         res = Result()
         flags = (FLAG_VERBOSE if verbose else 0) | (FLAG_QUIET if quiet else 0) | \
                 (FLAG_TRACE if trace else 0) | (FLAG_UNFUSED if unfused else 0) | \

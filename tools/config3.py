@@ -62,20 +62,24 @@ def solve(n, m, batch, prof):
     return out
 
 
-def to_solution(n, m, mode, reps=3):
+def to_solution(n, m, mode, reps=3, fresh_out=False):
     """lbfgs_minimize end to end (x0 upload from the caller's pageable buffer, the solve, x
-    download) with LBFGS_XFER=mode; median of reps, the context created beforehand"""
+    download) with LBFGS_XFER=mode; median of reps, the context created beforehand. The result
+    goes into a caller buffer that exists (touched) unless fresh_out: then into a new array,
+    whose first-touch page faults the download pays (what round 2's 0.112 s measured)."""
     os.environ["LBFGS_BATCH"] = "1"
     os.environ["LBFGS_XFER"] = mode
     x0 = L.x0_uniform(n, 42, -2.0, 2.0)
+    out = None if fresh_out else np.ones(n)
     times, r = [], None
     with L.Context(n, m) as c:
         for _ in range(reps + 1):
             t0 = time.perf_counter()
-            r = c.minimize("quad_tridiag", x0, "wolfe", 1000, tolerance=1e-5)
+            r = c.minimize("quad_tridiag", x0, "wolfe", 1000, tolerance=1e-5, out=out)
             times.append(time.perf_counter() - t0)
     times = sorted(times[1:])
-    return dict(mode=mode, seconds=times[len(times) // 2], seconds_all=times, iterations=r["iterations"],
+    return dict(mode=mode, output_buffer="new array" if fresh_out else "caller's (touched)",
+                seconds=times[len(times) // 2], seconds_all=times, iterations=r["iterations"],
                 status=r["status"], f=r["f"], x_checksum=int(r["x"].view(np.uint64).sum(dtype=np.uint64)))
 
 
@@ -84,7 +88,8 @@ def main():
     outp = sys.argv[1] if len(sys.argv) > 1 and not sys.argv[1].startswith("--") else None
     res = dict(config="configs[3]: quad_tridiag n=%d m=20 wolfe, tol 1e-5, x0 ~ U(-2,2) seed 42" % n)
     # time to solution including the caller's transfers, per transfer mode
-    res["with_transfers"] = [to_solution(n, 20, mode) for mode in ("pageable", "register", "staged")]
+    res["with_transfers"] = [to_solution(n, 20, mode, fresh_out=fresh) for fresh in (False, True)
+                             for mode in ("pageable", "register", "staged")]
     for row in res["with_transfers"]:
         print("with_transfers", json.dumps(row), flush=True)
     os.environ.pop("LBFGS_XFER", None)

@@ -63,7 +63,12 @@ step_profile() {
 step_rehearse() {
     local W=$1; shift
     BENCH_DEVICE_MOD=1 timeout -k 10 1100 python -m torch.distributed.run --nnodes=1 --nproc-per-node "$W" \
-        --master-addr 127.0.0.1 --master-port 29519 bench.py --gpus "$W" "$@" > "gpurun_out/rehearse_w$W.log" 2>&1
+        --master-addr 127.0.0.1 --master-port 29519 bench.py --gpus "$W" "$@" > "gpurun_out/rehearse_w$W.log" 2>&1 &
+    local pid=$! n=0
+    while kill -0 $pid 2> /dev/null; do  # a progress line a minute
+        sleep 5; n=$((n + 1)); [ $((n % 12)) -eq 0 ] && echo "rehearse W=$W running ($((n * 5)) s)"
+    done
+    wait $pid
     local rc=$?; echo "rehearse W=$W rc=$rc"
     [ $rc -eq 0 ] || { tail -30 "gpurun_out/rehearse_w$W.log"; return 1; }
     grep '^{' "gpurun_out/rehearse_w$W.log" > "gpurun_out/rehearse_w$W.json"; cat "gpurun_out/rehearse_w$W.json"
