@@ -12,6 +12,9 @@
 //
 // Reports algorithmic GB/s = (NR + NW) * 8 * n / kernel time (HIP events, median of 15 reps, one
 // warm-up), n = 1e8 (configs[2]: 800 MB per vector, far beyond the 256 MiB Infinity Cache).
+// "_alt" cases walk the segments in the opposite direction on every other rep, as the product's
+// consecutive passes do (LBFGS_REV): a rep then starts on the tail the previous rep touched last.
+// Above n = 4e8 only the cases with at most 4 inputs run (8 vectors of 8n bytes are allocated).
 // Build: hipcc --offload-arch=gfx950 -O3 -o tools/mixprobe tools/mixprobe.hip
 // Run:   tools/mixprobe [n]
 #include <hip/hip_runtime.h>
@@ -54,9 +57,10 @@ __device__ __forceinline__ void st(double* p, dvec2 v) {
 // vectors q / r / d of the product) keep the default policy; INPL: output 0 is input 0 (in place,
 // as the two-loop's q)
 template <int NR, int NW, int U, bool LNT, bool SNT, int TWL, int TWS, bool INPL>
-__global__ __launch_bounds__(256) void k_mix(Vecs v, int64_t n, int64_t L, double* sink) {
+__global__ __launch_bounds__(256) void k_mix(Vecs v, int64_t n, int64_t L, int rev, double* sink) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int64_t sbeg = (int64_t)blockIdx.x * L;
+    const int64_t seg = rev ? (int64_t)gridDim.x - 1 - blockIdx.x : blockIdx.x;
+    const int64_t sbeg = seg * L;
     const int64_t len = min(L, n - sbeg);
     const int nrows = (int)(len / 128);
     const int myrows = nrows > w ? (nrows - w + 3) / 4 : 0;
@@ -96,12 +100,14 @@ __global__ __launch_bounds__(256) void k_mix(Vecs v, int64_t n, int64_t L, doubl
 struct Case {
     const char* name;
     int nr, nw;
-    void (*launch)(Vecs, int64_t, int64_t, int, double*);
+    void (*launch)(Vecs, int64_t, int64_t, int, int, double*);
+    bool alt;
 };
 
 template <int NR, int NW, int U, bool LNT, bool SNT, int TWL, int TWS, bool INPL>
-void launch(Vecs v, int64_t n, int64_t L, int nseg, double* sink) {
-    hipLaunchKernelGGL((k_mix<NR, NW, U, LNT, SNT, TWL, TWS, INPL>), dim3(nseg), dim3(256), 0, 0, v, n, L, sink);
+void launch(Vecs v, int64_t n, int64_t L, int nseg, int rev, double* sink) {
+    hipLaunchKernelGGL((k_mix<NR, NW, U, LNT, SNT, TWL, TWS, INPL>), dim3(nseg), dim3(256), 0, 0, v, n, L, rev,
+                       sink);
 }
 
 int main(int argc, char** argv) {
@@ -110,10 +116,12 @@ int main(int argc, char** argv) {
     const int64_t L = std::max<int64_t>(512, ((n + 8191) / 8192 + 127) / 128 * 128);
     const int nseg = (int)((n + L - 1) / L);
     const int64_t npad = (int64_t)nseg * L;
-    std::vector<double*> bufs(MAXV + 4);
-    for (auto& b : bufs) {
-        CK(hipMalloc(&b, sizeof(double) * npad));
-        CK(hipMemset(b, 0, sizeof(double) * npad));
+    const int maxnr = n > 400000000 ? 4 : MAXV;
+    std::vector<double*> bufs(MAXV + 4, nullptr);
+    for (int k = 0; k < MAXV + 4; ++k) {
+        if (k >= maxnr && k < MAXV) continue;
+        CK(hipMalloc(&bufs[k], sizeof(double) * npad));
+        CK(hipMemset(bufs[k], 0, sizeof(double) * npad));
     }
     double* sink;
     CK(hipMalloc(&sink, 64));
@@ -124,33 +132,42 @@ int main(int argc, char** argv) {
     // product's kernels: k_mid q (df) + y -> r (df); k_axpy_dot q (df) + y + s -> q (df, in place);
     // k_commit r (df) + x + s + g -> x' + g' + s + y; k_vf_commit 22 nt -> 4 nt
     Case cases[] = {
-        {"1r0w_u4_nt", 1, 0, launch<1, 0, 4, true, true, 0, 0, false>},
-        {"1r1w_u4_ntnt", 1, 1, launch<1, 1, 4, true, true, 0, 0, false>},
-        {"mid_2r1w_u4", 2, 1, launch<2, 1, 4, true, true, 1, 1, false>},
-        {"mid_2r1w_u8", 2, 1, launch<2, 1, 8, true, true, 1, 1, false>},
-        {"axpy_3r1w_u4", 3, 1, launch<3, 1, 4, true, true, 1, 1, true>},
-        {"3r1w_u4_allnt", 3, 1, launch<3, 1, 4, true, true, 0, 0, false>},
-        {"commit_4r4w_u4", 4, 4, launch<4, 4, 4, true, true, 1, 0, false>},
-        {"commit_4r4w_u2", 4, 4, launch<4, 4, 2, true, true, 1, 0, false>},
-        {"commit_4r4w_u8", 4, 4, launch<4, 4, 8, true, true, 1, 0, false>},
-        {"4r4w_u4_ntld_dfst", 4, 4, launch<4, 4, 4, true, false, 1, 0, false>},
-        {"4r4w_u4_alldf", 4, 4, launch<4, 4, 4, false, false, 0, 0, false>},
-        {"4r2w_u4", 4, 2, launch<4, 2, 4, true, true, 1, 0, false>},
-        {"4r0w_u4", 4, 0, launch<4, 0, 4, true, true, 1, 0, false>},
-        {"vf_22r4w_u1", 22, 4, launch<22, 4, 1, true, true, 0, 0, false>},
-        {"vf_22r4w_u2", 22, 4, launch<22, 4, 2, true, true, 0, 0, false>},
-        {"22r4w_u1_ntld_dfst", 22, 4, launch<22, 4, 1, true, false, 0, 0, false>},
-        {"22r0w_u1", 22, 0, launch<22, 0, 1, true, true, 0, 0, false>},
+        {"1r0w_u4_nt", 1, 0, launch<1, 0, 4, true, true, 0, 0, false>, false},
+        {"1r1w_u4_ntnt", 1, 1, launch<1, 1, 4, true, true, 0, 0, false>, false},
+        {"mid_2r1w_u4", 2, 1, launch<2, 1, 4, true, true, 1, 1, false>, false},
+        {"mid_2r1w_u8", 2, 1, launch<2, 1, 8, true, true, 1, 1, false>, false},
+        {"axpy_3r1w_u4", 3, 1, launch<3, 1, 4, true, true, 1, 1, true>, false},
+        {"3r1w_u4_allnt", 3, 1, launch<3, 1, 4, true, true, 0, 0, false>, false},
+        {"commit_4r4w_u4", 4, 4, launch<4, 4, 4, true, true, 1, 0, false>, false},
+        {"commit_4r4w_u2", 4, 4, launch<4, 4, 2, true, true, 1, 0, false>, false},
+        {"commit_4r4w_u8", 4, 4, launch<4, 4, 8, true, true, 1, 0, false>, false},
+        {"4r4w_u4_ntld_dfst", 4, 4, launch<4, 4, 4, true, false, 1, 0, false>, false},
+        {"4r4w_u4_alldf", 4, 4, launch<4, 4, 4, false, false, 0, 0, false>, false},
+        {"4r2w_u4", 4, 2, launch<4, 2, 4, true, true, 1, 0, false>, false},
+        {"4r0w_u4", 4, 0, launch<4, 0, 4, true, true, 1, 0, false>, false},
+        {"vf_22r4w_u1", 22, 4, launch<22, 4, 1, true, true, 0, 0, false>, false},
+        {"vf_22r4w_u2", 22, 4, launch<22, 4, 2, true, true, 0, 0, false>, false},
+        {"22r4w_u1_ntld_dfst", 22, 4, launch<22, 4, 1, true, false, 0, 0, false>, false},
+        {"22r0w_u1", 22, 0, launch<22, 0, 1, true, true, 0, 0, false>, false},
+        {"axpy_3r1w_u4_inpl_allnt", 3, 1, launch<3, 1, 4, true, true, 0, 0, true>, false},
+        {"3r1w_u4_outpl_qdf", 3, 1, launch<3, 1, 4, true, true, 1, 1, false>, false},
+        {"axpy_3r1w_u4_inpl_allnt_alt", 3, 1, launch<3, 1, 4, true, true, 0, 0, true>, true},
+        {"mid_2r1w_u8_allnt", 2, 1, launch<2, 1, 8, true, true, 0, 0, false>, false},
+        {"commit_4r4w_u4_allnt", 4, 4, launch<4, 4, 4, true, true, 0, 0, false>, false},
+        {"mid_2r1w_u8_alt", 2, 1, launch<2, 1, 8, true, true, 1, 1, false>, true},
+        {"axpy_3r1w_u4_alt", 3, 1, launch<3, 1, 4, true, true, 1, 1, true>, true},
+        {"commit_4r4w_u4_alt", 4, 4, launch<4, 4, 4, true, true, 1, 0, false>, true},
     };
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     printf("n=%lld L=%lld segments=%d (one 256-thread workgroup each)\n", (long long)n, (long long)L, nseg);
     for (const Case& c : cases) {
+        if (c.nr > maxnr) continue;
         std::vector<float> ms;
         for (int r = 0; r < 16; ++r) {
             CK(hipEventRecord(e0, 0));
-            c.launch(v, n, L, nseg, sink);
+            c.launch(v, n, L, nseg, c.alt ? (r & 1) : 0, sink);
             CK(hipEventRecord(e1, 0));
             CK(hipEventSynchronize(e1));
             float t;
@@ -160,9 +177,10 @@ int main(int argc, char** argv) {
         std::sort(ms.begin(), ms.end());
         const double med = ms[ms.size() / 2];
         const double gbs = (double)(c.nr + c.nw) * 8.0 * (double)n / (med * 1e-3) / 1e9;
-        printf("%-22s %2dR %2dW  %9.1f us  %7.1f GB/s  (min %.1f us)\n", c.name, c.nr, c.nw, med * 1e3, gbs,
+        printf("%-28s %2dR %2dW  %9.1f us  %7.1f GB/s  (min %.1f us)\n", c.name, c.nr, c.nw, med * 1e3, gbs,
                ms.front() * 1e3);
     }
-    for (auto b : bufs) CK(hipFree(b));
+    for (auto b : bufs)
+        if (b) CK(hipFree(b));
     return 0;
 }
