@@ -528,10 +528,15 @@ def roofline(prof, n, world):
     achieved = per_launch / avg_s / 1e9
     traffic, tsrc = pmc_traffic(dom, n, world)
     tot = sum(q["ms"] for q in prof.values())
+    # every streaming kernel's own rate (algorithmic bytes / event-timed duration), for A/B lines
+    rates = {k: {"avg_launch_us": round(prof[k]["ms"] / prof[k]["launches"] * 1e3, 2),
+                 "gbps": round(prof[k]["bytes"] / (prof[k]["ms"] / 1e3) / 1e9, 1)}
+             for k in streaming if prof[k]["launches"] and prof[k]["ms"] > 0}
     return dict(bound="hbm", kernel=dom, achieved=round(achieved, 1), peak=HBM_PEAK_GBPS, unit="GB/s",
                 frac=round(achieved / HBM_PEAK_GBPS, 4), traffic=traffic, traffic_unit="bytes/launch",
                 traffic_source=tsrc, bytes_per_launch=per_launch, avg_launch_us=round(avg_s * 1e6, 2),
-                launches=p["launches"], kernel_share={k: round(v["ms"] / tot, 4) for k, v in prof.items()})
+                launches=p["launches"], kernel_share={k: round(v["ms"] / tot, 4) for k, v in prof.items()},
+                kernel_rates=rates)
 
 
 def main():

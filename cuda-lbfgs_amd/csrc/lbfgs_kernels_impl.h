@@ -1066,16 +1066,25 @@ struct DirArgs {
     unsigned long long tmo;
 };
 
+// A/B: LBK_DIR_NT=1 streams the direction source (d, or r of the last second-loop pass) of the
+// commit and the trials non-temporal
+#ifndef LBK_DIR_NT
+#define LBK_DIR_NT 0
+#endif
+template <bool NT>
+__device__ __forceinline__ double2 ldd(const double* p) {
+    return LBK_DIR_NT ? ldv<NT>(p) : ldw<NT>(p);
+}
 template <int DMODE, bool NT>
 __device__ __forceinline__ double2 load_dir(const DirArgs& da, int64_t i, double2 gv) {
     double2 d;
     if (DMODE == LBK_D_BUF) {
-        d = ldw<NT>(da.dsrc + i);
+        d = ldd<NT>(da.dsrc + i);
     } else if (DMODE == LBK_D_NEG_G) {
         d.x = -gv.x;
         d.y = -gv.y;
     } else {
-        const double2 rv = ldw<NT>(da.dsrc + i);
+        const double2 rv = ldd<NT>(da.dsrc + i);
         const double2 sv = ldv<NT>(da.s + i);
         d.x = -(rv.x + sv.x * da.coef);
         d.y = -(rv.y + sv.y * da.coef);
