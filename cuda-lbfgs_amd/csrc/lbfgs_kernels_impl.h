@@ -2685,7 +2685,10 @@ Red kred(lbk_ctx* c, int slot, int K = 1) {
     r.fp = FoldPush{nullptr, 0, 0, 0, 0u};
     const int si = slot < LBK_NSLOTS ? slot : LBK_NSLOTS + slot - LBK_WSLOT0;
     c->slot_s2[si] = 0;
-    if (r.ticket && r.hslot && c->geo.world == 1 && !c->comm && !c->grp && c->sp_dh) {
+    // each group's last arriver stores the word, so it stands for the whole slot only when every
+    // segment is in one group (with several, the first group done would release the host early)
+    if (r.ticket && r.hslot && c->geo.world == 1 && !c->comm && !c->grp && c->sp_dh &&
+        c->geo.nseg <= LBK_SEG_PER_GROUP) {
         r.done = c->sp_dh + 1;
         r.epoch = ++c->s2_epoch;
         c->slot_s2[si] = r.epoch;

@@ -389,6 +389,33 @@ def test_deferred_stage2_bit_exact(monkeypatch, n, m, ls, obj):
     assert np.array_equal(bits(b["tr_f"]), bits(o["f"]))
 
 
+@pytest.mark.parametrize("n,m,ls,obj,vf", [(3_000_000, 10, "backtracking", "rosenbrock", False),
+                                           (5_000_000, 5, "wolfe", "quad_tridiag", False),
+                                           (2_500_000, 7, "interpolation", "rosenbrock", True)])
+def test_ticket_stage2_one_rank_bit_exact(monkeypatch, n, m, ls, obj, vf):
+    """In-launch tickets on ONE rank over several groups (LBFGS_TICKET=1; the default only up to
+    64 segments): each group's last arriver forms its tree, and the host may read a result slot
+    only once every group has. Round 3 found the single completion word of the one-group case
+    releasing the host after the first group here (NaN trajectories at n = 2.5e6 .. 3e7); the
+    trajectories must be the reduce-kernel sequence's bit for bit."""
+    x0 = L.x0_uniform(n, 11, -2.0, 2.0)
+    out = []
+    for ticket in ("0", "1"):
+        monkeypatch.setenv("LBFGS_TICKET", ticket)
+        with L.Context(n, m) as c:
+            c.prof_reset()
+            c.prof_enable(True)
+            r = c.minimize(obj, x0, ls, 12, trace=True, vector_free=vf)
+            r["reduce_launches"] = c.prof_get("group_reduce")["launches"]
+            out.append(r)
+    a, b = out
+    assert b["reduce_launches"] < a["reduce_launches"]  # the ticket path really ran
+    for key in ("tr_f", "tr_gnorm", "x"):
+        assert np.array_equal(bits(a[key]), bits(b[key])), key
+    assert np.array_equal(a["tr_c1"], b["tr_c1"]) and a["messages"] == b["messages"]
+    assert np.all(np.isfinite(b["tr_f"]))
+
+
 @pytest.mark.parametrize("vector_free", [False, True])
 def test_full_run_to_convergence_bit_exact(vector_free):
     """BASELINE configs[0] to convergence (Rosenbrock n=1e4, m=5, backtracking, tol 1e-5: ~17k
