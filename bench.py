@@ -303,6 +303,11 @@ def measure(a, D, n, x0, dev, rank, world, uid, unfused=False, vector_free=False
             p = ctx.prof_get(kname)
             if p["launches"]:
                 prof[kname] = p
+        # the GPU's busy share of those iterations: kernel time (exchange launches included) over
+        # wall time; the rest is launch gaps, host decisions and waits (the events add a few us)
+        kms = sum(p["ms"] for p in prof.values())
+        prof["_busy"] = {"kernel_ms": round(kms, 3), "wall_ms": round(prof_wall_ms, 3),
+                         "share": round(kms / max(prof_wall_ms, 1e-9), 4)}
         if world > 1:
             # the share of the (instrumented) iterations this rank spent in reduction exchanges,
             # waiting for its peers included; the max over ranks is reported
@@ -652,6 +657,7 @@ def main():
             "roofline": roof,
             "exchange_latency_us": xlat,
             "exchange_share": prof.get("_exchange_share"),
+            "kernel_busy": prof.get("_busy"),
             "cpu_baseline": cpu,
             "reference_parity": parity,
             "solver": {"status": res["status"], "f": res["f"], "gnorm": res["gnorm"],
