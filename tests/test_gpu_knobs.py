@@ -1,0 +1,85 @@
+"""Every A/B knob of the device layer and the driver, alone and in the combinations that share
+state, against the default path: identical trajectories, bit for bit (the canonical order does
+not depend on how a pass is launched, where its stage 2 runs, which cache policy it streams with
+or in which direction it walks). Round 3 found in-launch tickets on one rank releasing the host
+after the first of several groups (LBFGS_TICKET=1 at mid n: NaN trajectories); this matrix is the
+net for that class of interaction bug. Sizes cover each stage-2 regime of the default path:
+cooperative (<= 256 segments), deferred (<= 1024), reduce kernel (> 1024, 512- and 640-element
+segments)."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "cuda-lbfgs_amd"))
+import lbfgs_amd as L  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+KNOBS = ["LBFGS_TICKET", "LBFGS_DEFER", "LBFGS_REV", "LBFGS_NT", "LBFGS_DIRECT", "LBFGS_COOP",
+         "LBFGS_PERSIST", "LBFGS_PINGPONG", "LBFGS_SPEC", "LBFGS_BATCH", "LBFGS_SMALL_SEGS"]
+
+VARIANTS = {
+    "ticket1": {"LBFGS_TICKET": "1"},
+    "ticket0": {"LBFGS_TICKET": "0"},
+    "defer0": {"LBFGS_DEFER": "0"},
+    "defer_all": {"LBFGS_DEFER": "8192", "LBFGS_TICKET": "0"},
+    "rev0": {"LBFGS_REV": "0"},
+    "nt0": {"LBFGS_NT": "0"},
+    "nt1": {"LBFGS_NT": "1"},
+    "direct0": {"LBFGS_DIRECT": "0"},
+    "coop0": {"LBFGS_COOP": "0"},
+    "persist1": {"LBFGS_PERSIST": "1"},
+    "pingpong1": {"LBFGS_PINGPONG": "1"},
+    "spec0": {"LBFGS_SPEC": "0"},
+    "batch0": {"LBFGS_BATCH": "0"},
+    "ticket1_direct0": {"LBFGS_TICKET": "1", "LBFGS_DIRECT": "0"},
+    "ticket1_rev0_nt0": {"LBFGS_TICKET": "1", "LBFGS_REV": "0", "LBFGS_NT": "0"},
+    "ticket1_pingpong1": {"LBFGS_TICKET": "1", "LBFGS_PINGPONG": "1"},
+    "persist1_coop0_nt1": {"LBFGS_PERSIST": "1", "LBFGS_COOP": "0", "LBFGS_NT": "1"},
+    "defer_all_rev0_pingpong1": {"LBFGS_DEFER": "8192", "LBFGS_TICKET": "0", "LBFGS_REV": "0",
+                                 "LBFGS_PINGPONG": "1"},
+    "coop0_spec0_batch0": {"LBFGS_COOP": "0", "LBFGS_SPEC": "0", "LBFGS_BATCH": "0"},
+}
+
+CASES = [  # n, m, objective, line search, iterations
+    (100_003, 5, "rosenbrock", "backtracking", 25),       # 196 segments: cooperative iteration
+    (700_001, 7, "quad_tridiag", "wolfe", 12),             # 342 segments of 2048: deferred stage 2
+    (3_000_017, 5, "rosenbrock", "interpolation", 14),     # 5860 segments of 512: reduce kernel
+    (5_000_000, 10, "rosenbrock", "backtracking", 14),     # 7813 segments of 640, h = m reached
+]
+
+_default = {}
+
+
+def bits(a):
+    return np.ascontiguousarray(a, np.float64).view(np.uint64)
+
+
+def solve(monkeypatch, case, env):
+    n, m, obj, ls, iters = case
+    for k in KNOBS:
+        monkeypatch.delenv(k, raising=False)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    x0 = L.x0_uniform(n, 29, -2.0, 2.0)
+    with L.Context(n, m) as c:  # knobs are read at creation and per solve
+        return c.minimize(obj, x0, ls, iters, trace=True)
+
+
+@pytest.mark.parametrize("variant", sorted(VARIANTS))
+@pytest.mark.parametrize("case", CASES, ids=lambda c: f"n{c[0]}_{c[2]}_{c[3]}")
+def test_knob_bit_identical(monkeypatch, case, variant):
+    if case not in _default:
+        _default[case] = solve(monkeypatch, case, {})
+    a = _default[case]
+    b = solve(monkeypatch, case, VARIANTS[variant])
+    assert np.all(np.isfinite(b["tr_f"])) and np.all(np.isfinite(b["tr_gnorm"]))
+    for key in ("tr_f", "tr_gnorm", "x"):
+        assert np.array_equal(bits(a[key]), bits(b[key])), key
+    ta, tb = a["tr_alpha"], b["tr_alpha"]
+    assert np.array_equal(np.isnan(ta), np.isnan(tb)) and np.array_equal(ta[~np.isnan(ta)], tb[~np.isnan(tb)])
+    assert np.array_equal(a["tr_c1"], b["tr_c1"]) and np.array_equal(a["tr_c2"], b["tr_c2"])
+    assert a["messages"] == b["messages"] and a["status"] == b["status"] and a["iterations"] == b["iterations"]
