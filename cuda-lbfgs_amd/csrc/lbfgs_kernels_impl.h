@@ -660,9 +660,8 @@ struct op_unroll<OpMid<NT>> {
 };
 
 template <int K, class Op>
-__device__ __forceinline__ void stream(const Op& op, const Seg& s, const Geo& geo, double (&acc)[K]) {
-    int u0 = 0;
-    if (LBK_PIPELINE && s.len == geo.L) {
+__device__ __forceinline__ void stream(const Op& op, const Seg& s, const Geo& geo, double (&acc)[K], int u0 = 0) {
+    if (LBK_PIPELINE && s.len == geo.L && u0 == 0) {
         stream_pipelined(op, s, acc);
         return;
     }
@@ -812,6 +811,7 @@ struct OpAxpyDot {  // q = qin - alpha y;  acc += s . q       (lbfgs.cpp:133-137
     const double* __restrict__ y;
     const double* __restrict__ s;
     double alpha;
+    __device__ void set_coef(double a) { alpha = a; }
     struct Row {
         double2 q, y, s;
     };
@@ -851,6 +851,7 @@ struct OpMid {  // r = (qin - alpha0 y0) * gamma;  acc += y0 . r      (:134-137,
     double* edge_slot;  // sharded: this rank's edge r for the neighbours' commit halo
     int64_t n_loc;
     int g_lo, g_hi;
+    __device__ void set_coef(double a) { alpha = a; }
     struct Row {
         double2 q, y;
     };
@@ -879,6 +880,7 @@ struct OpAxpy2Dot {  // r += s (alpha - beta);  acc += ynext . r      (:159-164)
     double* edge_slot;  // sharded: this rank's edge r for the neighbours' commit halo
     int64_t n_loc;
     int g_lo, g_hi;
+    __device__ void set_coef(double c) { coef = c; }
     struct Row {
         double2 r, s, y;
     };
@@ -978,6 +980,32 @@ __device__ __forceinline__ void run_pass(const Op& op, const Geo& geo, const Red
     reduce_publish<K, FOLD>(acc, geo, red);
 }
 
+// Folded consumer (sharded over the mailboxes): the pass's coefficient waits for the peers' group
+// values, so a full segment issues its first row group's loads before it polls; the wait for the
+// xGMI hop runs under those loads instead of ahead of them. coef() is called by every thread (it
+// synchronises the workgroup). The rows are applied and accumulated in the same order as
+// run_pass, so the bits are the same.
+template <class Op, int K, class Coef>
+__device__ __forceinline__ void run_pass_prefetch(Op op, const Geo& geo, const Red& red, Coef coef) {
+    const Seg s = seg_setup(geo);
+    double acc[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) acc[k] = 0.0;
+    constexpr int U = op_unroll<Op>::value;
+    if (s.len == geo.L && s.nrows >= U) {
+        typename Op::Row r[U];
+        load_group<U, K>(op, s, 0, r);
+        op.set_coef(coef());
+        apply_group<U, K>(op, s, 0, r, acc);
+        stream(op, s, geo, acc, U);
+    } else {
+        op.set_coef(coef());
+        stream(op, s, geo, acc);
+    }
+    if (red.fp.peers && geo.edge_slot) fold_push_edges(geo, s, red.fp);
+    reduce_publish<K, true>(acc, geo, red);
+}
+
 template <class Op, int K>
 __device__ __forceinline__ void run_pass_halo(const Op& op, const Geo& geo, const Red& red) {
     const Seg s = seg_setup(geo);
@@ -1002,7 +1030,14 @@ template <bool NT, bool FOLD = false>
 __global__ __launch_bounds__(LB_BLOCK) void k_axpy_dot(double* qout, const double* qin, const double* __restrict__ y,
                                                        const double* __restrict__ sv, double rho,
                                                        const double* __restrict__ prev, Geo geo, Red red, FoldSrc fs) {
-    const double alpha = rho * ((FOLD && fs.mbx) ? src_total_mailbox(prev, geo, fs) : src_total(prev, geo));
+    if constexpr (FOLD) {
+        if (fs.mbx) {
+            run_pass_prefetch<OpAxpyDot<NT>, 1>(OpAxpyDot<NT>{qout, qin, y, sv, 0.0}, geo, red,
+                                                [&] { return rho * src_total_mailbox(prev, geo, fs); });
+            return;
+        }
+    }
+    const double alpha = rho * src_total(prev, geo);
     run_pass<OpAxpyDot<NT>, 1, FOLD>(OpAxpyDot<NT>{qout, qin, y, sv, alpha}, geo, red);
 }
 
@@ -1010,7 +1045,15 @@ template <bool NT, bool FOLD = false>
 __global__ __launch_bounds__(LB_BLOCK) void k_mid(double* __restrict__ rout, const double* __restrict__ qin,
                                                   const double* __restrict__ y0, double rho0, double gamma,
                                                   const double* __restrict__ prev, Geo geo, Red red, FoldSrc fs) {
-    const double alpha = rho0 * ((FOLD && fs.mbx) ? src_total_mailbox(prev, geo, fs) : src_total(prev, geo));
+    if constexpr (FOLD) {
+        if (fs.mbx) {
+            run_pass_prefetch<OpMid<NT>, 1>(OpMid<NT>{rout, qin, y0, 0.0, gamma, geo.edge_slot, geo.n_loc, geo.g_lo,
+                                                      geo.g_hi},
+                                            geo, red, [&] { return rho0 * src_total_mailbox(prev, geo, fs); });
+            return;
+        }
+    }
+    const double alpha = rho0 * src_total(prev, geo);
     run_pass<OpMid<NT>, 1, FOLD>(OpMid<NT>{rout, qin, y0, alpha, gamma, geo.edge_slot, geo.n_loc, geo.g_lo, geo.g_hi},
                                  geo, red);
 }
@@ -1021,7 +1064,18 @@ __global__ __launch_bounds__(LB_BLOCK) void k_axpy2_dot(double* r, const double*
                                                         const double* __restrict__ yn, double rho,
                                                         const double* __restrict__ pb, const double* __restrict__ pa,
                                                         Geo geo, Red red, FoldSrc fs) {
-    const double beta = rho * ((FOLD && fs.mbx) ? src_total_mailbox(pb, geo, fs) : src_total(pb, geo));
+    if constexpr (FOLD) {
+        if (fs.mbx) {
+            run_pass_prefetch<OpAxpy2Dot<NT>, 1>(
+                OpAxpy2Dot<NT>{r, rin, sv, yn, 0.0, geo.edge_slot, geo.n_loc, geo.g_lo, geo.g_hi}, geo, red, [&] {
+                    const double beta = rho * src_total_mailbox(pb, geo, fs);
+                    const double alpha = rho * slot_total(pa);
+                    return alpha - beta;
+                });
+            return;
+        }
+    }
+    const double beta = rho * src_total(pb, geo);
     const double alpha = rho * slot_total(pa);
     run_pass<OpAxpy2Dot<NT>, 1, FOLD>(
         OpAxpy2Dot<NT>{r, rin, sv, yn, alpha - beta, geo.edge_slot, geo.n_loc, geo.g_lo, geo.g_hi}, geo, red);
