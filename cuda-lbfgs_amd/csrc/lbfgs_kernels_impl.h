@@ -985,6 +985,9 @@ __device__ __forceinline__ void run_pass(const Op& op, const Geo& geo, const Red
 // xGMI hop runs under those loads instead of ahead of them. coef() is called by every thread (it
 // synchronises the workgroup). The rows are applied and accumulated in the same order as
 // run_pass, so the bits are the same.
+#ifndef LBK_FOLD_PREFETCH
+#define LBK_FOLD_PREFETCH 1  // A/B: 0 polls before any load, as round 3's first folded consumers
+#endif
 template <class Op, int K, class Coef>
 __device__ __forceinline__ void run_pass_prefetch(Op op, const Geo& geo, const Red& red, Coef coef) {
     const Seg s = seg_setup(geo);
@@ -992,7 +995,7 @@ __device__ __forceinline__ void run_pass_prefetch(Op op, const Geo& geo, const R
 #pragma unroll
     for (int k = 0; k < K; ++k) acc[k] = 0.0;
     constexpr int U = op_unroll<Op>::value;
-    if (s.len == geo.L && s.nrows >= U) {
+    if (LBK_FOLD_PREFETCH && s.len == geo.L && s.nrows >= U) {
         typename Op::Row r[U];
         load_group<U, K>(op, s, 0, r);
         op.set_coef(coef());
@@ -2634,6 +2637,7 @@ struct lbk_ctx {
     unsigned xf_epoch;
     int xf_edges;          // ... whose producer also pushed its rank edges
     int xf_taken;          // the launch in progress consumes it (src_total polls the mailbox)
+    int xf_gate_err;       // a shared-GPU gate launch (take_fold) failed: the next launch reports it
     unsigned long long* fold_wait;  // profiling: ticks the consumers' workgroup 0 waited (device)
     void* xfer_pool;       // staged whole-vector transfers (LBFGS_XFER=staged), lazily
     int fold_now;          // the launch in progress pushes its reduction (epoch fold_epoch)
@@ -2918,6 +2922,21 @@ void fold_producer(lbk_ctx* c, Red& r, bool edges) {
 FoldSrc take_fold(lbk_ctx* c, int ref) {
     FoldSrc f{nullptr, 0u, nullptr, 0ull, nullptr};
     if (c->xf_slot < 0 || ref % LBK_KMAX != 0 || c->xf_slot != ref / LBK_KMAX) return f;
+    if (c->xf.shared_device) {
+        // ranks sharing one GPU (forced fold: tests, rehearsals): a consuming pass's workgroups
+        // polling in its prologue can hold every CU a peer's producing pass waits for. A
+        // one-wavefront gate (the collect kernel) waits first, so the pass launches with the
+        // values already in the mailbox and its prologue's poll is the same code, satisfied at once.
+        hipEvent_t a = nullptr, b = nullptr;
+        if (c->prof_on && (a = ev_get(c)) && (b = ev_get(c))) (void)hipEventRecord(a, c->stream);
+        if (lbk_xgmi_collect(c->xg, c->stream, slot_base(c, c->xf_slot), slot_stride(c->xf_slot), c->geo.g_lo,
+                             c->geo.g_hi, c->xf_epoch, 0) != 0)
+            c->xf_gate_err = 1;
+        if (a && b) {
+            (void)hipEventRecord(b, c->stream);
+            c->pending.push_back({LBK_K_EXCHANGE, a, b, 0.0});
+        }
+    }
     f.mbx = c->xf.own + (size_t)(c->xf_epoch & 1u) * (size_t)c->xf.positions * 2;
     f.mepoch = c->xf_epoch;
     f.merr = c->xf.err;
@@ -2950,6 +2969,10 @@ const double* take_pending(lbk_ctx* c, int ref) {
 template <class F>
 int launch(lbk_ctx* c, int kind, double vec_passes, int slot, F&& fn, int K = 1, bool exchange = true,
            const Geo* gv = nullptr) {
+    if (c->xf_gate_err) {
+        snprintf(c->err, sizeof c->err, "xgmi gate launch failed");
+        return -3;
+    }
     if (c->xf_slot >= 0 && !c->xf_taken) {
         const int rc = flush_fold(c);
         if (rc) return rc;
