@@ -37,6 +37,7 @@
 struct Vecs {
     const double* in[MAXV];
     double* out[MAXV];
+    const double* pair;  // IL > 0: inputs 1 and 2 share this buffer, alternating blocks of IL rows
 };
 
 typedef double dvec2 __attribute__((ext_vector_type(2)));
@@ -55,30 +56,42 @@ __device__ __forceinline__ void st(double* p, dvec2 v) {
 
 // LNT / SNT: nt loads / stores; the first TWL inputs and the first TWS outputs (the "work"
 // vectors q / r / d of the product) keep the default policy; INPL: output 0 is input 0 (in place,
-// as the two-loop's q)
-template <int NR, int NW, int U, bool LNT, bool SNT, int TWL, int TWS, bool INPL>
+// as the two-loop's q); IL > 0: inputs 1 and 2 (the two-loop's s_i and y_{i+1}) are one stream,
+// blocks of IL rows of 128 elements alternating between them
+// RUN: wave w takes the contiguous rows [w R, (w + 1) R), R = ceil(rows / 4) (the vector-free
+// commit's ORC_CANON_VF walk) instead of rows 4u + w
+template <int NR, int NW, int U, bool LNT, bool SNT, int TWL, int TWS, bool INPL, int IL = 0, bool RUN = false>
 __global__ __launch_bounds__(256) void k_mix(Vecs v, int64_t n, int64_t L, int rev, double* sink) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int64_t seg = rev ? (int64_t)gridDim.x - 1 - blockIdx.x : blockIdx.x;
-    const int64_t sbeg = seg * L;
-    const int64_t len = min(L, n - sbeg);
+    const int64_t sbeg0 = seg * L;
+    const int64_t len = min(L, n - sbeg0);
     const int nrows = (int)(len / 128);
-    const int myrows = nrows > w ? (nrows - w + 3) / 4 : 0;
+    const int R = (nrows + 3) / 4;
+    const int myrows = RUN ? max(0, min(R, nrows - w * R)) : (nrows > w ? (nrows - w + 3) / 4 : 0);
+    const int64_t sbeg = sbeg0;
     double acc = 0.0;
     for (int u0 = 0; u0 < myrows; u0 += U) {
         dvec2 a[U][NR];
 #pragma unroll
         for (int j = 0; j < U; ++j) {
             if (u0 + j >= myrows) break;
-            const int64_t off = sbeg + (int64_t)(4 * (u0 + j) + w) * 128 + 2 * lane;
+            const int64_t off = sbeg + (RUN ? (int64_t)(w * R + u0 + j) : (int64_t)(4 * (u0 + j) + w)) * 128 + 2 * lane;
 #pragma unroll
-            for (int k = 0; k < NR; ++k)
-                a[j][k] = (k < TWL) ? ld<false>(v.in[k] + off) : ld<LNT>(v.in[k] + off);
+            for (int k = 0; k < NR; ++k) {
+                if (IL > 0 && (k == 1 || k == 2)) {
+                    const int64_t grow = off / 128;
+                    const int64_t ioff = ((grow / IL) * 2 * IL + (k - 1) * IL + grow % IL) * 128 + 2 * lane;
+                    a[j][k] = ld<LNT>(v.pair + ioff);
+                } else {
+                    a[j][k] = (k < TWL) ? ld<false>(v.in[k] + off) : ld<LNT>(v.in[k] + off);
+                }
+            }
         }
 #pragma unroll
         for (int j = 0; j < U; ++j) {
             if (u0 + j >= myrows) break;
-            const int64_t off = sbeg + (int64_t)(4 * (u0 + j) + w) * 128 + 2 * lane;
+            const int64_t off = sbeg + (RUN ? (int64_t)(w * R + u0 + j) : (int64_t)(4 * (u0 + j) + w)) * 128 + 2 * lane;
             dvec2 s = a[j][0];
 #pragma unroll
             for (int k = 1; k < NR; ++k) s = s + a[j][k];
@@ -104,10 +117,13 @@ struct Case {
     bool alt;
 };
 
-template <int NR, int NW, int U, bool LNT, bool SNT, int TWL, int TWS, bool INPL>
+// LDSK > 0: LDSK KiB of dynamic LDS per workgroup (caps the workgroups per CU: 60 KiB -> 2, the
+// vector-free commit's occupancy of 2 waves per SIMD)
+template <int NR, int NW, int U, bool LNT, bool SNT, int TWL, int TWS, bool INPL, int IL = 0, bool RUN = false,
+          int LDSK = 0>
 void launch(Vecs v, int64_t n, int64_t L, int nseg, int rev, double* sink) {
-    hipLaunchKernelGGL((k_mix<NR, NW, U, LNT, SNT, TWL, TWS, INPL>), dim3(nseg), dim3(256), 0, 0, v, n, L, rev,
-                       sink);
+    hipLaunchKernelGGL((k_mix<NR, NW, U, LNT, SNT, TWL, TWS, INPL, IL, RUN>), dim3(nseg), dim3(256), LDSK * 1024, 0, v,
+                       n, L, rev, sink);
 }
 
 int main(int argc, char** argv) {
@@ -125,7 +141,11 @@ int main(int argc, char** argv) {
     }
     double* sink;
     CK(hipMalloc(&sink, 64));
+    double* pair;
+    CK(hipMalloc(&pair, sizeof(double) * 2 * npad));
+    CK(hipMemset(pair, 0, sizeof(double) * 2 * npad));
     Vecs v;
+    v.pair = pair;
     for (int k = 0; k < MAXV; ++k) v.in[k] = bufs[k];
     for (int k = 0; k < MAXV; ++k) v.out[k] = bufs[MAXV + 3 - (k % 4)];  // outputs disjoint from the inputs (NW <= 4)
     // names: <R>r<W>w_u<U>_<load policy><store policy>  (nt / df = default); "work" operands as the
@@ -157,6 +177,22 @@ int main(int argc, char** argv) {
         {"mid_2r1w_u8_alt", 2, 1, launch<2, 1, 8, true, true, 1, 1, false>, true},
         {"axpy_3r1w_u4_alt", 3, 1, launch<3, 1, 4, true, true, 1, 1, true>, true},
         {"commit_4r4w_u4_alt", 4, 4, launch<4, 4, 4, true, true, 1, 0, false>, true},
+        // s_i / y_{i+1} interleaved in one buffer (blocks of 1, 4, 16, 96 rows), q in place
+        {"axpy_3r1w_u4_il1", 3, 1, launch<3, 1, 4, true, true, 1, 1, true, 1>, false},
+        {"axpy_3r1w_u4_il4", 3, 1, launch<3, 1, 4, true, true, 1, 1, true, 4>, false},
+        {"axpy_3r1w_u4_il16", 3, 1, launch<3, 1, 4, true, true, 1, 1, true, 16>, false},
+        {"axpy_3r1w_u4_il96", 3, 1, launch<3, 1, 4, true, true, 1, 1, true, 96>, false},
+        {"axpy_3r1w_u4_il1_alt", 3, 1, launch<3, 1, 4, true, true, 1, 1, true, 1>, true},
+        {"axpy_3r1w_u4_il4_alt", 3, 1, launch<3, 1, 4, true, true, 1, 1, true, 4>, true},
+        {"axpy_3r1w_u4_il1_allnt", 3, 1, launch<3, 1, 4, true, true, 0, 0, true, 1>, false},
+        {"axpy_3r1w_u4_il4_allnt", 3, 1, launch<3, 1, 4, true, true, 0, 0, true, 4>, false},
+        // the vector-free commit's walk (contiguous run per wave) and occupancy (2 waves / SIMD)
+        {"vf_22r4w_u1_occ2", 22, 4, launch<22, 4, 1, true, true, 0, 0, false, 0, false, 60>, false},
+        {"vf_22r4w_u1_run", 22, 4, launch<22, 4, 1, true, true, 0, 0, false, 0, true>, false},
+        {"vf_22r4w_u1_run_occ2", 22, 4, launch<22, 4, 1, true, true, 0, 0, false, 0, true, 60>, false},
+        {"vf_22r4w_u2_occ2", 22, 4, launch<22, 4, 2, true, true, 0, 0, false, 0, false, 60>, false},
+        {"vf_22r4w_u2_run_occ2", 22, 4, launch<22, 4, 2, true, true, 0, 0, false, 0, true, 60>, false},
+        {"vf_22r4w_u1_occ1", 22, 4, launch<22, 4, 1, true, true, 0, 0, false, 0, false, 100>, false},
     };
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
@@ -182,5 +218,6 @@ int main(int argc, char** argv) {
     }
     for (auto b : bufs)
         if (b) CK(hipFree(b));
+    CK(hipFree(pair));
     return 0;
 }
