@@ -222,6 +222,15 @@ int lbk_small_iter(lbk_ctx* c, int obj, int h, const double* g, double* q, doubl
                    const double* const* Y, const double* rho, double gamma, int p0_ref, double a0, const double* x,
                    double* xn, double* gn, double* so, double* yo, int slot_p0, int slot_a0, int slot_b0,
                    int slot_c, double cand, const lbk_spec* spec, unsigned long long* epoch);
+/* Persistent two-loop (LBFGS_PERSIST=2, large n, one rank): the two-loop passes of
+ * lbk_small_iter (P0 dot unless p0_ref >= 0, axpy_dot into slot_a0 + i, mid into slot_b0,
+ * axpy2_dot into slot_b0 + i) in one launch of resident workgroups, the same slot contents and
+ * vectors as the launch sequence; the commit is the caller's next launch. lbk_twoloop_ok: the
+ * mode is on and its grid fits this n. */
+int lbk_twoloop_ok(const lbk_ctx* c, int h);
+int lbk_twoloop_persist(lbk_ctx* c, int h, const double* g, double* q, double* r, const double* const* S,
+                        const double* const* Y, const double* rho, double gamma, int p0_ref, int slot_p0,
+                        int slot_a0, int slot_b0);
 /* waits for launch `epoch` to finish its commit (spinning on a pinned word, no stream
  * synchronisation: a speculative launch queued behind it keeps running), then the fixed-order
  * totals of slot_c. *went (may be NULL): 0 if a speculative launch found a test failing (it wrote

@@ -1251,43 +1251,63 @@ static int iterate(lbfgs_ctx* c) {
             double rho[MMAX];
             for (int i = 0; i < h; ++i) rho[i] = 1.0 / c->sy[c->ring[i]];
             const int top = c->ring[h - 1];
-            if (c->sg_valid) {
-                refA[h - 1] = c->sg_ref; /* s_{h-1}.g from the previous commit */
+            if (!ext_obj(c) && c->geo->world == 1 && lbk_twoloop_ok(c->dev, h)) {
+                /* LBFGS_PERSIST=2: the passes below in one persistent launch, same slots */
+                const double* Sr[MMAX];
+                const double* Yr[MMAX];
+                for (int i = 0; i < h; ++i) {
+                    Sr[i] = c->S[c->ring[i]];
+                    Yr[i] = c->Y[c->ring[i]];
+                }
+                DEV(lbk_twoloop_persist(c->dev, h, c->g, c->q, c->r, Sr, Yr, rho, gamma, c->sg_valid ? c->sg_ref : -1,
+                                        SLOT_P0, SLOT_A0, SLOT_B0(m)));
+                refA[h - 1] = c->sg_valid ? c->sg_ref : REF(SLOT_P0, 0);
+                for (int i = h - 2; i >= 0; --i) refA[i] = REF(SLOT_A0 + i, 0);
+                for (int i = 0; i < h; ++i) refB[i] = REF(SLOT_B0(m) + i, 0);
+                c->rc = c->r;
+                c->rho_last = rho[h - 1];
+                c->ref_b_last = refB[h - 1];
+                c->ref_a_last = refA[h - 1];
+                c->s_last_pair = top;
             } else {
-                DEV(lbk_dot(c->dev, c->S[top], c->g, SLOT_P0));
-                refA[h - 1] = REF(SLOT_P0, 0);
+                if (c->sg_valid) {
+                    refA[h - 1] = c->sg_ref; /* s_{h-1}.g from the previous commit */
+                } else {
+                    DEV(lbk_dot(c->dev, c->S[top], c->g, SLOT_P0));
+                    refA[h - 1] = REF(SLOT_P0, 0);
+                }
+                /* q and r ping-pong between two buffers when c->pingpong: every pass writes a
+                 * different vector than it reads (same values; measured faster) */
+                const double* qsrc = c->g;
+                double* qb[2] = {c->q, c->pingpong ? c->q2 : c->q};
+                int qi = 0;
+                for (int i = h - 2; i >= 0; --i) {
+                    double* qout = qb[qi];
+                    qi ^= 1;
+                    DEV(lbk_axpy_dot(c->dev, qout, qsrc, c->Y[c->ring[i + 1]], c->S[c->ring[i]], rho[i + 1],
+                                     refA[i + 1], SLOT_A0 + i));
+                    refA[i] = REF(SLOT_A0 + i, 0);
+                    qsrc = qout;
+                }
+                DEV(lbk_mid(c->dev, c->r, qsrc, c->Y[c->ring[0]], rho[0], gamma, refA[0], SLOT_B0(m)));
+                refB[0] = REF(SLOT_B0(m), 0);
+                double* rb[2] = {c->r, c->pingpong ? c->r2 : c->r};
+                int ri = 1;
+                const double* rcur = c->r;
+                for (int i = 0; i + 1 < h; ++i) {
+                    double* rout = rb[ri];
+                    ri ^= 1;
+                    DEV(lbk_axpy2_dot(c->dev, rout, rcur, c->S[c->ring[i]], c->Y[c->ring[i + 1]], rho[i], refB[i],
+                                      refA[i], SLOT_B0(m) + i + 1));
+                    refB[i + 1] = REF(SLOT_B0(m) + i + 1, 0);
+                    rcur = rout;
+                }
+                c->rc = rcur;
+                c->rho_last = rho[h - 1];
+                c->ref_b_last = refB[h - 1];
+                c->ref_a_last = refA[h - 1];
+                c->s_last_pair = top;
             }
-            /* q and r ping-pong between two buffers when c->pingpong: every pass writes a
-             * different vector than it reads (same values; measured faster) */
-            const double* qsrc = c->g;
-            double* qb[2] = {c->q, c->pingpong ? c->q2 : c->q};
-            int qi = 0;
-            for (int i = h - 2; i >= 0; --i) {
-                double* qout = qb[qi];
-                qi ^= 1;
-                DEV(lbk_axpy_dot(c->dev, qout, qsrc, c->Y[c->ring[i + 1]], c->S[c->ring[i]], rho[i + 1],
-                                 refA[i + 1], SLOT_A0 + i));
-                refA[i] = REF(SLOT_A0 + i, 0);
-                qsrc = qout;
-            }
-            DEV(lbk_mid(c->dev, c->r, qsrc, c->Y[c->ring[0]], rho[0], gamma, refA[0], SLOT_B0(m)));
-            refB[0] = REF(SLOT_B0(m), 0);
-            double* rb[2] = {c->r, c->pingpong ? c->r2 : c->r};
-            int ri = 1;
-            const double* rcur = c->r;
-            for (int i = 0; i + 1 < h; ++i) {
-                double* rout = rb[ri];
-                ri ^= 1;
-                DEV(lbk_axpy2_dot(c->dev, rout, rcur, c->S[c->ring[i]], c->Y[c->ring[i + 1]], rho[i], refB[i],
-                                  refA[i], SLOT_B0(m) + i + 1));
-                refB[i + 1] = REF(SLOT_B0(m) + i + 1, 0);
-                rcur = rout;
-            }
-            c->rc = rcur;
-            c->rho_last = rho[h - 1];
-            c->ref_b_last = refB[h - 1];
-            c->ref_a_last = refA[h - 1];
-            c->s_last_pair = top;
         }
     }
     if (c->sp_pend && c->sp_k == k) { /* queued for this iteration, which took another path */

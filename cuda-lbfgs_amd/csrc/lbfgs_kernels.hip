@@ -219,10 +219,41 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
         po = std::min(po, o);
         CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, (k_persist_iter<LBK_OBJ_QUAD_SEPARABLE, true>), LB_BLOCK, 0));
         po = std::min(po, o);
-        c->persist_gmax = std::min(po, 4) * cus;
+        int cap = 4;  // workgroups per CU (A/B: LBFGS_PERSIST_WG)
+        if (const char* e = getenv("LBFGS_PERSIST_WG")) cap = std::max(1, atoi(e));
+        c->persist_gmax = std::min(po, cap) * cus;
+        // the persistent two-loop (LBFGS_PERSIST=2) without the commit's registers
+        CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, k_persist_twoloop<true>, LB_BLOCK, 0));
+        po = o;
+        CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, k_persist_twoloop<false>, LB_BLOCK, 0));
+        po = std::min(po, o);
+        c->persist2_gmax = std::min(po, cap) * cus;
+        // an LDS reservation that lets exactly `cap` workgroups onto a CU, so the dispatcher spreads
+        // the resident grid evenly (without it two workgroups can share a CU while another idles;
+        // A/B LBFGS_PERSIST_LDS=0)
+        c->persist_lds = 0;
+        int lds_on = 1;
+        if (const char* e = getenv("LBFGS_PERSIST_LDS")) lds_on = atoi(e) != 0;
+        if (lds_on) {
+            c->persist_lds = 160 * 1024 / (cap + 1) + 1024;
+            (void)hipFuncSetAttribute((const void*)k_persist_twoloop<true>, hipFuncAttributeMaxDynamicSharedMemorySize, c->persist_lds);
+            (void)hipFuncSetAttribute((const void*)k_persist_twoloop<false>, hipFuncAttributeMaxDynamicSharedMemorySize, c->persist_lds);
+#define PSET(O)                                                                                                        \
+    (void)hipFuncSetAttribute((const void*)k_persist_iter<O, true>, hipFuncAttributeMaxDynamicSharedMemorySize, c->persist_lds); \
+    (void)hipFuncSetAttribute((const void*)k_persist_iter<O, false>, hipFuncAttributeMaxDynamicSharedMemorySize, c->persist_lds)
+            PSET(LBK_OBJ_ROSENBROCK);
+            PSET(LBK_OBJ_QUAD_TRIDIAG);
+            PSET(LBK_OBJ_QUAD_SEPARABLE);
+#undef PSET
+            (void)hipGetLastError();
+        }
     }
     c->persist_on = 0;
-    if (const char* e = getenv("LBFGS_PERSIST")) c->persist_on = atoi(e) != 0;
+    if (const char* e = getenv("LBFGS_PERSIST")) c->persist_on = atoi(e);  // 1: whole iteration, 2: two-loop
+    c->persist_stride = 0;
+    if (const char* e = getenv("LBFGS_PERSIST_OWN")) c->persist_stride = strcmp(e, "stride") == 0;
+    c->persist_alt = 1;
+    if (const char* e = getenv("LBFGS_PERSIST_ALT")) c->persist_alt = atoi(e) != 0;
     CK(hipMalloc(&c->fold_wait, sizeof(unsigned long long)));
     CK(hipMemset(c->fold_wait, 0, sizeof(unsigned long long)));
     CK(hipMalloc(&c->persist_cnt, sizeof(unsigned long long) * LBK_GROUPS));
@@ -697,11 +728,64 @@ int lbk_elementwise(lbk_ctx* c, int op, double* out, const double* a, const doub
 // ---- vector-free mode -------------------------------------------------------------------
 // the persistent iteration's segments per workgroup (1..16, dividing a group's 1024) for this n,
 // or 0 when it is off or the grid would not be resident
-static int persist_fits(const lbk_ctx* c) {
-    if (!c->persist_on || c->geo.world != 1 || c->comm || !c->direct || c->geo.nseg <= c->coop_max) return 0;
-    for (int spw = 1; spw <= 16; spw *= 2)
-        if ((c->geo.nseg + spw - 1) / spw <= c->persist_gmax) return spw;
-    return 0;
+// the persistent forms' grid (resident workgroups, each owning every G-th segment) when `mode` is
+// on for this context, else 0
+static int persist_grid(const lbk_ctx* c, int mode, int gmax) {
+    if (c->persist_on != mode || c->geo.world != 1 || c->comm || !c->direct || c->geo.nseg <= c->coop_max) return 0;
+    return (int)std::min<int64_t>(gmax, c->geo.nseg);
+}
+static int persist_fits(const lbk_ctx* c) { return persist_grid(c, 1, c->persist_gmax); }
+
+int lbk_twoloop_ok(const lbk_ctx* c, int h) {
+    return h >= 1 && h <= LBK_SMALL_HMAX && persist_grid(c, 2, c->persist2_gmax) > 0;
+}
+
+int lbk_twoloop_persist(lbk_ctx* c, int h, const double* g, double* q, double* r, const double* const* S,
+                        const double* const* Y, const double* rho, double gamma, int p0_ref, int slot_p0,
+                        int slot_a0, int slot_b0) {
+    const int nb = lbk_twoloop_ok(c, h) ? persist_grid(c, 2, c->persist2_gmax) : 0;
+    if (!nb) return -1;
+    SmallArgs a;
+    memset(&a, 0, sizeof a);
+    a.h = h;
+    a.p0_from_slot = p0_ref >= 0;
+    a.p0_slot = p0_ref >= 0 ? sref(c, p0_ref) : nullptr;
+    a.g = g;
+    a.q = q;
+    a.r = r;
+    for (int i = 0; i < h; ++i) {
+        a.S[i] = S[i];
+        a.Y[i] = Y[i];
+        a.rho[i] = rho[i];
+    }
+    a.gamma = gamma;
+    a.slots = c->slots;
+    // written by block 0 of the launch, read on the device by the next passes / the commit
+    c->slot_mirror[slot_p0] = 0;
+    c->slot_s2[slot_p0] = 0;
+    for (int i = 0; i < h; ++i) {
+        c->slot_mirror[slot_a0 + i] = c->slot_mirror[slot_b0 + i] = 0;
+        c->slot_s2[slot_a0 + i] = c->slot_s2[slot_b0 + i] = 0;
+    }
+    a.slot_p0 = slot_p0;
+    a.slot_a0 = slot_a0;
+    a.slot_b0 = slot_b0;
+    a.ll = c->coop_ll;
+    a.seq_base = (unsigned)c->coop_base;
+    a.err = c->coop_err_d;
+    a.timeout = (unsigned long long)(2.0 * c->wall_khz * 1e3);  // 2 s: a grid that is not resident ends
+    a.partials = c->partials;
+    a.pcnt = c->persist_cnt;
+    a.gflag = c->persist_gflag;
+    a.spw = c->persist_stride ? 0 : (c->geo.nseg + nb - 1) / nb;
+    a.alt = c->persist_alt;
+    c->coop_base += (unsigned long long)((p0_ref >= 0 ? 0 : 1) + 2 * h - 1);
+    Geo geo = kgeo(c);
+    geo.rev = 0;
+    const double vec = (p0_ref >= 0 ? 0.0 : 2.0) + 4.0 * (h - 1) + 3.0 + 4.0 * (h - 1);
+    return launch(c, LBK_K_SMALL_ITER, vec, -1, [&] {
+        NT_DISPATCH(c, hipLaunchKernelGGL((k_persist_twoloop<NT_>), dim3(nb), dim3(LB_BLOCK), c->persist_lds, c->stream, a, geo));
+    });
 }
 
 int lbk_small_iter(lbk_ctx* c, int obj, int h, const double* g, double* q, double* r, const double* const* S,
@@ -784,16 +868,17 @@ int lbk_small_iter(lbk_ctx* c, int obj, int h, const double* g, double* q, doubl
         c->coop_base += (unsigned long long)passes;
         geo.rev = 0;
         if (persist) {
-            a.spw = persist;
             a.partials = c->partials;
             a.pcnt = c->persist_cnt;
             a.gflag = c->persist_gflag;
-            const int nb = (int)((c->geo.nseg + persist - 1) / persist);
+            const int nb = persist;
+            a.spw = c->persist_stride ? 0 : (c->geo.nseg + nb - 1) / nb;
+            a.alt = c->persist_alt;
             return launch(c, LBK_K_SMALL_ITER, vec, -1, [&] {
                 NT_DISPATCH(c, switch (obj) {
-                    case LBK_OBJ_ROSENBROCK: hipLaunchKernelGGL((k_persist_iter<LBK_OBJ_ROSENBROCK, NT_>), dim3(nb), dim3(LB_BLOCK), 0, c->stream, a, geo); break;
-                    case LBK_OBJ_QUAD_TRIDIAG: hipLaunchKernelGGL((k_persist_iter<LBK_OBJ_QUAD_TRIDIAG, NT_>), dim3(nb), dim3(LB_BLOCK), 0, c->stream, a, geo); break;
-                    default: hipLaunchKernelGGL((k_persist_iter<LBK_OBJ_QUAD_SEPARABLE, NT_>), dim3(nb), dim3(LB_BLOCK), 0, c->stream, a, geo); break;
+                    case LBK_OBJ_ROSENBROCK: hipLaunchKernelGGL((k_persist_iter<LBK_OBJ_ROSENBROCK, NT_>), dim3(nb), dim3(LB_BLOCK), c->persist_lds, c->stream, a, geo); break;
+                    case LBK_OBJ_QUAD_TRIDIAG: hipLaunchKernelGGL((k_persist_iter<LBK_OBJ_QUAD_TRIDIAG, NT_>), dim3(nb), dim3(LB_BLOCK), c->persist_lds, c->stream, a, geo); break;
+                    default: hipLaunchKernelGGL((k_persist_iter<LBK_OBJ_QUAD_SEPARABLE, NT_>), dim3(nb), dim3(LB_BLOCK), c->persist_lds, c->stream, a, geo); break;
                 });
             });
         }

@@ -443,6 +443,16 @@ __global__ __launch_bounds__(LB_BLOCK) void k_group_reduce_wide(const double* __
     }
 }
 
+// A wait on a peer's mailbox word ends past `timeout` wall-clock ticks, or - once it has waited
+// 1/65536 of that (~1 ms of the default 60 s) - as soon as the pinned error word shows that an
+// earlier wait of this rank already timed out: a broken channel costs one timeout per solve, not
+// one per exchange queued before the host's next synchronisation.
+__device__ __forceinline__ bool peer_wait_over(unsigned long long t0, unsigned long long timeout, const unsigned* err) {
+    const unsigned long long el = wall_clock64() - t0;
+    if (el > timeout) return true;
+    return el > (timeout >> 16) && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u;
+}
+
 // Total of a launch's first source slot (the previous pass's reduction). Normally stage 2 ran
 // after the producer (k_group_reduce or tickets) and the slot holds the group values. With a
 // deferred stage 2 (geo.ppart, mid n on one rank) every workgroup of the consuming launch forms
@@ -469,7 +479,7 @@ __device__ __forceinline__ double src_total_mailbox(const double* slot, const Ge
                 a = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 b = __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 if ((unsigned)(a >> 32) == fs.mepoch && (unsigned)(b >> 32) == fs.mepoch) break;
-                if (wall_clock64() - t0 > fs.mtmo) {
+                if (peer_wait_over(t0, fs.mtmo, fs.merr)) {
                     __hip_atomic_store(fs.merr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     a = 0;
                     b = 0x7ff80000ull;  // quiet NaN
@@ -1907,10 +1917,12 @@ struct SmallArgs {
     unsigned long long* vd;             // device verdict word of this launch ((epoch << 1) | went)
     const unsigned long long* chain;    // the previous speculative launch's verdict word, or nullptr
     unsigned long long chain_want;
-    // persistent form (k_persist_iter) only: segments per workgroup, the canonical stage 2's
-    // partials and per-group arrival counters (monotonic over passes), the group values as
-    // flagged words [pass parity][component][group][2]
-    int spw;
+    // persistent forms (k_persist_iter, k_persist_twoloop) only: segments per workgroup (chunks;
+    // 0: strided ownership), alternate the walk direction by pass, the canonical stage 2's
+    // partials and per-group arrival counters (segments, monotonic over passes), the group values
+    // as flagged words [pass parity][component][group][2]
+    int64_t spw;
+    int alt;
     double* partials;
     unsigned long long* pcnt;
     unsigned long long* gflag;
@@ -2274,40 +2286,54 @@ __global__ __launch_bounds__(LB_BLOCK) void k_coop_iter(SmallArgs a, Geo geo) {
 #undef SL
 
 // ---------------------------------------------------------------------------------------
-// Persistent iteration for large n (LBFGS_PERSIST=1; VERDICT r02 item 8, SURVEY §7 step 5 at
-// configs[2]'s size): the cooperative iteration above with one resident grid of G workgroups
-// instead of one workgroup per segment. Workgroup b walks the contiguous canonical segments
-// [b spw, (b+1) spw) of every pass (spw | 1024, so they lie in one group) exactly as the pass
-// kernels do, storing each segment partial write-through; then one agent-scope ticket per
-// workgroup on its group's counter (monotonic: the last arriver of pass seq sees
-// seq * workgroups-in-group), and the group's last arriver forms the canonical stage-2 tree
-// (group_tree, the same bits as k_group_reduce) and publishes the group values as flagged words.
-// Every workgroup then waits for the 8 group words of each component and forms the fixed-order
-// total. One launch per iteration: the pass boundaries and stage-2 launches of the launch
-// sequence become one ticket round trip plus one flagged hop per pass.
+// Persistent forms for large n (LBFGS_PERSIST=1: the whole iteration, k_persist_iter;
+// LBFGS_PERSIST=2: the two-loop, k_persist_twoloop; VERDICT r02 item 8, the north star's
+// "persistent-block fused two-loop" at configs[2]'s size): one resident grid of G workgroups
+// instead of one workgroup per segment. Workgroup b owns a contiguous chunk of spw canonical
+// segments of every vector (LBFGS_PERSIST_OWN=stride: the segments b, b + G, b + 2G, ..., so the
+// live segments form one window as in the launch sequence; measured slower) and walks them in
+// every pass exactly as the pass kernels walk one segment (the same waves the same rows), storing
+// each segment partial write-through; a workgroup only ever reads back rows it wrote itself.
+// Passes with odd sequence numbers walk the owned segments last to first, so a workgroup starts
+// on the segment it touched last, still in the Infinity Cache (the LBFGS_REV effect; A/B
+// LBFGS_PERSIST_ALT=0). After its segments, thread g < 8 of the workgroup adds its
+// segment count in group g to the group's agent-scope counter (monotonic: after pass seq it
+// holds seq * segments-in-group); the arrival that completes a group forms its canonical stage-2
+// tree (group_tree, the same bits as k_group_reduce) and publishes the group values as flagged
+// words. Every workgroup then waits for the 8 group words of each component and forms the
+// fixed-order total. The pass boundaries and stage-2 launches of the launch sequence become one
+// counter round trip plus one flagged hop per pass.
 // ---------------------------------------------------------------------------------------
+__device__ __forceinline__ int64_t ceil_pos(int64_t x, int64_t y) { return x <= 0 ? 0 : (x + y - 1) / y; }
+
 template <int K, bool HALO, class Op>
 __device__ __forceinline__ void persist_pass(const Op& op, const Geo& geo, const SmallArgs& a, int pass, double* slot,
                                              double* hslot, const double* rvec, double (&tot)[K],
-                                             double (&lds)[4][8], double (&gv)[8][8], int& last_flag) {
+                                             double (&lds)[4][8], double (&gv)[8][8], int (&last)[8]) {
     static_assert(K + 2 <= LBK_LL_COMPS && K <= 8, "flagged components");
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    const int64_t s0 = (int64_t)blockIdx.x * a.spw, s1 = min(s0 + a.spw, geo.nseg);
+    const int64_t G = gridDim.x, b = blockIdx.x;
+    // owned segments: chunk [c0, c0 + cnt) (a.spw > 0), or b, b + G, ... (a.spw == 0)
+    const int64_t c0 = a.spw > 0 ? min(geo.nseg, b * a.spw) : 0;
+    const int64_t cnt = a.spw > 0 ? min(geo.nseg, c0 + a.spw) - c0 : (b < geo.nseg ? (geo.nseg - 1 - b) / G + 1 : 0);
     const unsigned seq = a.seq_base + (unsigned)pass + 1u;
+    const bool down = (seq & 1u) != 0 && a.alt;
     unsigned long long* P = a.ll + (size_t)(pass & 1) * LBK_LL_COMPS * LBK_LL_SEGS * 2;
-    for (int64_t sidx = s0; sidx < s1; ++sidx) {
+    for (int64_t k = 0; k < cnt; ++k) {
+        const int64_t kk = down ? cnt - 1 - k : k;
+        const int64_t sidx = a.spw > 0 ? c0 + kk : b + kk * G;
         const Seg s = seg_at(geo, sidx, t);
         double acc[K];
 #pragma unroll
-        for (int k = 0; k < K; ++k) acc[k] = 0.0;
+        for (int k2 = 0; k2 < K; ++k2) acc[k2] = 0.0;
         if constexpr (HALO)
             stream_halo(op, s, geo, acc);
         else
             stream(op, s, geo, acc);
 #pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const double v = wave_sum(acc[k]);
-            if (lane == 0) lds[w][k] = v;
+        for (int k2 = 0; k2 < K; ++k2) {
+            const double v = wave_sum(acc[k2]);
+            if (lane == 0) lds[w][k2] = v;
         }
         // this segment's vector stores are read by other waves of the workgroup (its edge r below,
         // the next pass)
@@ -2316,9 +2342,9 @@ __device__ __forceinline__ void persist_pass(const Op& op, const Geo& geo, const
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         if (t == 0) {
 #pragma unroll
-            for (int k = 0; k < K; ++k)
-                __hip_atomic_store(reinterpret_cast<unsigned long long*>(a.partials + (int64_t)k * LBK_SEGS + sidx),
-                                   dbits((lds[0][k] + lds[1][k]) + (lds[2][k] + lds[3][k])), __ATOMIC_RELAXED,
+            for (int k2 = 0; k2 < K; ++k2)
+                __hip_atomic_store(reinterpret_cast<unsigned long long*>(a.partials + (int64_t)k2 * LBK_SEGS + sidx),
+                                   dbits((lds[0][k2] + lds[1][k2]) + (lds[2][k2] + lds[3][k2])), __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
             if (rvec) {  // the segment's first / last r for the commit's halo across segments
                 ll_store(P + ((int64_t)K * LBK_LL_SEGS + sidx) * 2, rvec[s.lb], seq);
@@ -2327,17 +2353,25 @@ __device__ __forceinline__ void persist_pass(const Op& op, const Geo& geo, const
         }
         __syncthreads();  // lds reuse
     }
-    const int g = (int)(s0 / LBK_SEG_PER_GROUP);
-    if (t == 0) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const int64_t gend = min(geo.nseg, (int64_t)(g + 1) * LBK_SEG_PER_GROUP);
-        const unsigned long long nwg = (unsigned long long)((gend - (int64_t)g * LBK_SEG_PER_GROUP + a.spw - 1) / a.spw);
-        const unsigned long long old =
-            __hip_atomic_fetch_add(a.pcnt + g, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        last_flag = (old + 1ull == (unsigned long long)seq * nwg);
+    // wave 0 stored the partials: drained before its counter adds
+    if (t < 64) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (t < LBK_GROUPS) {
+        const int64_t glo = (int64_t)t * LBK_SEG_PER_GROUP, ghi = min(geo.nseg, glo + LBK_SEG_PER_GROUP);
+        const int64_t c = ghi <= glo       ? 0
+                          : a.spw > 0      ? max((int64_t)0, min(c0 + cnt, ghi) - max(c0, glo))
+                                           : ceil_pos(ghi - b, G) - ceil_pos(glo - b, G);
+        int fl = 0;
+        if (c > 0) {
+            const unsigned long long old =
+                __hip_atomic_fetch_add(a.pcnt + t, (unsigned long long)c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            fl = old + (unsigned long long)c == (unsigned long long)seq * (unsigned long long)(ghi - glo);
+        }
+        last[t] = fl;
     }
     __syncthreads();
-    if (last_flag) {  // stage 2 of group g, then its values as flagged words
+    for (int g = 0; g < LBK_GROUPS; ++g) {
+        if (!last[g]) continue;  // uniform: shared
+        // stage 2 of group g, then its values as flagged words
         __shared__ double glds[4][K];
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         double* sg = slot + g * LBK_KMAX;
@@ -2352,9 +2386,9 @@ __device__ __forceinline__ void persist_pass(const Op& op, const Geo& geo, const
     // fixed-order total of slot_total()
     const int ng = (int)((geo.nseg + LBK_SEG_PER_GROUP - 1) / LBK_SEG_PER_GROUP);
     if (t < K * 8) {
-        const int k = t >> 3, gg = t & 7;
-        gv[k][gg] = gg < ng ? ll_load(a.gflag + ((size_t)((pass & 1) * 8 + k) * 8 + gg) * 2, seq, a.err, a.timeout)
-                            : 0.0;
+        const int k2 = t >> 3, gg = t & 7;
+        gv[k2][gg] = gg < ng ? ll_load(a.gflag + ((size_t)((pass & 1) * 8 + k2) * 8 + gg) * 2, seq, a.err, a.timeout)
+                             : 0.0;
     }
     __syncthreads();
     if (t < K) {
@@ -2372,17 +2406,22 @@ __device__ __forceinline__ void persist_pass(const Op& op, const Geo& geo, const
     }
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < K; ++k) tot[k] = lds[0][k];
+    for (int k2 = 0; k2 < K; ++k2) tot[k2] = lds[0][k2];
     __syncthreads();  // lds / gv reuse by the next pass
 }
 
+// the persistent passes stream k_mid's pass in op_unroll's default 4-row groups: the launch form's
+// 8-row groups would set the whole persistent kernel's register budget
+template <bool NT>
+struct OpMid4 : OpMid<NT> {};
+
 #define SL(sl) (a.slots + (int64_t)(sl) * LBK_SLOT)
-template <int OBJ, bool NT>
-__global__ __launch_bounds__(LB_BLOCK) void k_persist_iter(SmallArgs a, Geo geo) {
-    __shared__ double lds[4][8];
-    __shared__ double gv[8][8];
-    __shared__ double TA[LBK_SMALL_HMAX], TB[LBK_SMALL_HMAX];
-    __shared__ int last_flag;
+// The two-loop recursion of k_persist_iter (passes P0, the h - 1 first-loop passes, mid and the
+// h - 1 second-loop passes); EDGES: the r passes also publish the segments' edge r for an
+// in-launch commit. Returns the number of passes run; TA / TB hold the two loops' dots.
+template <bool NT, bool EDGES>
+__device__ __forceinline__ int persist_twoloop(const SmallArgs& a, const Geo& geo, double (&lds)[4][8],
+                                               double (&gv)[8][8], double* TA, double* TB, int (&last_flag)[8]) {
     const int h = a.h;
     int pass = 0;
     double t1[1];
@@ -2402,18 +2441,31 @@ __global__ __launch_bounds__(LB_BLOCK) void k_persist_iter(SmallArgs a, Geo geo)
         alpha = a.rho[i] * t1[0];
         qsrc = a.q;
     }
-    persist_pass<1, false>(OpMid<NT>{a.r, qsrc, a.Y[0], alpha, gamma}, geo, a, pass++, SL(a.slot_b0), nullptr,
-                           h == 1 ? a.r : nullptr, t1, lds, gv, last_flag);
+    persist_pass<1, false>(OpMid4<NT>{{a.r, qsrc, a.Y[0], alpha, gamma}}, geo, a, pass++, SL(a.slot_b0), nullptr,
+                           EDGES && h == 1 ? a.r : nullptr, t1, lds, gv, last_flag);
     if (threadIdx.x == 0) TB[0] = t1[0];
     __syncthreads();
     for (int i = 0; i + 1 < h; ++i) {  // r += s_i (alpha_i - beta_i);  y_{i+1} . r
         const double beta = a.rho[i] * TB[i];
         const double alph = a.rho[i] * TA[i];
         persist_pass<1, false>(OpAxpy2Dot<NT>{a.r, a.r, a.S[i], a.Y[i + 1], alph - beta}, geo, a, pass++,
-                               SL(a.slot_b0 + i + 1), nullptr, i + 2 == h ? a.r : nullptr, t1, lds, gv, last_flag);
+                               SL(a.slot_b0 + i + 1), nullptr, EDGES && i + 2 == h ? a.r : nullptr, t1, lds, gv,
+                               last_flag);
         if (threadIdx.x == 0) TB[i + 1] = t1[0];
         __syncthreads();
     }
+    return pass;
+}
+
+template <int OBJ, bool NT>
+__global__ __launch_bounds__(LB_BLOCK) void k_persist_iter(SmallArgs a, Geo geo) {
+    __shared__ double lds[4][8];
+    __shared__ double gv[8][8];
+    __shared__ double TA[LBK_SMALL_HMAX], TB[LBK_SMALL_HMAX];
+    __shared__ int last_flag[8];
+    const int h = a.h;
+    const double rho_top = a.rho[h - 1], gamma = a.gamma;
+    int pass = persist_twoloop<NT, true>(a, geo, lds, gv, TA, TB, last_flag);
     const int rp = pass - 1;
     DirArgs da = {a.r, a.S[h - 1], a.g, 0.0, nullptr, nullptr, rho_top, nullptr, geo.g_lo, geo.g_hi,
                   a.ll + (size_t)(rp & 1) * LBK_LL_COMPS * LBK_LL_SEGS * 2, geo.L, a.seq_base + (unsigned)rp + 1u, a.err,
@@ -2428,6 +2480,26 @@ __global__ __launch_bounds__(LB_BLOCK) void k_persist_iter(SmallArgs a, Geo geo)
                                                                        geo.n_loc, a.cand},
                           geo, a, pass++, SL(a.slot_c), HS(a.slot_c), nullptr, t8, lds, gv, last_flag);
     coop_publish(a, 1, rho_top, gamma);
+}
+
+// The persistent two-loop alone (LBFGS_PERSIST=2; the north star's "persistent-block fused
+// two-loop"): one resident grid runs all 2h (or 2h - 1) two-loop passes of an iteration, the
+// m-deep s/y ring streamed by the same workgroups pass after pass, with the in-launch stage 2 of
+// persist_pass; the commit follows as its own launch and reads the passes' slots as after the
+// launch sequence. Without the commit's registers (162 VGPRs, 3 waves per SIMD) the grid keeps the
+// two-loop passes' occupancy. Every workgroup reads only the rows it wrote itself in an earlier
+// pass (same segments, same waves), so no vector data crosses workgroups inside the launch.
+#ifndef LBK_PERSIST2_WAVES
+#define LBK_PERSIST2_WAVES 4  // waves per SIMD the register allocation must allow
+#endif
+template <bool NT>
+__global__ __launch_bounds__(LB_BLOCK) __attribute__((amdgpu_waves_per_eu(LBK_PERSIST2_WAVES)))
+void k_persist_twoloop(SmallArgs a, Geo geo) {
+    __shared__ double lds[4][8];
+    __shared__ double gv[8][8];
+    __shared__ double TA[LBK_SMALL_HMAX], TB[LBK_SMALL_HMAX];
+    __shared__ int last_flag[8];
+    (void)persist_twoloop<NT, false>(a, geo, lds, gv, TA, TB, last_flag);
 }
 #undef SL
 
@@ -2604,7 +2676,7 @@ struct lbk_ctx {
     int coop_max;
     // persistent iteration for large n (LBFGS_PERSIST=1, opt-in A/B): resident workgroups, their
     // segments per pass, stage-2 counters and flagged group values
-    int persist_on, persist_gmax;
+    int persist_on, persist_gmax, persist2_gmax, persist_stride, persist_alt, persist_lds;
     unsigned long long *persist_cnt, *persist_gflag;
     unsigned long long coop_ll_bytes;
     unsigned long long* coop_ll;   // flagged partials (SmallArgs::ll)

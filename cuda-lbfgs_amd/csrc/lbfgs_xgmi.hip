@@ -40,6 +40,14 @@ struct lbk_xgmi {
 
 namespace {
 
+// a wait ends past `timeout` ticks, or after 1/65536 of it once the pinned error word shows an
+// earlier timeout of this rank (one timeout per solve on a broken channel, not one per exchange)
+__device__ __forceinline__ bool wait_over(unsigned long long t0, unsigned long long timeout, const unsigned* err) {
+    const unsigned long long el = wall_clock64() - t0;
+    if (el > timeout) return true;
+    return el > (timeout >> 16) && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u;
+}
+
 // One workgroup. Push: own positions [lo, hi) to every peer's mailbox (two LL words per 64-bit
 // value). Poll: every other position of the own mailbox until both of its words carry this
 // epoch, then write the value into the slot. A peer that never arrives ends the wait after
@@ -73,7 +81,7 @@ __global__ __launch_bounds__(256) void k_xgmi_exchange(unsigned long long* __res
             a = __hip_atomic_load(mine + 2 * (size_t)j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             b = __hip_atomic_load(mine + 2 * (size_t)j + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             if ((unsigned)(a >> 32) == epoch && (unsigned)(b >> 32) == epoch) break;
-            if (wall_clock64() - t0 > timeout) {
+            if (wait_over(t0, timeout, err)) {
                 __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 a = 0;
                 b = 0x7ff80000ull;  // quiet NaN
@@ -108,7 +116,7 @@ __global__ __launch_bounds__(64) void k_xgmi_collect(unsigned long long* __restr
         a = __hip_atomic_load(mine + 2 * (size_t)pos, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         b = __hip_atomic_load(mine + 2 * (size_t)pos + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         if ((unsigned)(a >> 32) == epoch && (unsigned)(b >> 32) == epoch) break;
-        if (wall_clock64() - t0 > timeout) {
+        if (wait_over(t0, timeout, err)) {
             __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             a = 0;
             b = 0x7ff80000ull;

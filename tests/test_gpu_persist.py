@@ -1,7 +1,9 @@
-"""The persistent large-n iteration (LBFGS_PERSIST=1, k_persist_iter): one
-resident grid walks every canonical segment of every pass of the iteration, with the stage 2 of
-each pass in the launch. Same per-segment arithmetic, same group trees, same fixed-order totals:
-its trajectories must be the launch sequence's bit for bit (and so the canonical oracle's)."""
+"""The persistent large-n forms: LBFGS_PERSIST=1 (k_persist_iter) runs the
+whole iteration in one launch, LBFGS_PERSIST=2 (k_persist_twoloop, the north star's persistent
+two-loop) the two-loop passes in one launch with the commit after it. One resident grid walks every
+canonical segment of every pass, with the stage 2 of each pass in the launch. Same per-segment
+arithmetic, same group trees, same fixed-order totals: their trajectories must be the launch
+sequence's bit for bit (and so the canonical oracle's)."""
 import os
 import sys
 
@@ -29,17 +31,18 @@ def same(a, b):
     assert a["messages"] == b["messages"] and a["status"] == b["status"] and a["iterations"] == b["iterations"]
 
 
+@pytest.mark.parametrize("mode", ["1", "2"])
 @pytest.mark.parametrize("n,m,obj,ls,iters", [
     (3_000_000, 10, "rosenbrock", "backtracking", 16),     # 5860 segments of 512: tail group, 8 per workgroup
     (10_000_003, 10, "rosenbrock", "backtracking", 14),    # L = 1280, a short last segment
     (2_500_000, 7, "quad_tridiag", "wolfe", 12),           # rejected first trials: trial passes + recommits
     (1_200_000, 5, "rosenbrock", "interpolation", 20),     # 2048-element segments (mid-n rule)
 ])
-def test_persistent_iteration_bit_exact(monkeypatch, n, m, obj, ls, iters):
+def test_persistent_iteration_bit_exact(monkeypatch, mode, n, m, obj, ls, iters):
     x0 = L.x0_uniform(n, 5, -2.0, 2.0)
     with L.Context(n, m) as c:
         ref = c.minimize(obj, x0, ls, iters, trace=True)
-    monkeypatch.setenv("LBFGS_PERSIST", "1")
+    monkeypatch.setenv("LBFGS_PERSIST", mode)
     with L.Context(n, m) as c:
         c.prof_reset()
         c.prof_enable(True)
@@ -50,10 +53,11 @@ def test_persistent_iteration_bit_exact(monkeypatch, n, m, obj, ls, iters):
     assert launches >= 1  # the persistent kernel ran (one launch per iteration with h >= 1)
 
 
-def test_persistent_iteration_vs_oracle():
+@pytest.mark.parametrize("mode", ["1", "2"])
+def test_persistent_iteration_vs_oracle(mode):
     """n = 3e6 through the persistent kernel against the canonical oracle itself (10 iterations)."""
     n, m, iters = 3_000_000, 10, 10
-    os.environ["LBFGS_PERSIST"] = "1"
+    os.environ["LBFGS_PERSIST"] = mode
     try:
         x0 = L.x0_uniform(n, 42, -2.0, 2.0)
         with L.Context(n, m) as c:

@@ -154,6 +154,29 @@ def test_xgmi_silent_peer_times_out(tmp_path):
     assert procs[1].returncode == 0, outs[1][-2000:]
 
 
+@pytest.mark.parametrize("fold", ["0", "2"])
+def test_xgmi_stalled_peer_fails_once(tmp_path, fold):
+    """A peer that connects and then stops exchanging: the solving rank's first wait times out
+    (LBFGS_XGMI_TIMEOUT = 3 s) and every exchange queued behind it ends within ~1/65536 of that
+    once the error word is set, so the solve fails in about one timeout, not one per exchange
+    queued before the host's next synchronisation (with the fold forced, the gated consumers'
+    collect launches wait the same way). The stalled rank stays alive meanwhile, so its mailbox
+    stays mapped."""
+    e = dict(os.environ, LBFGS_XGMI_TIMEOUT="3", XGMI_STALL_S="25", LBFGS_XGMI_FOLD=fold)
+    args = [str(tmp_path), "", "2", "4000003", "5", "rosenbrock", "backtracking", "40", ""]
+    procs = []
+    for r, mode in ((0, "expect_fail"), (1, "stall")):
+        a = list(args)
+        a[1], a[8] = str(r), mode
+        procs.append(subprocess.Popen([sys.executable, WORKER] + a, stdout=subprocess.PIPE,
+                                      stderr=subprocess.STDOUT, text=True, env=e))
+    outs = [p.communicate(timeout=180)[0] for p in procs]
+    assert procs[0].returncode == 4, outs[0][-2000:]
+    took = float(outs[0].split("failed after ")[1].split(" s")[0])
+    assert took < 15.0, outs[0][-2000:]
+    assert procs[1].returncode == 0, outs[1][-2000:]
+
+
 def test_xgmi_exchange_latency_collective(tmp_path):
     """lbfgs_exchange_latency (bench.py's exchange_latency_us) runs as a collective on every rank
     and returns a positive per-exchange time for both slot widths."""

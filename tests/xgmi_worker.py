@@ -64,6 +64,20 @@ def main():
         sys.exit(3)
     assert ctx.backend == "xgmi", ctx.backend
     folded = ctx.folded
+    if mode == "stall":  # connected, then never exchanges while a peer solves (timeout test)
+        time.sleep(float(os.environ.get("XGMI_STALL_S", "20")))
+        ctx.close()
+        return
+    if mode == "expect_fail":  # the peer stalls: the solve must fail, once, within its timeout
+        t0 = time.time()
+        try:
+            ctx.minimize(obj, x0, ls, iters, trace=True)
+        except L.LbfgsError as e:
+            print(f"rank {rank}: failed after {time.time() - t0:.1f} s: {e}", flush=True)
+            ctx.close()
+            sys.exit(4)
+        print(f"rank {rank}: no failure", flush=True)
+        sys.exit(0)
     if mode == "latency":  # lbfgs_exchange_latency through the mailboxes (collective)
         us8 = ctx.exchange_latency("xgmi", 8, 50)
         us96 = ctx.exchange_latency("xgmi", 96, 50)
