@@ -19,7 +19,8 @@ import lbfgs_amd as L  # noqa: E402
 pytestmark = pytest.mark.gpu
 
 KNOBS = ["LBFGS_TICKET", "LBFGS_DEFER", "LBFGS_REV", "LBFGS_NT", "LBFGS_DIRECT", "LBFGS_COOP",
-         "LBFGS_PERSIST", "LBFGS_PINGPONG", "LBFGS_SPEC", "LBFGS_BATCH", "LBFGS_SMALL_SEGS"]
+         "LBFGS_PERSIST", "LBFGS_PINGPONG", "LBFGS_SPEC", "LBFGS_BATCH", "LBFGS_SMALL_SEGS",
+         "LBFGS_PERSIST_WG", "LBFGS_PERSIST_OWN", "LBFGS_PERSIST_ALT", "LBFGS_PERSIST_LDS"]
 
 VARIANTS = {
     "ticket1": {"LBFGS_TICKET": "1"},
@@ -32,6 +33,10 @@ VARIANTS = {
     "direct0": {"LBFGS_DIRECT": "0"},
     "coop0": {"LBFGS_COOP": "0"},
     "persist1": {"LBFGS_PERSIST": "1"},
+    "persist2": {"LBFGS_PERSIST": "2"},
+    "persist2_wg1_stride": {"LBFGS_PERSIST": "2", "LBFGS_PERSIST_WG": "1", "LBFGS_PERSIST_OWN": "stride"},
+    "persist2_alt0_lds0_nt1": {"LBFGS_PERSIST": "2", "LBFGS_PERSIST_ALT": "0", "LBFGS_PERSIST_LDS": "0",
+                               "LBFGS_NT": "1"},
     "pingpong1": {"LBFGS_PINGPONG": "1"},
     "spec0": {"LBFGS_SPEC": "0"},
     "batch0": {"LBFGS_BATCH": "0"},
