@@ -70,7 +70,8 @@ struct Geo {
 struct FoldSrc {
     const unsigned long long* mbx;  // nullptr: the source is an ordinary slot
     unsigned mepoch;
-    unsigned* merr;
+    unsigned* merr;   // pinned error flag (the host reads it)
+    unsigned* merrd;  // its device copy (the waiting polls read it)
     unsigned long long mtmo;
     unsigned long long* wait;  // profiling: workgroup 0 adds its prologue's wall-clock ticks here
 };
@@ -444,13 +445,13 @@ __global__ __launch_bounds__(LB_BLOCK) void k_group_reduce_wide(const double* __
 }
 
 // A wait on a peer's mailbox word ends past `timeout` wall-clock ticks, or - once it has waited
-// 1/65536 of that (~1 ms of the default 60 s) - as soon as the pinned error word shows that an
-// earlier wait of this rank already timed out: a broken channel costs one timeout per solve, not
+// 1/65536 of that (~1 ms of the default 60 s) - as soon as the error flag's device copy shows that
+// an earlier wait of this rank already timed out: a broken channel costs one timeout per solve, not
 // one per exchange queued before the host's next synchronisation.
-__device__ __forceinline__ bool peer_wait_over(unsigned long long t0, unsigned long long timeout, const unsigned* err) {
+__device__ __forceinline__ bool peer_wait_over(unsigned long long t0, unsigned long long timeout, const unsigned* errd) {
     const unsigned long long el = wall_clock64() - t0;
     if (el > timeout) return true;
-    return el > (timeout >> 16) && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u;
+    return el > (timeout >> 16) && __hip_atomic_load(errd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
 }
 
 // Total of a launch's first source slot (the previous pass's reduction). Normally stage 2 ran
@@ -479,7 +480,8 @@ __device__ __forceinline__ double src_total_mailbox(const double* slot, const Ge
                 a = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 b = __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 if ((unsigned)(a >> 32) == fs.mepoch && (unsigned)(b >> 32) == fs.mepoch) break;
-                if (peer_wait_over(t0, fs.mtmo, fs.merr)) {
+                if (peer_wait_over(t0, fs.mtmo, fs.merrd)) {
+                    __hip_atomic_store(fs.merrd, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     __hip_atomic_store(fs.merr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     a = 0;
                     b = 0x7ff80000ull;  // quiet NaN
@@ -2992,7 +2994,7 @@ void fold_producer(lbk_ctx* c, Red& r, bool edges) {
 // Folded exchange, consumer: a launch whose first source (src_total) is the pending folded slot
 // polls the mailbox for it in its prologue
 FoldSrc take_fold(lbk_ctx* c, int ref) {
-    FoldSrc f{nullptr, 0u, nullptr, 0ull, nullptr};
+    FoldSrc f{nullptr, 0u, nullptr, nullptr, 0ull, nullptr};
     if (c->xf_slot < 0 || ref % LBK_KMAX != 0 || c->xf_slot != ref / LBK_KMAX) return f;
     if (c->xf.shared_device) {
         // ranks sharing one GPU (forced fold: tests, rehearsals): a consuming pass's workgroups
@@ -3012,6 +3014,7 @@ FoldSrc take_fold(lbk_ctx* c, int ref) {
     f.mbx = c->xf.own + (size_t)(c->xf_epoch & 1u) * (size_t)c->xf.positions * 2;
     f.mepoch = c->xf_epoch;
     f.merr = c->xf.err;
+    f.merrd = c->xf.errd;
     f.mtmo = c->xf.timeout;
     f.wait = c->prof_on ? c->fold_wait : nullptr;
     c->xf_taken = 1;

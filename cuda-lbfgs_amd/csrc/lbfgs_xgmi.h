@@ -51,6 +51,7 @@ struct lbk_xgmi_fold {
     unsigned long long* const* peers;  // device array [world]: every rank's mailbox as mapped here
     const unsigned long long* own;     // this rank's mailbox
     unsigned* err;                     // pinned: set by a poll that timed out
+    unsigned* errd;                    // the same flag in device memory, read by waiting polls
     unsigned long long timeout;        // wall-clock ticks
     int positions;                     // doubles per parity (the mailbox's [2][positions][2] layout)
     int rank, world;

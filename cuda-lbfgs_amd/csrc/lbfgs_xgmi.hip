@@ -29,6 +29,7 @@ struct lbk_xgmi {
     hipIpcMemHandle_t handle;
     unsigned* err_h;  // pinned, written by the kernel on a timeout
     unsigned* err_d;
+    unsigned* err_dev;  // the same flag in device memory: what the waiting polls read
     unsigned epoch;
     unsigned long long timeout_ticks;  // wall-clock ticks (hipDeviceAttributeWallClockRate)
     double wall_khz;
@@ -40,12 +41,16 @@ struct lbk_xgmi {
 
 namespace {
 
-// a wait ends past `timeout` ticks, or after 1/65536 of it once the pinned error word shows an
-// earlier timeout of this rank (one timeout per solve on a broken channel, not one per exchange)
-__device__ __forceinline__ bool wait_over(unsigned long long t0, unsigned long long timeout, const unsigned* err) {
+// a wait ends past `timeout` ticks, or after 1/65536 of it once the error flag (device copy) shows
+// an earlier timeout of this rank (one timeout per solve on a broken channel, not one per exchange)
+__device__ __forceinline__ bool wait_over(unsigned long long t0, unsigned long long timeout, const unsigned* errd) {
     const unsigned long long el = wall_clock64() - t0;
     if (el > timeout) return true;
-    return el > (timeout >> 16) && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u;
+    return el > (timeout >> 16) && __hip_atomic_load(errd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+}
+__device__ __forceinline__ void set_failed(unsigned* err, unsigned* errd) {
+    __hip_atomic_store(errd, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // One workgroup. Push: own positions [lo, hi) to every peer's mailbox (two LL words per 64-bit
@@ -55,7 +60,7 @@ __device__ __forceinline__ bool wait_over(unsigned long long t0, unsigned long l
 // next synchronisation) instead of a hung queue.
 __global__ __launch_bounds__(256) void k_xgmi_exchange(unsigned long long* __restrict__ slot, int ks, int g_lo,
                                                         int g_hi, XPeers P, int rank, int world, int positions,
-                                                        unsigned epoch, unsigned* err,
+                                                        unsigned epoch, unsigned* err, unsigned* errd,
                                                         unsigned long long timeout,
                                                         unsigned long long* __restrict__ hm) {
     const int lo = g_lo * ks, hi = g_hi * ks, own = hi - lo, npos = XG_GROUPS * ks;
@@ -81,8 +86,8 @@ __global__ __launch_bounds__(256) void k_xgmi_exchange(unsigned long long* __res
             a = __hip_atomic_load(mine + 2 * (size_t)j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             b = __hip_atomic_load(mine + 2 * (size_t)j + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             if ((unsigned)(a >> 32) == epoch && (unsigned)(b >> 32) == epoch) break;
-            if (wait_over(t0, timeout, err)) {
-                __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (wait_over(t0, timeout, errd)) {
+                set_failed(err, errd);
                 a = 0;
                 b = 0x7ff80000ull;  // quiet NaN
                 break;
@@ -100,7 +105,7 @@ __global__ __launch_bounds__(256) void k_xgmi_exchange(unsigned long long* __res
 // rank's first group and 2 of its last) and write them into the slot.
 __global__ __launch_bounds__(64) void k_xgmi_collect(unsigned long long* __restrict__ slot, int ks, int g_lo,
                                                      int g_hi, const unsigned long long* mine, int world,
-                                                     unsigned epoch, int edges, unsigned* err,
+                                                     unsigned epoch, int edges, unsigned* err, unsigned* errd,
                                                      unsigned long long timeout) {
     const int per = XG_GROUPS / world;
     const int j = threadIdx.x;  // 0..7 group values, 8..15 first-group edges, 16..23 last-group edges
@@ -116,8 +121,8 @@ __global__ __launch_bounds__(64) void k_xgmi_collect(unsigned long long* __restr
         a = __hip_atomic_load(mine + 2 * (size_t)pos, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         b = __hip_atomic_load(mine + 2 * (size_t)pos + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         if ((unsigned)(a >> 32) == epoch && (unsigned)(b >> 32) == epoch) break;
-        if (wait_over(t0, timeout, err)) {
-            __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (wait_over(t0, timeout, errd)) {
+            set_failed(err, errd);
             a = 0;
             b = 0x7ff80000ull;
             break;
@@ -136,7 +141,7 @@ int launch(lbk_xgmi* x, hipStream_t s, unsigned long long* slot, int ks, int g_l
     if (ks < 1 || XG_GROUPS * ks > x->positions || g_lo < 0 || g_hi > XG_GROUPS || g_lo >= g_hi) return -1;
     lbk_xgmi_next_epoch(x);
     hipLaunchKernelGGL(k_xgmi_exchange, dim3(1), dim3(256), 0, s, slot, ks, g_lo, g_hi, x->peers, x->rank,
-                       x->world, x->positions, x->epoch, x->err_d, timeout, hm);
+                       x->world, x->positions, x->epoch, x->err_d, x->err_dev, timeout, hm);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
@@ -170,6 +175,8 @@ int lbk_xgmi_create(lbk_xgmi** out, int device, int rank, int world, int positio
     }
     if (e == hipSuccess) e = hipMemset(x->mb, 0, bytes);
     if (e == hipSuccess) e = hipIpcGetMemHandle(&x->handle, x->mb);
+    if (e == hipSuccess) e = hipMalloc((void**)&x->err_dev, sizeof(unsigned));
+    if (e == hipSuccess) e = hipMemset(x->err_dev, 0, sizeof(unsigned));
     if (e == hipSuccess) e = hipHostMalloc((void**)&x->err_h, sizeof(unsigned), hipHostMallocMapped);
     if (e == hipSuccess) {
         *x->err_h = 0;
@@ -201,6 +208,7 @@ void lbk_xgmi_destroy(lbk_xgmi* x) {
     if (x->peers_dev) (void)hipFree(x->peers_dev);
     if (x->mb) (void)hipFree(x->mb);
     if (x->err_h) (void)hipHostFree(x->err_h);
+    if (x->err_dev) (void)hipFree(x->err_dev);
     delete x;
 }
 
@@ -295,6 +303,7 @@ int lbk_xgmi_fold_info(const lbk_xgmi* x, lbk_xgmi_fold* out) {
     out->peers = x->peers_dev;
     out->own = x->mb;
     out->err = x->err_d;
+    out->errd = x->err_dev;
     out->timeout = x->timeout_ticks;
     out->positions = x->positions;
     out->rank = x->rank;
@@ -314,7 +323,7 @@ int lbk_xgmi_collect(lbk_xgmi* x, hipStream_t stream, double* slot, int ks, int 
     if (!x->connected) return -5;
     const unsigned long long* mine = x->mb + (size_t)(epoch & 1u) * (size_t)x->positions * 2;
     hipLaunchKernelGGL(k_xgmi_collect, dim3(1), dim3(64), 0, stream, reinterpret_cast<unsigned long long*>(slot), ks,
-                       g_lo, g_hi, mine, x->world, epoch, edges, x->err_d, x->timeout_ticks);
+                       g_lo, g_hi, mine, x->world, epoch, edges, x->err_d, x->err_dev, x->timeout_ticks);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
