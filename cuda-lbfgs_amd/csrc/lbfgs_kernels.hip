@@ -142,6 +142,13 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
     // 1e8 (profiles/r01/rev_ab.txt); bit-identical either way (per-segment partials)
     c->rev_on = 1;
     if (const char* e = getenv("LBFGS_REV")) c->rev_on = atoi(e) != 0;
+    // stage 2 inside the producing launch by each group's last-dispatched workgroup instead of a
+    // reduce kernel after it: measured +0.2..0.9 % at n = 3e7..1e9 (segments of 3712..122112),
+    // neutral at 1e7 and 1.5..3.5 % slower at 2.5e6..5e6, where short-lived workgroups leave the
+    // collector waiting on stragglers (profiles/r03/collect_ab/). Default for segments of at least
+    // 3072 elements; LBFGS_COLLECT=0/1 overrides
+    c->collect_on = G.L >= 3072 ? 1 : 0;
+    if (const char* e = getenv("LBFGS_COLLECT")) c->collect_on = atoi(e) != 0;
     // sharded slots are completed by the exchange on the device: those fetch with a copy
     c->direct = world == 1 ? 1 : 0;
     if (const char* e = getenv("LBFGS_DIRECT")) c->direct = world == 1 && atoi(e) != 0;
@@ -181,6 +188,11 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
         const size_t llb = sizeof(unsigned long long) * 2 * LBK_LL_COMPS * LBK_LL_SEGS * 2;
         CK(hipMalloc(&c->coop_ll, llb));
         CK(hipMemset(c->coop_ll, 0, llb));  // tag 0: no pass (sequence numbers start at 1)
+    }
+    {
+        const size_t llb = sizeof(unsigned long long) * 2 * LBK_KW * LBK_SEGS;
+        CK(hipMalloc(&c->coll_ll, llb));
+        CK(hipMemset(c->coll_ll, 0, llb));  // tag 0: no launch (tags start at 1)
     }
     CK(hipHostMalloc((void**)&c->coop_err_h, sizeof(unsigned), hipHostMallocMapped | hipHostMallocCoherent));
     *c->coop_err_h = 0;
@@ -312,6 +324,7 @@ void lbk_destroy(lbk_ctx* c) {
     if (c->d_ckslot) (void)hipFree(c->d_ckslot);
     (void)hipFree(c->partials);
     (void)hipFree(c->coop_ll);
+    (void)hipFree(c->coll_ll);
     xfer_pool_free(c);
     (void)hipFree(c->persist_cnt);
     (void)hipFree(c->fold_wait);

@@ -109,6 +109,11 @@ struct Red {
     unsigned long long* done;
     unsigned long long epoch;
     FoldPush fp;  // folded exchange: the last arriver pushes the group value (K == 1)
+    // collect: segment partials as flagged words, stage 2 by each group's last-dispatched workgroup
+    unsigned long long* ll;  // [LBK_KW][LBK_SEGS][2] flagged partials, or nullptr (other modes)
+    unsigned seq;            // this launch's tag
+    unsigned* err;           // pinned: set on a timeout
+    unsigned long long timeout;
 };
 
 // Streaming loads/stores; NT = non-temporal (the vectors are touched once per pass and, at
@@ -337,6 +342,115 @@ __device__ __forceinline__ void group_tree(const double* partials, int64_t lbase
     }
 }
 
+// Collect mode's stage 2 of group g inside the producing launch: group_tree's arithmetic exactly
+// (the same two shapes: <= 64 valid partials, or 4 per thread + butterflies + the wave pairs),
+// with the partials read as flagged words (ll_store, tag = the launch's sequence number) that
+// every workgroup of the group stored without waiting. Each batch of words is issued at once and
+// polled until every tag matches; a wait past `timeout` sets *err and gives NaN.
+template <int M>
+__device__ __forceinline__ void ll_load_batch(const unsigned long long* const (&p)[M], const bool (&on)[M],
+                                              unsigned seq, double (&out)[M], unsigned* err,
+                                              unsigned long long timeout) {
+    unsigned long long w0[M], w1[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+        w0[m] = on[m] ? __hip_atomic_load(p[m], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+        w1[m] = on[m] ? __hip_atomic_load(p[m] + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+    }
+    unsigned long long t0 = 0;
+    for (;;) {
+        bool all = true;
+#pragma unroll
+        for (int m = 0; m < M; ++m)
+            if (on[m] && ((unsigned)(w0[m] >> 32) != seq || (unsigned)(w1[m] >> 32) != seq)) all = false;
+        if (all) break;
+        if (t0 == 0) t0 = wall_clock64();
+        if (wall_clock64() - t0 > timeout) {
+            if (err) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#pragma unroll
+            for (int m = 0; m < M; ++m) out[m] = __builtin_nan("");
+            return;
+        }
+        __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+            if (on[m] && (unsigned)(w0[m] >> 32) != seq)
+                w0[m] = __hip_atomic_load(p[m], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (on[m] && (unsigned)(w1[m] >> 32) != seq)
+                w1[m] = __hip_atomic_load(p[m] + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+#pragma unroll
+    for (int m = 0; m < M; ++m) out[m] = on[m] ? bitsd((w1[m] << 32) | (w0[m] & 0xffffffffull)) : 0.0;
+}
+
+template <int K>
+__device__ __forceinline__ void collect_tree(const Red& red, int64_t lbase, int64_t gseg0, int64_t nseg, int spg,
+                                             double* slot_g, double* hslot_g, double (&lds)[4][K > 0 ? K : 1]) {
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    auto word = [&](int k, int64_t j) { return red.ll + ((int64_t)k * LBK_SEGS + lbase + j) * 2; };
+    const int64_t nvalid = min((int64_t)spg, nseg - gseg0);
+    if (nvalid <= 64) {  // group_tree's short shape
+        constexpr int KQ = (K + 3) / 4;
+        const unsigned long long* pp[KQ];
+        bool on[KQ];
+        double p[KQ];
+#pragma unroll
+        for (int i = 0; i < KQ; ++i) {
+            const int k = w + 4 * i;
+            on[i] = k < K && lane < nvalid;
+            pp[i] = on[i] ? word(k, lane) : red.ll;
+        }
+        ll_load_batch<KQ>(pp, on, red.seq, p, red.err, red.timeout);
+#pragma unroll
+        for (int i = 0; i < KQ; ++i) {
+            const int k = w + 4 * i;
+            const double v = wave_sum(p[i]) + 0.0;
+            if (k < K && lane == 0) {
+                slot_g[k] = v;
+                if (hslot_g) hslot_g[k] = v;
+            }
+        }
+        return;
+    }
+    double q[K];
+    constexpr int KC = 2;  // components per batch of polled words (4 words... 8 per component)
+#pragma unroll
+    for (int k0 = 0; k0 < K; k0 += KC) {
+        const unsigned long long* pp[KC * 4];
+        bool on[KC * 4];
+        double p[KC * 4];
+#pragma unroll
+        for (int kc = 0; kc < KC; ++kc)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int64_t j = 4 * t + i;
+                on[kc * 4 + i] = k0 + kc < K && j < spg && gseg0 + j < nseg;
+                pp[kc * 4 + i] = on[kc * 4 + i] ? word(k0 + kc, j) : red.ll;
+            }
+        ll_load_batch<KC * 4>(pp, on, red.seq, p, red.err, red.timeout);
+#pragma unroll
+        for (int kc = 0; kc < KC; ++kc) {
+            if (k0 + kc >= K) break;
+            q[k0 + kc] = wave_sum((p[kc * 4] + p[kc * 4 + 1]) + (p[kc * 4 + 2] + p[kc * 4 + 3]));
+        }
+    }
+    __syncthreads();  // lds reuse
+    if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) lds[w][k] = q[k];
+    }
+    __syncthreads();
+    if (t == 0) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const double v = (lds[0][k] + lds[1][k]) + (lds[2][k] + lds[3][k]);
+            slot_g[k] = v;
+            if (hslot_g) hslot_g[k] = v;
+        }
+    }
+}
+
 // Segment partial (wave butterflies, ((w0 + w1) + (w2 + w3))), then either
 //   red.ticket : write-through store + per-group agent-scope ticket; the last-arriving
 //                workgroup of the group runs stage 2 (one launch; used for small grids), or
@@ -359,6 +473,24 @@ __device__ __forceinline__ void reduce_publish(double (&acc)[K], const Geo& geo,
     const int64_t b = seg_block(geo);
     const int64_t sg = geo.seg_lo + b;
     const int g = (int)(sg / geo.spg);
+    if (red.ll) {
+        // collect: the partial as flagged words, no wait; the group's last-dispatched workgroup
+        // (highest block index: the group's last segment, or its first when the walk is
+        // reversed) forms the group tree from them. It waits only for workgroups dispatched
+        // before it, none of which waits on anything, so the wait always ends.
+        if (t == 0) {
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+                ll_store(red.ll + ((int64_t)k * LBK_SEGS + b) * 2, (lds[0][k] + lds[1][k]) + (lds[2][k] + lds[3][k]),
+                         red.seq);
+        }
+        const int64_t gseg0 = (int64_t)g * geo.spg;
+        const int64_t glast = min(geo.nseg, gseg0 + geo.spg) - 1;
+        if (sg != (geo.rev ? gseg0 : glast)) return;  // uniform over the workgroup
+        collect_tree<K>(red, gseg0 - geo.seg_lo, gseg0, geo.nseg, geo.spg, red.slot + g * red.kstride,
+                        red.hslot ? red.hslot + g * red.kstride : nullptr, lds);
+        return;
+    }
     if (!red.ticket) {
         if (t == 0) {
 #pragma unroll
@@ -2669,6 +2801,10 @@ struct lbk_ctx {
     // deferred stage 2 (src_total): single-component two-loop reductions with
     // coop_max < nseg <= defer_max leave their partials for the consuming pass
     int defer_max;
+    // collect-mode stage 2 (kred): on, the launch being set up uses it, flagged partials, tags
+    int collect_on, collect_now;
+    unsigned long long* coll_ll;
+    unsigned coll_seq;
     int defer_now;        // the launch in progress defers its stage 2
     int defer_region;     // partials region (component) the next deferred producer writes
     int pend_slot;        // slot whose stage 2 is still pending (-1: none)
@@ -2815,6 +2951,22 @@ Red kred(lbk_ctx* c, int slot, int K = 1) {
     r.done = nullptr;
     r.epoch = 0;
     r.fp = FoldPush{nullptr, 0, 0, 0, 0u};
+    r.ll = nullptr;
+    r.seq = 0;
+    r.err = nullptr;
+    r.timeout = 0;
+    c->collect_now = 0;
+    // collect mode (one rank, reduce-kernel stage 2 otherwise): stage 2 inside the launch, no
+    // reduce kernel after it (LBFGS_COLLECT)
+    // (regular slots only: a wide slot's tree would poll its up to 96 components batch by batch)
+    if (c->collect_on && !r.ticket && c->geo.world == 1 && !c->comm && !c->grp && c->geo.nseg > c->coop_max &&
+        K <= LBK_KMAX && slot < LBK_NSLOTS) {
+        r.ll = c->coll_ll;
+        r.seq = ++c->coll_seq;
+        r.err = c->coop_err_d;
+        r.timeout = (unsigned long long)(2.0 * c->wall_khz * 1e3);
+        c->collect_now = 1;
+    }
     const int si = slot < LBK_NSLOTS ? slot : LBK_NSLOTS + slot - LBK_WSLOT0;
     c->slot_s2[si] = 0;
     // each group's last arriver stores the word, so it stands for the whole slot only when every
@@ -3029,6 +3181,8 @@ Red kred_deferrable(lbk_ctx* c, int slot) {
     if (c->geo.world == 1 && !c->comm && !c->ticket && c->geo.nseg > c->coop_max && c->geo.nseg <= c->defer_max) {
         r.partials = defer_part(c, c->defer_region);
         c->defer_now = 1;
+        r.ll = nullptr;  // the consumer forms the trees instead
+        c->collect_now = 0;
     }
     return r;
 }
@@ -3075,7 +3229,7 @@ int launch(lbk_ctx* c, int kind, double vec_passes, int slot, F&& fn, int K = 1,
         HIPCHK(c, hipEventRecord(b, c->stream));
         c->pending.push_back({kind, a, b, bytes});
         a = b = nullptr;
-        if (slot >= 0 && !c->ticket && !c->defer_now) {
+        if (slot >= 0 && !c->ticket && !c->defer_now && !c->collect_now) {
             a = ev_get(c);
             b = ev_get(c);
             if (a) HIPCHK(c, hipEventRecord(a, c->stream));
@@ -3098,7 +3252,7 @@ int launch(lbk_ctx* c, int kind, double vec_passes, int slot, F&& fn, int K = 1,
         c->pend_part = defer_part(c, c->defer_region);
         c->defer_region ^= 1;
         c->defer_now = 0;
-    } else if (slot >= 0 && !c->ticket) {
+    } else if (slot >= 0 && !c->ticket && !c->collect_now) {
         const Geo g = gv ? *gv : kgeo(c);
         double* sl = slot_base(c, slot);
         double* hs = mirrored(c, slot, K) ? slot_dhost(c, slot) : nullptr;
@@ -3120,6 +3274,7 @@ int launch(lbk_ctx* c, int kind, double vec_passes, int slot, F&& fn, int K = 1,
         HIPCHK(c, hipEventRecord(b, c->stream));
         c->pending.push_back({kind, a, b, 0.0});
     }
+    c->collect_now = 0;
     if (c->fold_now) {  // pushed by the pass (or its reduce kernel): no exchange launch
         c->xf_slot = slot;
         c->xf_epoch = c->fold_epoch;

@@ -20,7 +20,7 @@ pytestmark = pytest.mark.gpu
 
 KNOBS = ["LBFGS_TICKET", "LBFGS_DEFER", "LBFGS_REV", "LBFGS_NT", "LBFGS_DIRECT", "LBFGS_COOP",
          "LBFGS_PERSIST", "LBFGS_PINGPONG", "LBFGS_SPEC", "LBFGS_BATCH", "LBFGS_SMALL_SEGS",
-         "LBFGS_PERSIST_WG", "LBFGS_PERSIST_OWN", "LBFGS_PERSIST_ALT", "LBFGS_PERSIST_LDS"]
+         "LBFGS_PERSIST_WG", "LBFGS_PERSIST_OWN", "LBFGS_PERSIST_ALT", "LBFGS_PERSIST_LDS", "LBFGS_COLLECT"]
 
 VARIANTS = {
     "ticket1": {"LBFGS_TICKET": "1"},
@@ -38,6 +38,9 @@ VARIANTS = {
     "persist2_alt0_lds0_nt1": {"LBFGS_PERSIST": "2", "LBFGS_PERSIST_ALT": "0", "LBFGS_PERSIST_LDS": "0",
                                "LBFGS_NT": "1"},
     "pingpong1": {"LBFGS_PINGPONG": "1"},
+    "collect1": {"LBFGS_COLLECT": "1"},
+    "collect1_rev0_nt1": {"LBFGS_COLLECT": "1", "LBFGS_REV": "0", "LBFGS_NT": "1"},
+    "collect1_defer0_batch0": {"LBFGS_COLLECT": "1", "LBFGS_DEFER": "0", "LBFGS_BATCH": "0"},
     "spec0": {"LBFGS_SPEC": "0"},
     "batch0": {"LBFGS_BATCH": "0"},
     "ticket1_direct0": {"LBFGS_TICKET": "1", "LBFGS_DIRECT": "0"},
