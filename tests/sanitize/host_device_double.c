@@ -29,6 +29,7 @@ struct lbk_ctx {
     /* the small-n single-launch iteration and its speculative form (LBFGS_DOUBLE_SMALL=1; the
      * product uses it for nseg <= its cooperative limit): launches run at once, in stream order */
     int small_on;
+    int twoloop_on;
     unsigned long long epoch, vd[4];
     int rec_went[4];
     double rec_rho[4], rec_gamma[4];
@@ -76,6 +77,8 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
     }
     const char* e = getenv("LBFGS_DOUBLE_SMALL");
     c->small_on = e && atoi(e) != 0;
+    e = getenv("LBFGS_DOUBLE_TWOLOOP");  /* the driver's persistent two-loop branch (LBFGS_PERSIST=2) */
+    c->twoloop_on = e && atoi(e) != 0;
     *out = c;
     return 0;
 }
@@ -539,6 +542,34 @@ int lbk_small_iter(lbk_ctx* c, int obj, int h, const double* g, double* q, doubl
     return lbk_commit(c, obj, LBK_D_TWOLOOP, x, r, S[h - 1], g, rho_top, refB[h - 1], refA[h - 1], a0, xn, gn, so, yo,
                       slot_c, cand);
 }
+/* the persistent two-loop: the same passes into the same slots, no commit */
+int lbk_twoloop_ok(const lbk_ctx* c, int h) { return c->twoloop_on && h >= 1 && h <= 16; }
+int lbk_twoloop_persist(lbk_ctx* c, int h, const double* g, double* q, double* r, const double* const* S,
+                        const double* const* Y, const double* rho, double gamma, int p0_ref, int slot_p0,
+                        int slot_a0, int slot_b0) {
+    if (!lbk_twoloop_ok(c, h)) return -1;
+    int refA[16], refB[16];
+    if (p0_ref >= 0) {
+        refA[h - 1] = p0_ref;
+    } else {
+        if (lbk_dot(c, S[h - 1], g, slot_p0)) return -1;
+        refA[h - 1] = slot_p0 * LBK_KMAX;
+    }
+    const double* qsrc = g;
+    for (int i = h - 2; i >= 0; --i) {
+        if (lbk_axpy_dot(c, q, qsrc, Y[i + 1], S[i], rho[i + 1], refA[i + 1], slot_a0 + i)) return -1;
+        refA[i] = (slot_a0 + i) * LBK_KMAX;
+        qsrc = q;
+    }
+    if (lbk_mid(c, r, qsrc, Y[0], rho[0], gamma, refA[0], slot_b0)) return -1;
+    refB[0] = slot_b0 * LBK_KMAX;
+    for (int i = 0; i + 1 < h; ++i) {
+        if (lbk_axpy2_dot(c, r, r, S[i], Y[i + 1], rho[i], refB[i], refA[i], slot_b0 + i + 1)) return -1;
+        refB[i + 1] = (slot_b0 + i + 1) * LBK_KMAX;
+    }
+    return 0;
+}
+
 int lbk_mark(lbk_ctx* c) {
     (void)c;
     return 0;

@@ -114,7 +114,7 @@ static std::vector<double> x0_for(int64_t n, uint32_t seed) {
 }
 
 // device objectives, every line search, default / batched-off / unfused / the small-n single
-// launch per iteration with and without the speculative next iteration
+// launch per iteration with and without the speculative next iteration / the persistent two-loop
 static void device_objectives() {
     const int64_t sizes[] = {1, 2, 3, 1000, 4097, 70001};
     const int objs[] = {LBFGS_OBJ_ROSENBROCK, LBFGS_OBJ_QUAD_TRIDIAG, LBFGS_OBJ_QUAD_SEPARABLE};
@@ -122,12 +122,13 @@ static void device_objectives() {
     for (int64_t n : sizes)
         for (int obj : objs)
             for (int ls = 0; ls < 4; ++ls)
-                for (int mode = 0; mode < 5; ++mode) {
+                for (int mode = 0; mode < 6; ++mode) {
                     const int m = n < 10 ? 2 : 5, maxit = n > 10000 ? 12 : 40;
                     if (obj == LBFGS_OBJ_QUAD_SEPARABLE && ls == LBFGS_LS_WOLFE) continue;  // diverges to NaN
                     setenv("LBFGS_BATCH", mode == 1 ? "0" : "1", 1);
-                    setenv("LBFGS_DOUBLE_SMALL", mode >= 3 ? "1" : "0", 1);
+                    setenv("LBFGS_DOUBLE_SMALL", mode == 3 || mode == 4 ? "1" : "0", 1);
                     setenv("LBFGS_SPEC", mode == 4 ? "0" : "1", 1);
+                    setenv("LBFGS_DOUBLE_TWOLOOP", mode == 5 ? "1" : "0", 1);
                     const auto x0 = x0_for(n, 42 + (uint32_t)n);
                     lbfgs_ctx* c = nullptr;
                     EXPECT(lbfgs_ctx_create(&c, n, m, 0) == 0, "create n=%lld", (long long)n);
@@ -156,6 +157,7 @@ static void device_objectives() {
     setenv("LBFGS_BATCH", "1", 1);
     setenv("LBFGS_DOUBLE_SMALL", "0", 1);
     setenv("LBFGS_SPEC", "1", 1);
+    setenv("LBFGS_DOUBLE_TWOLOOP", "0", 1);
 }
 
 // host callbacks: the reference call sequence call for call, and one call per point by default
