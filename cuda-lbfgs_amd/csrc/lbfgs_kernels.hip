@@ -190,7 +190,7 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
         CK(hipMemset(c->coop_ll, 0, llb));  // tag 0: no pass (sequence numbers start at 1)
     }
     {
-        const size_t llb = sizeof(unsigned long long) * 2 * LBK_KW * LBK_SEGS;
+        const size_t llb = sizeof(unsigned long long) * 2 * LBK_KMAX * LBK_SEGS;  // regular slots only
         CK(hipMalloc(&c->coll_ll, llb));
         CK(hipMemset(c->coll_ll, 0, llb));  // tag 0: no launch (tags start at 1)
     }

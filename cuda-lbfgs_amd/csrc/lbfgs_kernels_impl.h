@@ -110,7 +110,7 @@ struct Red {
     unsigned long long epoch;
     FoldPush fp;  // folded exchange: the last arriver pushes the group value (K == 1)
     // collect: segment partials as flagged words, stage 2 by each group's last-dispatched workgroup
-    unsigned long long* ll;  // [LBK_KW][LBK_SEGS][2] flagged partials, or nullptr (other modes)
+    unsigned long long* ll;  // [LBK_KMAX][LBK_SEGS][2] flagged partials, or nullptr (other modes)
     unsigned seq;            // this launch's tag
     unsigned* err;           // pinned: set on a timeout
     unsigned long long timeout;
