@@ -473,6 +473,9 @@ __device__ __forceinline__ void reduce_publish(double (&acc)[K], const Geo& geo,
     const int64_t b = seg_block(geo);
     const int64_t sg = geo.seg_lo + b;
     const int g = (int)(sg / geo.spg);
+    // (compiled for regular slots only: the code would cost the wide-slot vector-free commit a
+    // wave per SIMD of registers)
+    if constexpr (K <= LBK_KMAX) {
     if (red.ll) {
         // collect: the partial as flagged words, no wait; the group's last-dispatched workgroup
         // (highest block index: the group's last segment, or its first when the walk is
@@ -490,6 +493,7 @@ __device__ __forceinline__ void reduce_publish(double (&acc)[K], const Geo& geo,
         collect_tree<K>(red, gseg0 - geo.seg_lo, gseg0, geo.nseg, geo.spg, red.slot + g * red.kstride,
                         red.hslot ? red.hslot + g * red.kstride : nullptr, lds);
         return;
+    }
     }
     if (!red.ticket) {
         if (t == 0) {
