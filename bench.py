@@ -6,13 +6,17 @@ series sharding the same n across ranks).
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 
+With --gpus N > 1 and no launcher around it (no RANK in the environment) bench.py is its own
+launcher: it starts the N rank processes itself (self_launch) before anything touches a GPU.
+
 A step is one L-BFGS iteration of the whole n-vector problem (two-loop recursion, line search,
 commit). Before the W warm-up steps, m untimed iterations fill the m-pair history
 (`history_fill`), so every timed step uses h = m pairs whatever W is; the line reports the
 h range of the timed steps (`h_min`, `h_max`, `steady_state`).
 All vectors are resident in HBM before timing starts. One process per GPU; the solver's data
-path exchanges group partials with RCCL all-gathers inside liblbfgs_hip.so; torch.distributed
-(gloo) is only used for the rendezvous (unique id), barriers and the max-over-ranks time.
+path exchanges group partials through the xGMI peer mailboxes (or RCCL all-gathers) inside
+liblbfgs_hip.so; torch.distributed (gloo) is only used for the rendezvous (unique id), barriers,
+votes and the max-over-ranks time.
 
 Prints ONE JSON line (rank 0).
 """
@@ -21,6 +25,8 @@ import json
 import os
 import platform
 import shutil
+import signal
+import socket
 import struct
 import subprocess
 import sys
@@ -29,18 +35,13 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "cuda-lbfgs_amd"))
-import lbfgs_amd as L  # noqa: E402
-
-# load liblbfgs_hip.so (and through it /opt/rocm's HIP runtime and RCCL) before torch can load its
-# bundled copies: libraries with the same soname are then shared, not duplicated
-L.lib()
-
+import lbfgs_amd as L  # noqa: E402  (ctypes only: the library is loaded in main(), not here)
 import numpy as np  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=100)
@@ -68,7 +69,103 @@ def parse():
                    help="sharded runs: reductions through the xGMI peer mailboxes (falls back to RCCL "
                         "when any rank's self-test fails) or RCCL all-gathers; auto: the mailboxes "
                         "unless RCCL measures >10%% faster per exchange on this node")
-    return p.parse_args()
+    p.add_argument("--launch-timeout", type=float, default=float(os.environ.get("BENCH_LAUNCH_TIMEOUT", 3000)),
+                   help="--gpus N > 1 without a launcher: seconds before the self-launched ranks are stopped")
+    p.add_argument("--no-box-probe", action="store_true", help="skip the in-process HBM stream probe")
+    return p.parse_args(argv)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def self_launch(argv, world, timeout, script=None):
+    """--gpus N > 1 with no launcher around the command (no RANK in the environment): start the N
+    rank processes here, as `torch.distributed.run --nnodes 1 --nproc-per-node N --master-addr
+    127.0.0.1` would - RANK, LOCAL_RANK, WORLD_SIZE, LOCAL_WORLD_SIZE, MASTER_ADDR = 127.0.0.1 and
+    a free MASTER_PORT in each child's environment - and wait for them. This process never touches
+    a GPU (it has not loaded liblbfgs_hip.so): the ranks are fresh child processes, nothing is
+    re-executed. Rank 0's JSON line is this process's only stdout; every other line any rank
+    prints on stdout (gloo's connection notes, for one) goes to stderr. As soon as a rank fails, or `timeout` seconds pass, the remaining ranks are
+    stopped (their process groups: SIGTERM, then SIGKILL after 15 s) and the exit status is
+    non-zero: the failed rank's, or 124 on the time limit. Returns the exit status."""
+    script = script or os.path.abspath(__file__)
+    port = _free_port()
+    procs = []
+    base = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world),
+                LOCAL_WORLD_SIZE=str(world))
+    base.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC for the peer mailboxes / RCCL
+
+    def stop(reason):
+        alive = [p for p in procs if p.poll() is None]
+        if alive:
+            print(f"bench.py launcher: {reason}; stopping {len(alive)} rank(s)", file=sys.stderr, flush=True)
+        for p in alive:
+            try:
+                os.killpg(p.pid, signal.SIGTERM)
+            except ProcessLookupError:
+                pass
+        t_end = time.monotonic() + 15
+        for p in alive:
+            try:
+                p.wait(timeout=max(t_end - time.monotonic(), 0.1))
+            except subprocess.TimeoutExpired:
+                try:
+                    os.killpg(p.pid, signal.SIGKILL)
+                except ProcessLookupError:
+                    pass
+                p.wait()
+
+    def on_term(signum, frame):  # the launcher itself is stopped: take the ranks with it
+        stop(f"signal {signum}")
+        sys.exit(128 + signum)
+
+    def forward(pipe):  # rank 0: JSON lines to stdout, the rest to stderr
+        for line in iter(pipe.readline, b""):
+            out = sys.stdout if line.startswith(b"{") else sys.stderr
+            out.buffer.write(line)
+            out.flush()
+        pipe.close()
+
+    import threading
+
+    old = signal.signal(signal.SIGTERM, on_term)
+    rc = 0
+    fwd = None
+    try:
+        for r in range(world):
+            env = dict(base, RANK=str(r), LOCAL_RANK=str(r), GROUP_RANK="0")
+            procs.append(subprocess.Popen([sys.executable, script, *argv], env=env, start_new_session=True,
+                                          stdout=subprocess.PIPE if r == 0 else sys.stderr.fileno()))
+            if r == 0:
+                fwd = threading.Thread(target=forward, args=(procs[0].stdout,), daemon=True)
+                fwd.start()
+        deadline = time.monotonic() + timeout
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+            if bad:
+                r, c = bad[0]
+                rc = c if c > 0 else 128 - c  # killed by signal s: 128 + s
+                stop(f"rank {r} exited with status {c}")
+                break
+            if all(c == 0 for c in codes):
+                break
+            if time.monotonic() > deadline:
+                rc = 124
+                stop(f"time limit of {timeout:.0f} s")
+                break
+            time.sleep(0.2)
+    finally:
+        stop("launcher exiting")
+        signal.signal(signal.SIGTERM, old)
+        if fwd is not None:
+            fwd.join(timeout=10)
+    return rc
 
 
 class Dist:
@@ -203,13 +300,18 @@ def ntag(n):
 
 
 def pmc_traffic(kernel, n, world):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of this
-    workload (profiles/*/pmc_bench_n<n>.json, produced by tools/pmc_summary.py from separate
-    FETCH_SIZE and WRITE_SIZE passes, gfx950 FETCH_SIZE x2 correction applied), or None."""
+    """HBM bytes per launch of `kernel` from a committed rocprofv3 PMC summary of this workload
+    (profiles/<round>/pmc_bench_n<n>.json, produced by tools/pmc_summary.py from separate FETCH_SIZE
+    and WRITE_SIZE passes, gfx950 FETCH_SIZE x2 correction applied), newest round first. Only a
+    summary profiled on THIS library counts: its `_build.library` must carry the loaded library's
+    source hash (lbfgs_build_info), else it describes other code and is refused.
+    Returns (bytes per launch or None, source file or None, why a file was refused or None)."""
     import glob
 
     if world != 1:
-        return None, None
+        return None, None, None
+    lib_src = L.build_info()[0].split()[0]  # "src=<hash>"
+    refused = []
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", f"pmc_bench_n{ntag(n)}.json")))
     for fn in reversed(files):
         try:
@@ -217,10 +319,15 @@ def pmc_traffic(kernel, n, world):
         except (OSError, ValueError):
             continue
         for k, v in d.items():
-            if k.startswith("k_" + kernel + "<") or k == "k_" + kernel:
-                if "hbm_bytes_per_launch" in v:
-                    return v["hbm_bytes_per_launch"], os.path.relpath(fn, ROOT)
-    return None, None
+            if (k.startswith("k_" + kernel + "<") or k == "k_" + kernel) and "hbm_bytes_per_launch" in v:
+                built = (d.get("_build") or {}).get("library", "")
+                rel = os.path.relpath(fn, ROOT)
+                if built.split(" ")[0] != lib_src:
+                    refused.append(f"{rel}: profiled on {built.split(' ')[0] or 'an unrecorded library'}, "
+                                   f"the loaded library is {lib_src}")
+                    break
+                return v["hbm_bytes_per_launch"], rel, None
+    return None, None, "; ".join(refused) or None
 
 
 def cpu_model():
@@ -233,16 +340,53 @@ def cpu_model():
     return platform.processor() or "unknown"
 
 
-def measure(a, D, n, x0, dev, rank, world, uid, unfused=False, vector_free=False):
+def measure(a, D, n, x0, dev, rank, world, uid, unfused=False, vector_free=False, box_probe=False):
     """W warm-up steps, then EXACTLY K timed steps (barrier + device sync on both sides, no
-    instrumentation), then a separate event-instrumented pass for per-kernel durations."""
-    ctx = L.Context(n, a.history, device=dev, rank=rank, world=world, uid=uid)
+    instrumentation), then a separate event-instrumented pass for per-kernel durations.
+
+    Every rank returns, or every rank raises LbfgsError: a failure on one rank (a mailbox wait
+    that timed out, an allocation) is carried through the same sequence of gloo collectives the
+    other ranks make - its compute is skipped, its collectives are not - to a vote that all ranks
+    reach after each stage, so no rank is left in a collective its peers never enter. The context
+    is closed on every path."""
+    ctx, err = None, None
+    try:
+        ctx = L.Context(n, a.history, device=dev, rank=rank, world=world, uid=uid)
+    except L.LbfgsError as e:
+        err = e
+    if not D.all_ok(err is None):
+        if ctx is not None:
+            ctx.close()
+        raise err or L.LbfgsError("context creation failed on another rank")
+    try:
+        return _measure(a, D, ctx, x0, rank, world, uid, unfused, vector_free, box_probe)
+    finally:
+        ctx.close()
+
+
+def _measure(a, D, ctx, x0, rank, world, uid, unfused, vector_free, box_probe):
+    failed = []  # this rank's first failure (sticky: later compute is skipped, collectives are not)
+
+    def run(fn, *args, **kw):
+        if failed:
+            return None
+        try:
+            return fn(*args, **kw)
+        except L.LbfgsError as e:
+            failed.append(e)
+            print(f"rank {rank}: {e}", file=sys.stderr, flush=True)
+            return None
+
+    def vote(stage):
+        if not D.all_ok(not failed):
+            raise failed[0] if failed else L.LbfgsError(f"{stage} failed on another rank")
+
     if world > 1 and a.exchange in ("xgmi", "auto"):
-        ok, msg = ctx.connect_peers(D.allgather_bytes, D.all_ok)
+        ok, msg = ctx.connect_peers(D.allgather_bytes, D.all_ok)  # collective, its own vote
         if msg:
             print(f"rank {rank}: {msg}", file=sys.stderr, flush=True)
         if not ok and uid is None:
-            raise L.LbfgsError("xGMI peer exchange unavailable and no RCCL communicator")
+            raise L.LbfgsError("xGMI peer exchange unavailable and no RCCL communicator")  # on every rank
         if ok and a.exchange == "auto" and uid is not None:
             # collective calls in the same order on every rank; the slowest rank decides
             # vote after each collective timing, so that no rank enters the RCCL all-gather
@@ -269,39 +413,49 @@ def measure(a, D, n, x0, dev, rank, world, uid, unfused=False, vector_free=False
     # the untimed history fill and warm-up record the trajectory (f, |g|, alpha, x checksums at
     # the top of every iteration) for reference_parity; the timed steps run untraced
     trace = not vector_free
-    ctx.init(a.objective, x0, a.line_search, tolerance=1e-5, unfused=unfused, vector_free=vector_free,
-             trace=trace)
+    run(ctx.init, a.objective, x0, a.line_search, tolerance=1e-5, unfused=unfused, vector_free=vector_free,
+        trace=trace)
     # history fill (untimed, not counted as warm-up): m iterations store m pairs, so every later
     # step uses h = m whatever --warmup is (B_iter grows with h)
-    fill = ctx.step(a.history)
-    ctx.step(a.warmup)
+    fill = run(ctx.step, a.history)
+    run(ctx.step, a.warmup)
     if trace:
-        ctx.trace_enable(False)
-    ctx.sync()
+        run(ctx.trace_enable, False)
+    run(ctx.sync)
+    vote("history fill / warm-up")
     D.barrier()
-    ctx.sync()
+    run(ctx.sync)
     t0 = time.perf_counter()
-    res = ctx.step(a.steps)
-    ctx.sync()
+    res = run(ctx.step, a.steps)
+    run(ctx.sync)
     t_local = time.perf_counter() - t0
     D.barrier()
     T = D.allreduce(t_local, "max")
-    bytes_all = D.allreduce(res["bytes"], "sum")
+    bytes_all = D.allreduce(res["bytes"] if res else 0.0, "sum")
+    vote("timed steps")
+    # this box's rate for the passes' 3 R + 1 W access pattern, on the same buffers, right after
+    # the timed steps (bench lines from different boxes are compared against it)
+    probe = None
+    if box_probe and not a.no_box_probe and res["status"] == "running":
+        probe = run(ctx.stream_probe, 20)
+        gb = D.allreduce(probe["gbps"] if probe and probe["gbps"] else 0.0, "min")
+        vote("box probe")
+        probe = dict(probe, gbps_min_over_ranks=gb) if probe else None
     # roofline region: the same kind of steps again with a HIP event pair around every launch
     # on the solver stream (per-kernel durations; the events add a few us per launch, which
     # is why they are kept out of the timed region above)
     prof = {}
     if not a.no_prof and res["status"] == "running":
-        ctx.prof_reset()
-        ctx.prof_enable(True)
+        run(ctx.prof_reset)
+        run(ctx.prof_enable, True)
         tp = time.perf_counter()
-        ctx.step(min(a.steps, 20))
-        ctx.sync()
+        run(ctx.step, min(a.steps, 20))
+        run(ctx.sync)
         prof_wall_ms = (time.perf_counter() - tp) * 1e3
-        ctx.prof_enable(False)
+        run(ctx.prof_enable, False)
         for kname in L.KERNELS:
-            p = ctx.prof_get(kname)
-            if p["launches"]:
+            p = run(ctx.prof_get, kname)
+            if p and p["launches"]:
                 prof[kname] = p
         # the GPU's busy share of those iterations: kernel time (exchange launches included) over
         # wall time; the rest is launch gaps, host decisions and waits (the events add a few us)
@@ -317,6 +471,7 @@ def measure(a, D, n, x0, dev, rank, world, uid, unfused=False, vector_free=False
                                        "rank0_ms": round(ex["ms"], 3), "rank0_exchanges": ex["launches"],
                                        "rank0_wall_ms": round(prof_wall_ms, 3),
                                        "iterations": min(a.steps, 20)}
+        vote("profiled steps")
     # sharded: the cost of one reduction exchange on this machine, per backend available on
     # every rank (collective calls, same sequence everywhere): the two-loop issues ~2h + 3 of
     # them per iteration, each on the critical path
@@ -326,11 +481,14 @@ def measure(a, D, n, x0, dev, rank, world, uid, unfused=False, vector_free=False
         backends = (["xgmi"] if backend.startswith("xgmi") else []) + (["rccl"] if uid is not None else [])
         for b in backends:
             for k in (8, 96):
-                lat[f"{b}_{k * 8}doubles"] = round(ctx.exchange_latency(b, k, 200), 2)
+                us = run(ctx.exchange_latency, b, k, 200)
+                if us is not None:
+                    lat[f"{b}_{k * 8}doubles"] = round(us, 2)
+        vote("exchange latency")
     if trace:
         res["trajectory"] = ctx.trace()
-    ctx.close()
     res["history_fill"] = fill["iterations"]
+    res["box_probe"] = probe
     done_steps = a.steps if res["status"] == "running" else max(res["iterations"] - a.warmup - fill["iterations"], 1)
     return T, res, prof, bytes_all, done_steps, (backend, lat)
 
@@ -521,6 +679,24 @@ def reference_parity(traj, live, fixture, fsrc):
     return out
 
 
+def box_fields(probe, value, achieved_gbps, world):
+    """This box's HBM rate for the two-loop passes' access pattern (lbfgs_stream_probe: 20 launches
+    of a 3 R + 1 W stream over the solver's own q, y, s in the passes' geometry and cache policy,
+    right after the timed steps; sharded: the slowest rank's) and the line's value against it, so
+    lines from different boxes compare by the code rather than by the box."""
+    if not probe or not probe.get("gbps"):
+        return {"box_copy_tbps": None}
+    gb = probe.get("gbps_min_over_ranks") or probe["gbps"]
+    return {"box_copy_tbps": round(gb / 1e3, 4),
+            "value_per_box_tbps": round(value / (gb / 1e3), 4),
+            "hbm_frac_of_box": round(achieved_gbps / gb, 4),
+            "box_probe": {"kernel": "k_probe_stream (3 R + 1 W, k_axpy_dot's loads and store, no stage 2)",
+                          "avg_launch_us": round(probe["avg_launch_us"], 2), "launches": 20,
+                          "bytes_per_launch": probe["bytes_per_launch"],
+                          "rank0_gbps": round(probe["gbps"], 1),
+                          "over": "slowest rank" if world > 1 else "one GPU"}}
+
+
 def roofline(prof, n, world):
     prof = {k: v for k, v in (prof or {}).items() if not k.startswith("_")}
     streaming = [k for k in prof if prof[k]["bytes"] > 0]  # not the stage-2 / exchange launches
@@ -531,7 +707,7 @@ def roofline(prof, n, world):
     avg_s = p["ms"] / p["launches"] / 1e3
     per_launch = p["bytes"] / p["launches"]  # this rank's algorithmic bytes per launch
     achieved = per_launch / avg_s / 1e9
-    traffic, tsrc = pmc_traffic(dom, n, world)
+    traffic, tsrc, trefused = pmc_traffic(dom, n, world)
     tot = sum(q["ms"] for q in prof.values())
     # every streaming kernel's own rate (algorithmic bytes / event-timed duration), for A/B lines
     rates = {k: {"avg_launch_us": round(prof[k]["ms"] / prof[k]["launches"] * 1e3, 2),
@@ -539,13 +715,19 @@ def roofline(prof, n, world):
              for k in streaming if prof[k]["launches"] and prof[k]["ms"] > 0}
     return dict(bound="hbm", kernel=dom, achieved=round(achieved, 1), peak=HBM_PEAK_GBPS, unit="GB/s",
                 frac=round(achieved / HBM_PEAK_GBPS, 4), traffic=traffic, traffic_unit="bytes/launch",
-                traffic_source=tsrc, bytes_per_launch=per_launch, avg_launch_us=round(avg_s * 1e6, 2),
+                traffic_source=tsrc, traffic_refused=trefused, bytes_per_launch=per_launch, avg_launch_us=round(avg_s * 1e6, 2),
                 launches=p["launches"], kernel_share={k: round(v["ms"] / tot, 4) for k, v in prof.items()},
                 kernel_rates=rates)
 
 
 def main():
     a = parse()
+    if a.gpus > 1 and "RANK" not in os.environ:
+        # no launcher around the command: bench.py starts the ranks itself, before any HIP call
+        sys.exit(self_launch(sys.argv[1:], a.gpus, a.launch_timeout))
+    # load liblbfgs_hip.so (and through it /opt/rocm's HIP runtime and RCCL) before torch can load
+    # its bundled copies: libraries with the same soname are then shared, not duplicated
+    L.lib()
     n = int(a.size)
     D = Dist(a.gpus)
     world, rank = a.gpus, D.rank
@@ -571,10 +753,11 @@ def main():
     fallback = None
     try:
         T, res, prof, bytes_all, done_steps, (backend, xlat) = measure(a, D, n, x0, dev, rank, world, uid,
-                                                      unfused=a.unfused, vector_free=a.vector_free)
+                                                      unfused=a.unfused, vector_free=a.vector_free, box_probe=True)
     except L.LbfgsError as e:
-        # a mailbox failure across GPUs (every rank's wait times out, so every rank lands here):
-        # the line is measured again over RCCL rather than lost, and says why
+        # a mailbox failure across GPUs: measure() raises on every rank together (its votes), so
+        # every rank lands here and the line is measured again over RCCL rather than lost, and
+        # says why
         if not (world > 1 and uid is not None and a.exchange in ("xgmi", "auto")):
             raise
         fallback = f"xgmi: {e}"
@@ -585,7 +768,7 @@ def main():
         a.exchange = "rccl"
         uid = D.broadcast_bytes(L.unique_id() if rank == 0 else None)
         T, res, prof, bytes_all, done_steps, (backend, xlat) = measure(a, D, n, x0, dev, rank, world, uid,
-                                                      unfused=a.unfused, vector_free=a.vector_free)
+                                                      unfused=a.unfused, vector_free=a.vector_free, box_probe=True)
     check = shard_check(a, D, n, x0, dev, rank, world, res) if world > 1 else None
     # the opt-in vector-free mode alongside the default (outside the bit-parity contract with
     # the reference's operation order); sharded runs need a fresh RCCL id
@@ -671,6 +854,7 @@ def main():
             "achieved_hbm_gbps": round(bytes_all / T / 1e9, 1),
             "bytes_per_step": bytes_all / max(done_steps, 1),
             "roofline": roof,
+            **box_fields(res.get("box_probe"), value, bytes_all / T / 1e9, world),
             "exchange_latency_us": xlat,
             "exchange_share": prof.get("_exchange_share"),
             "exchange_fallback": fallback,

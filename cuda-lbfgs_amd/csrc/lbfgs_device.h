@@ -131,6 +131,11 @@ int lbk_exchange_fold(const lbk_ctx* c);
 /* collective: iters back-to-back exchanges of a ks-component slot through backend 1 or 2;
  * host wall time per exchange in microseconds */
 int lbk_exchange_bench(lbk_ctx* c, int backend, int ks, int iters, double* us);
+/* LBFGS_CU_PARTITION: CUs of this rank's solver stream (0: not partitioned) */
+int lbk_cu_partition(const lbk_ctx* c);
+/* box probe: `launches` back-to-back 3 R + 1 W streams over (q, y, s) in the two-loop passes'
+ * geometry and cache policy, q written back unchanged; mean microseconds per launch */
+int lbk_stream_probe(lbk_ctx* c, double* q, const double* y, const double* s, int launches, double* us);
 
 /* memory */
 double* lbk_vec_alloc(lbk_ctx* c);

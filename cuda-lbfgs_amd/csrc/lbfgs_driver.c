@@ -445,6 +445,17 @@ int lbfgs_exchange_latency(lbfgs_ctx* c, int backend, int components, int iters,
     return rc == -1 ? LBFGS_ERR_BAD_ARG : rc == -5 ? LBFGS_ERR_STATE : rc == -3 ? LBFGS_ERR_RCCL : LBFGS_ERR_HIP;
 }
 
+int lbfgs_cu_partition(const lbfgs_ctx* c) { return c ? lbk_cu_partition(c->dev) : LBFGS_ERR_BAD_ARG; }
+
+int lbfgs_stream_probe(lbfgs_ctx* c, int launches, double* us, double* bytes) {
+    if (!c || !us || launches < 1) return LBFGS_ERR_BAD_ARG;
+    if (!c->inited) return LBFGS_ERR_STATE;
+    const int rc = lbk_stream_probe(c->dev, c->q, c->Y[0], c->S[0], launches, us);
+    if (rc != 0) return dev_err(c, rc);
+    if (bytes) *bytes = 32.0 * (double)c->geo->n_loc;
+    return 0;
+}
+
 /* ------------------------------------------------------------------------------------------
  * Host-callback objective (LBFGS_OBJ_HOST; single rank). The device forms every point the
  * objective is called at (z = x + alpha d, as the commit will form x_new) and the host calls

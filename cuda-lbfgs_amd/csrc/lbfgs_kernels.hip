@@ -166,7 +166,36 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
         }                                                                                    \
     } while (0)
     CK(hipSetDevice(device));
-    CK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    // LBFGS_CU_PARTITION=1 (sharded ranks sharing one GPU: tests and one-card rehearsals): rank r's
+    // solver stream runs on CUs [r, r + 1) * cus / world only, so no rank's spinning workgroups can
+    // occupy the CUs a peer's producing pass needs - the forward-progress situation of ranks on
+    // distinct GPUs. The folded exchanges then run ungated (take_fold), exactly the code path they
+    // take across GPUs.
+    c->cu_part = 0;
+    if (const char* e = getenv("LBFGS_CU_PARTITION")) c->cu_part = world > 1 && !grp && atoi(e) != 0;
+    if (c->cu_part) {
+        int cus = 0;
+        CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+        const int per = cus / world;
+        if (per < 1) {
+            snprintf(c->err, sizeof c->err, "LBFGS_CU_PARTITION: %d CUs cannot be split over %d ranks", cus, world);
+            return -1;
+        }
+        std::vector<uint32_t> mask((size_t)(cus + 31) / 32, 0u);
+        for (int i = rank * per; i < (rank + 1) * per; ++i) mask[(size_t)i >> 5] |= 1u << (i & 31);
+        CK(hipExtStreamCreateWithCUMask(&c->stream, (uint32_t)mask.size(), mask.data()));
+        std::vector<uint32_t> got(mask.size(), 0u);
+        CK(hipExtStreamGetCUMask(c->stream, (uint32_t)got.size(), got.data()));
+        c->cu_count = 0;
+        for (size_t i = 0; i < got.size(); ++i) c->cu_count += __builtin_popcount(got[i] & mask[i]);
+        if (c->cu_count != per) {
+            snprintf(c->err, sizeof c->err, "LBFGS_CU_PARTITION: stream CU mask holds %d of rank %d's %d CUs",
+                     c->cu_count, rank, per);
+            return -2;
+        }
+    } else {
+        CK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    }
     CK(hipMalloc(&c->partials, sizeof(double) * LBK_KW * LBK_SEGS));
     CK(hipMalloc(&c->cnt, sizeof(unsigned) * 16));
     CK(hipMalloc(&c->slots, sizeof(double) * LBK_NSLOTS * LBK_SLOT));
@@ -219,6 +248,7 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
         occ = std::min(occ, o);
         CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, k_coop_iter<LBK_OBJ_QUAD_SEPARABLE>, LB_BLOCK, 0));
         occ = std::min(occ, o);
+        if (c->cu_part) cus = c->cu_count;  // the stream sees only its own CUs
         c->coop_max = (int)std::min<int64_t>(c->coop_max, (int64_t)occ * cus);
         // the persistent iteration (LBFGS_PERSIST=1): every workgroup of its grid resident, at most
         // 4 per CU. The occupancy answer is VGPR-bound here (165 VGPRs: 3 per CU), where the API and
@@ -1189,8 +1219,44 @@ int lbk_peer_enable(lbk_ctx* c, int on) {
     c->xg_on = on ? 1 : 0;
     c->xf_on = 0;
     if (on && c->fold_env && c->geo.world > 1 && !c->grp && lbk_xgmi_fold_info(c->xg, &c->xf) == 0 &&
-        (c->fold_env == 2 || !c->xf.shared_device))
+        (c->fold_env == 2 || !c->xf.shared_device || c->cu_part))
         c->xf_on = 1;
+    return 0;
+}
+
+int lbk_cu_partition(const lbk_ctx* c) { return c->cu_part ? c->cu_count : 0; }
+
+int lbk_stream_probe(lbk_ctx* c, double* q, const double* y, const double* s, int launches, double* us) {
+    if (launches < 1 || !us || !q || !y || !s) return -1;
+    HIPCHK(c, hipSetDevice(c->device));
+    {
+        const int rc = flush_pending(c);
+        if (rc) return rc;
+    }
+    if (nblocks(c) <= 0) {
+        *us = 0.0;
+        return 0;
+    }
+    hipEvent_t a = ev_get(c), b = ev_get(c);
+    if (!a || !b) {
+        snprintf(c->err, sizeof c->err, "hipEventCreate failed");
+        return -2;
+    }
+    HIPCHK(c, hipEventRecord(a, c->stream));
+    for (int i = 0; i < launches; ++i) {
+        const Geo g = kgeo(c);  // alternating walk, as the passes
+        NT_DISPATCH(c, hipLaunchKernelGGL(k_probe_stream<NT_>, dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, q, y, s,
+                                          g, c->partials));
+        HIPCHK(c, hipGetLastError());
+        c->rev_par ^= 1;
+    }
+    HIPCHK(c, hipEventRecord(b, c->stream));
+    HIPCHK(c, hipEventSynchronize(b));
+    float ms = 0.f;
+    HIPCHK(c, hipEventElapsedTime(&ms, a, b));
+    c->ev_free.push_back(a);
+    c->ev_free.push_back(b);
+    *us = (double)ms * 1e3 / launches;
     return 0;
 }
 

@@ -2739,6 +2739,21 @@ __global__ void k_checksum(const double* __restrict__ x, int64_t n_loc, int64_t 
     }
 }
 
+// Box probe (lbk_stream_probe; bench.py's box_copy_tbps): the two-loop passes' 3 R + 1 W stream
+// in their own geometry, unroll and cache policy - k_axpy_dot's loads and store with alpha = 0, so
+// q is written back unchanged and the probe can run on the solver's own buffers - and no stage 2.
+// It measures what this box's HBM gives the passes' access pattern, so a bench line can be read
+// against the box it ran on. The dot is kept live (a store nobody reads, almost never taken) so
+// the s loads are not dropped.
+template <bool NT>
+__global__ __launch_bounds__(LB_BLOCK) void k_probe_stream(double* q, const double* __restrict__ y,
+                                                           const double* __restrict__ sv, Geo geo, double* sink) {
+    const Seg s = seg_setup(geo);
+    double acc[1] = {0.0};
+    stream(OpAxpyDot<NT>{q, q, y, sv, 0.0}, s, geo, acc);
+    if (acc[0] == 1.0) sink[blockIdx.x] = acc[0];
+}
+
 }  // namespace
 
 // =========================================================================================
@@ -2857,6 +2872,9 @@ struct lbk_ctx {
     int fold_now;          // the launch in progress pushes its reduction (epoch fold_epoch)
     unsigned fold_epoch;
     int fold_edges;
+    // LBFGS_CU_PARTITION (sharded, tests and one-card rehearsals): the solver stream runs on this
+    // rank's own cu_count CUs, disjoint from every other rank's, as if each rank had a GPU
+    int cu_part, cu_count;
 };
 
 namespace {
@@ -3152,11 +3170,13 @@ void fold_producer(lbk_ctx* c, Red& r, bool edges) {
 FoldSrc take_fold(lbk_ctx* c, int ref) {
     FoldSrc f{nullptr, 0u, nullptr, nullptr, 0ull, nullptr};
     if (c->xf_slot < 0 || ref % LBK_KMAX != 0 || c->xf_slot != ref / LBK_KMAX) return f;
-    if (c->xf.shared_device) {
+    if (c->xf.shared_device && !c->cu_part) {
         // ranks sharing one GPU (forced fold: tests, rehearsals): a consuming pass's workgroups
         // polling in its prologue can hold every CU a peer's producing pass waits for. A
         // one-wavefront gate (the collect kernel) waits first, so the pass launches with the
         // values already in the mailbox and its prologue's poll is the same code, satisfied at once.
+        // With the CUs partitioned between the ranks (cu_part) no rank can hold another's CUs, so
+        // there is no gate: the consumer waits in its prologue exactly as across distinct GPUs.
         hipEvent_t a = nullptr, b = nullptr;
         if (c->prof_on && (a = ev_get(c)) && (b = ev_get(c))) (void)hipEventRecord(a, c->stream);
         if (lbk_xgmi_collect(c->xg, c->stream, slot_base(c, c->xf_slot), slot_stride(c->xf_slot), c->geo.g_lo,

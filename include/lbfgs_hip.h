@@ -196,6 +196,19 @@ int lbfgs_exchange_fold(const lbfgs_ctx* ctx);
  * exchanges of a `components`-wide result slot (8 = a two-loop reduction, up to 96) through
  * backend 1 (RCCL) or 2 (xGMI mailboxes); *us = host wall time per exchange */
 int lbfgs_exchange_latency(lbfgs_ctx* ctx, int backend, int components, int iters, double* us);
+/* LBFGS_CU_PARTITION=1 at context creation (sharded ranks sharing one GPU: tests and one-card
+ * rehearsals of a multi-GPU run): the rank's solver stream is confined to its own cus / world
+ * CUs, disjoint from every other rank's, so the ranks make progress as on distinct GPUs and the
+ * folded exchanges run ungated, as across GPUs. Returns the rank's CU count, 0 when not
+ * partitioned. */
+int lbfgs_cu_partition(const lbfgs_ctx* ctx);
+/* Diagnostic (no reference counterpart): `launches` back-to-back streams of 3 reads + 1 write
+ * over the context's own work and history vectors (q, y, s of the pair pool) in the two-loop
+ * passes' geometry and cache policy, q written back unchanged. *us = mean microseconds per
+ * launch, *bytes = this rank's bytes per launch (32 n_loc). bench.py reports this box's rate for
+ * the passes' access pattern beside the solver's. Call between lbfgs_solver_step calls of an
+ * initialised solve. */
+int lbfgs_stream_probe(lbfgs_ctx* ctx, int launches, double* us, double* bytes);
 /* Emulated ranks: 'world' contexts driven by threads of ONE process (e.g. on one GPU, one
  * stream each) exchange their reductions through host memory instead of RCCL. Same data path
  * and results as the RCCL shards; used to test sharding on a single GPU. */

@@ -25,7 +25,15 @@ lose nothing either, but strings keep every reader honest). Writes tests/golden/
 Only runnable where /root/reference exists (this container): the reference needs ~15 s per
 iteration at n = 1e8 and the m = 20 runs ~40 GB of host memory, so the cases run one at a time.
 
-usage: python tests/golden/make_fullsize.py [config2_n1e8] [config3_n1e8]
+  config4_n1e9  configs[4]: Rosenbrock n = 1e9, m = 10, backtracking. A whole run does not fit
+                this container (~62 GB; every vector is 8 GB), so the fixture holds the first two
+                trace entries only: k = 0 (f, |g| and the x checksums at x0) and k = 1 (the first
+                step alpha_0 and the state after it), in the canonical order, by `first_steps`
+                below (3 vectors resident), which is checked bit for bit against the oracle's
+                whole-run restatement at smaller n before it runs at 1e9; and f(x0), |g(x0)| of
+                the reference itself (maxit = 0: it evaluates f and grad at x0 and stops).
+
+usage: python tests/golden/make_fullsize.py [config2_n1e8] [config3_n1e8] [config4_n1e9]
 """
 import json
 import os
@@ -135,11 +143,95 @@ def make(name):
     print(f"{name}: horizons {hz}", flush=True)
 
 
+def first_steps(x0, backtracking=(1.0, 0.5, 1e-8, 1e-4)):
+    """Trace entries k = 0 and k = 1 of ORC_CANON Rosenbrock with the backtracking search, with x0,
+    g0 and one trial point resident (orc_lbfgs holds ~10 vectors): iteration 0 has no history, so
+    d = -g0 (lbfgs.cpp:87-91); the search (line_search.cpp:19-30, oracle ls_backtracking) halves
+    alpha while f(x) - f(x + alpha d) < c1 alpha g.d; x1 = x + alpha_0 d (lbfgs.cpp:159).
+    x + alpha (-g) is formed as x - (alpha g): negation is exact, so the bits are the same, and
+    g.d = -(g.g) bit for bit (the canonical sums are symmetric under negation); both identities
+    are asserted against the oracle itself in check_first_steps."""
+    a0, beta, tol_a, c1 = backtracking
+    f0 = O.f("rosenbrock", x0)
+    g = O.grad("rosenbrock", x0)
+    gg = O.dot(g, g)
+    gd = -gg
+    alpha = a0
+    t = np.empty_like(x0)
+    while True:
+        np.multiply(g, alpha, out=t)
+        np.subtract(x0, t, out=t)
+        ft = O.f("rosenbrock", t)
+        if not (f0 - ft < c1 * alpha * gd):
+            break
+        alpha *= beta
+        if alpha < tol_a:
+            break
+    np.multiply(g, alpha, out=t)
+    np.subtract(x0, t, out=t)  # x1
+    c0 = O.checksum(x0)
+    del g
+    f1 = O.f("rosenbrock", t)
+    g1 = O.grad("rosenbrock", t)
+    gg1 = O.dot(g1, g1)
+    del g1
+    c1_ = O.checksum(t)
+    return dict(f=[f0, f1], gnorm=[float(np.sqrt(gg)), float(np.sqrt(gg1))], alpha=[alpha],
+                c1=[c0[0], c1_[0]], c2=[c0[1], c1_[1]])
+
+
+def check_first_steps(n, m=10):
+    """first_steps against the oracle's whole run (ORC_CANON, 1 iteration), bit for bit"""
+    x0 = O.x0_uniform(n, 42, -2.0, 2.0)
+    r = O.lbfgs("rosenbrock", x0, "backtracking", m, 1, 1e-5, mode=O.CANON)
+    q = first_steps(x0)
+    g = O.grad("rosenbrock", x0)
+    assert np.float64(O.dot(g, -g)).view(np.uint64) == np.float64(-O.dot(g, g)).view(np.uint64)
+    for k in range(2):
+        assert np.float64(q["f"][k]).view(np.uint64) == r["f"][k:k + 1].view(np.uint64)[0], ("f", n, k)
+        assert np.float64(q["gnorm"][k]).view(np.uint64) == r["gnorm"][k:k + 1].view(np.uint64)[0], ("g", n, k)
+        assert q["c1"][k] == int(r["c1"][k]) and q["c2"][k] == int(r["c2"][k]), ("x", n, k)
+    assert np.float64(q["alpha"][0]).view(np.uint64) == r["alpha"][0:1].view(np.uint64)[0], ("alpha", n)
+    print(f"  first_steps == orc_lbfgs at n={n}: alpha_0 = {q['alpha'][0]!r}", flush=True)
+
+
+def make_config4():
+    """tests/golden/fullsize/config4_n1e9.json (see the module docstring)"""
+    n, m, name = 10 ** 9, 10, "config4_n1e9"
+    for small in (4_000_003, 8192 * 8192 + 1):
+        check_first_steps(small, m)
+    with tempfile.TemporaryDirectory() as tmp:
+        ref = run_reference(("rosenbrock", n, m, "backtracking", 0, 1e-5, 42, -2.0, 2.0, "configs[4]"), tmp)
+    print(f"{name}: reference f(x0), grad(x0) in {ref['seconds']:.0f} s", flush=True)
+    t0 = time.time()
+    x0 = O.x0_uniform(n, 42, -2.0, 2.0)
+    q = first_steps(x0)
+    del x0
+    print(f"{name}: canonical k = 0, 1 in {time.time() - t0:.0f} s: alpha_0 = {q['alpha'][0]!r}", flush=True)
+    meta = dict(case=name, baseline_config="configs[4]", objective="rosenbrock", n=n, m=m, method="backtracking",
+                maxit=1, tol=1e-5, seed=42, lo=-2.0, hi=2.0,
+                reference=dict(f_calls=hexbits(ref["f_calls"]), grad_c1=dec(ref["grad_c"][:, 0]),
+                               grad_c2=dec(ref["grad_c"][:, 1]), grad_norm=hexbits(ref["grad_norm"]),
+                               stdout=ref["stdout"], seconds_in_this_container=round(ref["seconds"], 1),
+                               note="maxit = 0: f and grad at x0 only (lbfgs.cpp:29-30)"),
+                canon=dict(f=hexbits(q["f"]), gnorm=hexbits(q["gnorm"]), alpha=hexbits(q["alpha"]),
+                           c1=[str(v) for v in q["c1"]], c2=[str(v) for v in q["c2"]], entries=2),
+                generator=("tests/golden/make_fullsize.py make_config4: oracle/_ref/ref_lbfgs (the "
+                           "reference's sequential sources) at maxit 0, and first_steps (ORC_CANON, "
+                           "checked against orc_lbfgs at n = 4000003 and 8192^2 + 1)"))
+    os.makedirs(OUT, exist_ok=True)
+    with open(os.path.join(OUT, name + ".json"), "w") as fp:
+        json.dump(meta, fp, indent=1)
+
+
 def main(argv):
     if not os.path.exists(REF_BIN):
         sys.exit("build the reference first: make -C oracle ref")
-    for nm in argv or list(CASES):
-        make(nm)
+    for nm in argv or list(CASES) + ["config4_n1e9"]:
+        if nm == "config4_n1e9":
+            make_config4()
+        else:
+            make(nm)
 
 
 if __name__ == "__main__":

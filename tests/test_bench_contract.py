@@ -12,7 +12,7 @@ sys.path.insert(0, ROOT)
 
 @pytest.fixture(scope="module")
 def bench():
-    import bench as B  # loads liblbfgs_hip.so (no GPU needed to load it)
+    import bench as B  # liblbfgs_hip.so loads on first use (no GPU needed to load it)
 
     return B
 
@@ -35,14 +35,48 @@ def test_roofline_object(bench):
     assert bench.roofline({}, 10 ** 8, 1) is None
 
 
-def test_pmc_traffic_from_committed_profile(bench):
-    traffic, src = bench.pmc_traffic("axpy_dot", 10 ** 8, 1)
-    assert src and src.startswith("profiles/") and os.path.exists(os.path.join(ROOT, src))
-    # corrected PMC bytes per launch within 1 % of the algorithmic 4 vectors x 800 MB
-    assert traffic == pytest.approx(3.2e9, rel=0.01)
-    vf, _ = bench.pmc_traffic("vf_commit", 10 ** 8, 1)
-    assert vf == pytest.approx(26 * 8e8, rel=0.02)
-    assert bench.pmc_traffic("axpy_dot", 10 ** 8, 8) == (None, None)  # per-rank PMC not committed
+def test_pmc_traffic_requires_this_library(bench, tmp_path, monkeypatch):
+    """traffic comes only from a PMC summary profiled on the loaded library (its `_build` carries
+    the library's source hash); a summary of other code is refused and says why; the newest
+    round wins; sharded lines have no per-rank PMC."""
+    import json
+
+    lib = bench.L.build_info()[0]
+    (tmp_path / "profiles" / "r01").mkdir(parents=True)
+    (tmp_path / "profiles" / "r02").mkdir(parents=True)
+    entry = {"k_axpy_dot<true, false>": {"hbm_bytes_per_launch": 3.2e9}, "k_vf_commit<0, 10, true>":
+             {"hbm_bytes_per_launch": 2.08e10}}
+    (tmp_path / "profiles" / "r01" / "pmc_bench_n1e8.json").write_text(json.dumps(dict(entry, _build={"library": lib})))
+    (tmp_path / "profiles" / "r02" / "pmc_bench_n1e8.json").write_text(
+        json.dumps(dict(entry, _build={"library": "src=0000000000000000 built=x arch=gfx950"})))
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    t, src, why = bench.pmc_traffic("axpy_dot", 10 ** 8, 1)
+    assert t == 3.2e9 and src == "profiles/r01/pmc_bench_n1e8.json"
+    assert bench.pmc_traffic("vf_commit", 10 ** 8, 1)[0] == 2.08e10
+    (tmp_path / "profiles" / "r01" / "pmc_bench_n1e8.json").unlink()
+    t, src, why = bench.pmc_traffic("axpy_dot", 10 ** 8, 1)
+    assert t is None and src is None and "profiles/r02/pmc_bench_n1e8.json" in why and "src=0000" in why
+    assert bench.pmc_traffic("axpy_dot", 10 ** 8, 8) == (None, None, None)  # per-rank PMC not committed
+    r = bench.roofline({"axpy_dot": {"ms": 560.0, "launches": 1000, "bytes": 3.2e12}}, 10 ** 8, 1)
+    assert r["traffic"] is None and r["traffic_refused"] == why
+
+
+def test_committed_pmc_summaries_record_their_library(bench):
+    """every committed PMC summary from round 4 on names the library it was profiled on"""
+    import glob
+    import json
+
+    for fn in glob.glob(os.path.join(ROOT, "profiles", "r0[4-9]", "**", "pmc_bench_n*.json"), recursive=True):
+        b = json.load(open(fn)).get("_build") or {}
+        assert b.get("library", "").startswith("src="), fn
+
+
+def test_box_fields(bench):
+    p = {"avg_launch_us": 500.0, "bytes_per_launch": 3.2e9, "gbps": 6400.0, "gbps_min_over_ranks": 6400.0}
+    f = bench.box_fields(p, 90.0, 5900.0, 1)
+    assert f["box_copy_tbps"] == 6.4 and f["value_per_box_tbps"] == pytest.approx(90.0 / 6.4, rel=1e-3)
+    assert f["hbm_frac_of_box"] == pytest.approx(5900.0 / 6400.0, rel=1e-3)
+    assert bench.box_fields(None, 90.0, 5900.0, 1) == {"box_copy_tbps": None}
 
 
 def test_cpu_baseline_runner(bench):

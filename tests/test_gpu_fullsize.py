@@ -6,6 +6,12 @@
   relative of the reference itself over the reference's own order-sensitivity horizon
   (tests/golden/fullsize/*.json, made by tests/golden/make_fullsize.py from oracle/_ref/ref_lbfgs
   — the reference's sequential sources — and the oracle, which reproduces that run call for call).
+* configs[4] at its own size (n = 1e9, m = 10, backtracking): 8 processes over the mailboxes
+  with the CUs partitioned between them (LBFGS_CU_PARTITION=1: the folded exchanges ungated, as
+  on 8 distinct GPUs), history filled to h = 10, then 3 steps; bit-identical to the one-GPU run
+  at n = 1e9 (240 GB resident), whose first two trace entries are bit-exact with the canonical
+  fixture and whose f(x0), |g(x0)| are within 1e-10 of the reference's own
+  (tests/golden/fullsize/config4_n1e9.json).
 * configs[4]'s exchange exactly as bench.py's config4() runs it: 8 processes, no RCCL
   communicator (the xGMI peer mailboxes alone), the ticket stage 2 of segments >= 8192 elements
   (n = 8192^2 + 1, the smallest such n, L = 8320), m = 10, backtracking and Wolfe, plus the
@@ -88,6 +94,44 @@ def test_fullsize_parity(name):
     if fx["method"] == "backtracking":
         assert r["tr_c1"][1] == int(fx["reference"]["grad_c1"][1])
         assert r["tr_c2"][1] == int(fx["reference"]["grad_c2"][1])
+
+
+N9 = 10 ** 9
+
+
+@pytest.mark.timeout(1200)
+def test_config4_n1e9_8_processes_cu_partitioned(tmp_path):
+    fx = json.load(open(os.path.join(FULLSIZE, "config4_n1e9.json")))
+    assert (fx["n"], fx["m"], fx["method"]) == (N9, 10, "backtracking")
+    iters = 13  # the history fill (h reaches m = 10) and 3 steps with the ring full
+    outs = run_ranks(tmp_path, 8, N9, 10, "rosenbrock", "backtracking", iters, "steps",
+                     env={"LBFGS_CU_PARTITION": "1"},
+                     unset=("LBFGS_TICKET", "LBFGS_XGMI_MIRROR", "LBFGS_XGMI_FOLD"), timeout=900)
+    x0 = L.x0_uniform(N9, 42, -2.0, 2.0)
+    with L.Context(N9, 10) as c:
+        c.init("rosenbrock", x0, "backtracking", tolerance=1e-5, trace=True)
+        del x0
+        r = c.step(iters)
+        c.sync()
+        tr = c.trace()
+    assert r["status"] == "running" and r["h_max"] == 10
+    for k, o in enumerate(outs):
+        assert bool(o["folded"]) and int(o["cu_part"]) > 0, k
+        assert str(o["status"]) == "running" and int(o["h_max"]) == 10, k
+        for key in ("tr_f", "tr_gnorm", "tr_alpha"):
+            assert np.array_equal(bits(o[key]), bits(tr[key])), (k, key)
+        assert np.array_equal(o["tr_c1"], tr["tr_c1"]) and np.array_equal(o["tr_c2"], tr["tr_c2"]), k
+    # the canonical order's first two entries (x0 and the first step), bit for bit
+    can = fx["canon"]
+    assert np.array_equal(bits(tr["tr_f"][:2]), bits(f64(can["f"])))
+    assert np.array_equal(bits(tr["tr_gnorm"][:2]), bits(f64(can["gnorm"])))
+    assert np.array_equal(bits(tr["tr_alpha"][:1]), bits(f64(can["alpha"])))
+    assert np.array_equal(tr["tr_c1"][:2], u64(can["c1"])) and np.array_equal(tr["tr_c2"][:2], u64(can["c2"]))
+    # the reference itself at x0: f and |g| within 1e-10 relative; x0 has the reference's bits
+    ref = fx["reference"]
+    f_ref, g_ref = f64(ref["f_calls"])[0], f64(ref["grad_norm"])[0]
+    assert abs(tr["tr_f"][0] - f_ref) <= TOL * abs(f_ref) and abs(tr["tr_gnorm"][0] - g_ref) <= TOL * abs(g_ref)
+    assert tr["tr_c1"][0] == int(ref["grad_c1"][0]) and tr["tr_c2"][0] == int(ref["grad_c2"][0])
 
 
 N4 = 8192 * 8192 + 1

@@ -103,6 +103,41 @@ def test_xgmi_folded_exchange_bit_exact(tmp_path, world, obj, ls, mode):
     assert np.array_equal(bits(x), bits(ref["x"]))
 
 
+@pytest.mark.parametrize("world,obj,ls,mode", [
+    (2, "rosenbrock", "backtracking", "default"),
+    (4, "rosenbrock", "wolfe", "default"),
+    (8, "rosenbrock", "backtracking", "default"),
+    (8, "quad_tridiag", "wolfe", "default"),
+    (4, "rosenbrock", "interpolation", "default"),
+    (4, "rosenbrock", "backtracking", "vf"),
+    (8, "rosenbrock", "backtracking_wolfe", "vf"),
+])
+@pytest.mark.parametrize("ticket", ["0", "1"])
+def test_xgmi_ungated_fold_cu_partitioned(tmp_path, world, obj, ls, mode, ticket):
+    """The folded exchanges exactly as ranks on distinct GPUs run them: the library's default fold
+    setting (LBFGS_XGMI_FOLD unset) with every rank's stream confined to its own 1/world of the
+    CUs (LBFGS_CU_PARTITION=1), so no collect gate runs before a consuming pass and its workgroups
+    wait for the peers' pushes in their prologue (src_total_mailbox) while those producers run on
+    CUs of their own. Both producers: the reduce kernel's workgroups (ticket 0) and the group's
+    last arriving workgroup (ticket 1). Bit-identical to one GPU."""
+    n, m, iters = 4_000_003, 5, 12
+    x0 = L.x0_uniform(n, 42, -2.0, 2.0)
+    with L.Context(n, m) as c:
+        ref = c.minimize(obj, x0, ls, iters, trace=True, vector_free=(mode == "vf"))
+    outs = run_ranks(tmp_path, world, n, m, obj, ls, iters, mode,
+                     env={"LBFGS_TICKET": ticket, "LBFGS_CU_PARTITION": "1"}, unset=("LBFGS_XGMI_FOLD",))
+    x = np.zeros(n)
+    for r, o in enumerate(outs):
+        assert bool(o["folded"]) and int(o["cu_part"]) == int(outs[0]["cu_part"]) > 0, (r, o["folded"], o["cu_part"])
+        for key in ("tr_f", "tr_gnorm", "tr_alpha"):
+            assert np.array_equal(bits(o[key]), bits(ref[key])), (r, key)
+        assert np.array_equal(o["tr_c1"], ref["tr_c1"]) and np.array_equal(o["tr_c2"], ref["tr_c2"]), r
+        lo = int(o["lo"])
+        x[lo:lo + len(o["x"])] = o["x"]
+        assert str(o["messages"]) == ref["messages"]
+    assert np.array_equal(bits(x), bits(ref["x"]))
+
+
 def test_xgmi_fold_off_on_a_shared_gpu(tmp_path):
     """Ranks sharing one GPU do not fold by default (a pass's spinning workgroups could hold the CUs
     the peer's producing kernel waits for); the exchange kernel carries their reductions."""
@@ -154,15 +189,21 @@ def test_xgmi_silent_peer_times_out(tmp_path):
     assert procs[1].returncode == 0, outs[1][-2000:]
 
 
-@pytest.mark.parametrize("fold", ["0", "2"])
+@pytest.mark.parametrize("fold", ["0", "2", "cu"])
 def test_xgmi_stalled_peer_fails_once(tmp_path, fold):
     """A peer that connects and then stops exchanging: the solving rank's first wait times out
     (LBFGS_XGMI_TIMEOUT = 3 s) and every exchange queued behind it ends within ~1/65536 of that
     once the error word is set, so the solve fails in about one timeout, not one per exchange
     queued before the host's next synchronisation (with the fold forced, the gated consumers'
-    collect launches wait the same way). The stalled rank stays alive meanwhile, so its mailbox
-    stays mapped."""
-    e = dict(os.environ, LBFGS_XGMI_TIMEOUT="3", XGMI_STALL_S="25", LBFGS_XGMI_FOLD=fold)
+    collect launches wait the same way; "cu": the CUs partitioned, the fold ungated as across
+    GPUs, so the consuming passes' own prologues time out). The stalled rank stays alive
+    meanwhile, so its mailbox stays mapped."""
+    e = dict(os.environ, LBFGS_XGMI_TIMEOUT="3", XGMI_STALL_S="25")
+    if fold == "cu":
+        e.pop("LBFGS_XGMI_FOLD", None)
+        e["LBFGS_CU_PARTITION"] = "1"
+    else:
+        e["LBFGS_XGMI_FOLD"] = fold
     args = [str(tmp_path), "", "2", "4000003", "5", "rosenbrock", "backtracking", "40", ""]
     procs = []
     for r, mode in ((0, "expect_fail"), (1, "stall")):

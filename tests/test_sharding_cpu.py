@@ -81,3 +81,89 @@ def test_bench_distributed_bootstrap_gloo_world2():
     assert all(r[3] == 6.0 for r in res)  # sum over ranks (bench's byte count)
     assert all(r[4] for r in res)  # peer handles gathered in rank order
     assert all(r[5] and not r[6] for r in res)  # one failing rank vetoes the peer exchange everywhere
+
+
+STUB = '''
+import json, os, sys
+sys.path.insert(0, {root!r})
+import bench
+
+rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+mode = sys.argv[1]
+if mode == "fail" and rank == 1:
+    sys.exit(3)  # before the barrier: rank 0 would wait there forever
+D = bench.Dist(world)
+D.barrier()
+tmax = D.allreduce(float(rank), "max")
+if rank == 0:
+    print(json.dumps({{"world": world, "tmax": tmax, "local_rank": os.environ["LOCAL_RANK"],
+                      "master": os.environ["MASTER_ADDR"], "argv": sys.argv[1:]}}), flush=True)
+D.close()
+'''
+
+
+def _launch(tmp_path, world, mode, timeout=120.0):
+    import subprocess
+
+    stub = tmp_path / "stub_rank.py"
+    stub.write_text(STUB.format(root=ROOT))
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_PORT")}
+    code = (f"import sys; sys.path.insert(0, {ROOT!r}); import bench; "
+            f"sys.exit(bench.self_launch([{mode!r}], {world}, {timeout}, script={str(stub)!r}))")
+    return subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=180)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_bench_self_launch_starts_ranks(tmp_path, world):
+    """bench.py --gpus N > 1 with no launcher: self_launch starts N rank processes with the
+    torch.distributed env (127.0.0.1, a free port), they rendezvous over gloo, and rank 0's one
+    JSON line is the launcher's only stdout (the driver's N > 1 command shape, no wrapper)."""
+    import json
+
+    p = _launch(tmp_path, world, "ok")
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, p.stdout
+    d = json.loads(lines[0])
+    assert d == {"world": world, "tmax": float(world - 1), "local_rank": "0", "master": "127.0.0.1", "argv": ["ok"]}
+
+
+def test_bench_self_launch_stops_on_a_failed_rank(tmp_path):
+    """a rank that fails ends the launch at once with its status; the rank left waiting in a
+    collective for it is stopped, not left hanging until the time limit"""
+    import time
+
+    t0 = time.time()
+    p = _launch(tmp_path, 2, "fail", timeout=150.0)
+    assert p.returncode == 3, (p.returncode, p.stderr[-2000:])
+    assert time.time() - t0 < 90 and "rank 1 exited with status 3" in p.stderr
+
+
+def test_bench_self_launch_time_limit(tmp_path):
+    """past the launch time limit every rank is stopped and the status is 124"""
+    p = _launch(tmp_path, 2, "fail", timeout=3.0)  # rank 1 fails too, but the limit may come first
+    assert p.returncode in (3, 124)
+    stub = tmp_path / "sleeper.py"
+    stub.write_text("import time; time.sleep(600)\n")
+    import subprocess
+
+    code = (f"import sys; sys.path.insert(0, {ROOT!r}); import bench; "
+            f"sys.exit(bench.self_launch([], 2, 2.0, script={str(stub)!r}))")
+    q = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert q.returncode == 124 and "time limit" in q.stderr
+
+
+def test_bench_main_self_launches_without_rank(monkeypatch):
+    """main() takes the launcher branch before loading the library when --gpus > 1 and RANK is
+    unset, and passes its own argv through"""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    calls = []
+    monkeypatch.delenv("RANK", raising=False)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "2", "--steps", "3", "--launch-timeout", "77"])
+    monkeypatch.setattr(bench, "self_launch", lambda argv, world, timeout: calls.append((argv, world, timeout)) or 0)
+    monkeypatch.setattr(bench.L, "lib", lambda: pytest.fail("library loaded before the launch"))
+    with pytest.raises(SystemExit) as e:
+        bench.main()
+    assert e.value.code == 0 and calls == [(["--gpus", "2", "--steps", "3", "--launch-timeout", "77"], 2, 77.0)]

@@ -8,6 +8,9 @@ Bootstrap through files in a shared directory (each rank writes its handle, wait
 then the same for the connect verdict), so no torch import is needed.
 
     python xgmi_worker.py DIR RANK WORLD N M OBJ LS ITERS MODE
+
+LBFGS_CU_PARTITION=1 in the environment confines each rank's solver stream to its own CUs (the
+forward-progress situation of distinct GPUs; the folded exchanges then run ungated).
 """
 import os
 import sys
@@ -85,11 +88,24 @@ def main():
         ctx.close()
         print(f"rank {rank}: {us8:.2f} / {us96:.2f} us per exchange", flush=True)
         return
+    if mode == "steps":  # configs[4] sizes: init + step as bench.py's config4() (no full-size x back)
+        t0 = time.time()
+        ctx.init(obj, x0, ls, tolerance=1e-5, trace=True)
+        del x0
+        r = ctx.step(iters)
+        ctx.sync()
+        tr = ctx.trace()
+        np.savez(os.path.join(d, f"out{rank}.npz"), status=r["status"], iterations=r["iterations"], f=r["f"],
+                 gnorm=r["gnorm"], h_max=r["h_max"], folded=folded, cu_part=ctx.cu_partition,
+                 seconds=time.time() - t0, **tr)
+        ctx.close()
+        print(f"rank {rank}: {r['status']} after {r['iterations']} iterations, f={r['f']!r}", flush=True)
+        return
     r = ctx.minimize(obj, x0, ls, iters, trace=True, vector_free=(mode == "vf"))
     lo, nl = ctx.elem_lo, ctx.n_loc
     np.savez(os.path.join(d, f"out{rank}.npz"), tr_f=r["tr_f"], tr_gnorm=r["tr_gnorm"], tr_alpha=r["tr_alpha"],
              tr_c1=r["tr_c1"], tr_c2=r["tr_c2"], x=r["x"][lo:lo + nl], lo=lo, status=r["status"],
-             messages=r["messages"], folded=folded)
+             messages=r["messages"], folded=folded, cu_part=ctx.cu_partition)
     ctx.close()
     print(f"rank {rank}: {r['status']} after {r['iterations']} iterations, f={r['f']!r}", flush=True)
 

@@ -1,7 +1,11 @@
 #!/usr/bin/env python3
 """Summarise rocprofv3 outputs into profiles/: kernel stats (trace) and PMC byte counters.
 
-usage: python tools/pmc_summary.py <trace_dir> <fetch_dir> <write_dir> <out.json> [n]
+usage: python tools/pmc_summary.py <trace_dir> <fetch_dir> <write_dir> <out.json> [n [bench_log ...]]
+
+bench_log: the output of the profiled bench runs; the `build` of their JSON line (the library's
+source hash, lbfgs_build_info) is recorded as `_build`, and every log must name the same library.
+bench.py's pmc_traffic() only takes traffic from a summary whose `_build` is the loaded library's.
 
 FETCH_SIZE / WRITE_SIZE are in KiB per dispatch. On gfx950 FETCH_SIZE counts half of the bytes
 of wide (16 B/lane) coalesced streaming reads (MI355X_MICROARCH.md §HBM), so the corrected HBM
@@ -34,8 +38,31 @@ def short(name):
     return m.group(1) if m else name[:40]
 
 
-def main(trace_dir, fetch_dir, write_dir, out, n=None):
+def build_of(logs):
+    """the `build` object of the bench JSON line in each log; all must agree"""
+    seen = []
+    for fn in logs:
+        for line in open(fn):
+            if line.startswith("{"):
+                try:
+                    d = json.loads(line)
+                except ValueError:
+                    continue
+                if "build" in d:
+                    seen.append((fn, d["build"]))
+    libs = {b.get("library") for _, b in seen}
+    if len(libs) > 1:
+        raise SystemExit(f"profiled runs name different libraries: {seen}")
+    return seen[0][1] if seen else None
+
+
+def main(trace_dir, fetch_dir, write_dir, out, n=None, logs=()):
     res = collections.OrderedDict()
+    if logs:
+        b = build_of(logs)
+        if b is None:
+            raise SystemExit(f"no bench JSON line with a build field in {logs}")
+        res["_build"] = b
     for r in csv.DictReader(open(find(trace_dir, "run_kernel_stats.csv"))):
         k = short(r["Name"])
         res.setdefault(k, {})
@@ -48,6 +75,8 @@ def main(trace_dir, fetch_dir, write_dir, out, n=None):
         for k, v in agg.items():
             res.setdefault(k, {})[tag + "_KiB"] = sum(v) / len(v)
     for k, v in res.items():
+        if k.startswith("_"):
+            continue
         if "FETCH_SIZE_KiB" in v and "WRITE_SIZE_KiB" in v:
             rd = 2 * v["FETCH_SIZE_KiB"] * 1024
             wr = v["WRITE_SIZE_KiB"] * 1024
@@ -61,9 +90,13 @@ def main(trace_dir, fetch_dir, write_dir, out, n=None):
                 v["measured_GBps"] = (rd + wr) / (v["avg_us"] * 1e-6) / 1e9
     json.dump(res, open(out, "w"), indent=1)
     for k, v in res.items():
+        if k.startswith("_"):
+            print(f"{k}: {v}")
+            continue
         print(f"{k:34s} " + " ".join(f"{kk}={vv:.4g}" if isinstance(vv, float) else f"{kk}={vv}"
                                       for kk, vv in v.items()))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2], sys.argv[3], sys.argv[4], float(sys.argv[5]) if len(sys.argv) > 5 else None)
+    main(sys.argv[1], sys.argv[2], sys.argv[3], sys.argv[4], float(sys.argv[5]) if len(sys.argv) > 5 else None,
+         sys.argv[6:])
