@@ -149,6 +149,10 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
     // 3072 elements; LBFGS_COLLECT=0/1 overrides
     c->collect_on = G.L >= 3072 ? 1 : 0;
     if (const char* e = getenv("LBFGS_COLLECT")) c->collect_on = atoi(e) != 0;
+    // a collector waits for its group's other workgroups (at most 8 waiters per launch, all others
+    // wait-free: the wait ends unless the GPU is time-shared with something that holds it)
+    c->collect_timeout_s = 10.0;
+    if (const char* e = getenv("LBFGS_COLLECT_TIMEOUT")) c->collect_timeout_s = std::max(0.1, atof(e));
     // sharded slots are completed by the exchange on the device: those fetch with a copy
     c->direct = world == 1 ? 1 : 0;
     if (const char* e = getenv("LBFGS_DIRECT")) c->direct = world == 1 && atoi(e) != 0;
@@ -156,6 +160,8 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
     // the ranks share the card; the saved copy is ~1 % of an 8-GPU iteration at best: opt-in
     c->xg_mirror = 0;
     if (const char* e = getenv("LBFGS_XGMI_MIRROR")) c->xg_mirror = atoi(e) != 0;
+    c->vf_dma = 0;
+    if (const char* e = getenv("LBFGS_VF_DMA")) c->vf_dma = atoi(e) != 0;
     *out = c;
 #define CK(expr)                                                                             \
     do {                                                                                     \
@@ -250,45 +256,62 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
         occ = std::min(occ, o);
         if (c->cu_part) cus = c->cu_count;  // the stream sees only its own CUs
         c->coop_max = (int)std::min<int64_t>(c->coop_max, (int64_t)occ * cus);
-        // the persistent iteration (LBFGS_PERSIST=1): every workgroup of its grid resident, at most
-        // 4 per CU. The occupancy answer is VGPR-bound here (165 VGPRs: 3 per CU), where the API and
-        // the hardware agree; MI355X_MICROARCH.md's one-short case is SGPR-bound (82-98 SGPRs at
-        // 7-8 per CU). A grid that does not fit still ends: every flagged wait times out (2 s).
-        int po = 1 << 30;
-        CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, (k_persist_iter<LBK_OBJ_ROSENBROCK, true>), LB_BLOCK, 0));
-        po = std::min(po, o);
-        CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, (k_persist_iter<LBK_OBJ_QUAD_TRIDIAG, true>), LB_BLOCK, 0));
-        po = std::min(po, o);
-        CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, (k_persist_iter<LBK_OBJ_QUAD_SEPARABLE, true>), LB_BLOCK, 0));
-        po = std::min(po, o);
+        // the persistent forms: every workgroup of their grid resident, at most `cap` per CU (the
+        // occupancy answer is VGPR-bound here, where the API and the hardware agree;
+        // MI355X_MICROARCH.md's one-short case is SGPR-bound, 82-98 SGPRs at 7-8 per CU). A grid that
+        // does not fit still ends: every flagged wait times out (2 s).
         int cap = 4;  // workgroups per CU (A/B: LBFGS_PERSIST_WG)
         if (const char* e = getenv("LBFGS_PERSIST_WG")) cap = std::max(1, atoi(e));
-        c->persist_gmax = std::min(po, cap) * cus;
-        // the persistent two-loop (LBFGS_PERSIST=2) without the commit's registers
-        CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, k_persist_twoloop<true>, LB_BLOCK, 0));
-        po = o;
-        CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, k_persist_twoloop<false>, LB_BLOCK, 0));
-        po = std::min(po, o);
-        c->persist2_gmax = std::min(po, cap) * cus;
-        // an LDS reservation that lets exactly `cap` workgroups onto a CU, so the dispatcher spreads
-        // the resident grid evenly (without it two workgroups can share a CU while another idles;
-        // A/B LBFGS_PERSIST_LDS=0)
-        c->persist_lds = 0;
+        // LDS per CU from the device (160 KiB on gfx950): the reservation below and the occupancy
+        // queries use the same figure
+        int lds_cu = 0;
+        CK(hipDeviceGetAttribute(&lds_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, device));
         int lds_on = 1;
         if (const char* e = getenv("LBFGS_PERSIST_LDS")) lds_on = atoi(e) != 0;
-        if (lds_on) {
-            c->persist_lds = 160 * 1024 / (cap + 1) + 1024;
-            (void)hipFuncSetAttribute((const void*)k_persist_twoloop<true>, hipFuncAttributeMaxDynamicSharedMemorySize, c->persist_lds);
-            (void)hipFuncSetAttribute((const void*)k_persist_twoloop<false>, hipFuncAttributeMaxDynamicSharedMemorySize, c->persist_lds);
-#define PSET(O)                                                                                                        \
-    (void)hipFuncSetAttribute((const void*)k_persist_iter<O, true>, hipFuncAttributeMaxDynamicSharedMemorySize, c->persist_lds); \
-    (void)hipFuncSetAttribute((const void*)k_persist_iter<O, false>, hipFuncAttributeMaxDynamicSharedMemorySize, c->persist_lds)
+        c->persist_lds = lds_on && lds_cu > 0 ? lds_cu / (cap + 1) + 1024 : 0;
+        c->persist_gmax = 0;
+#if LBK_PERSIST_ITER
+        // the whole iteration (LBFGS_PERSIST=1, variant builds only; 165 VGPRs: 3 per CU)
+        int po = 1 << 30;
+        CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, (k_persist_iter<LBK_OBJ_ROSENBROCK, true>), LB_BLOCK, c->persist_lds));
+        po = std::min(po, o);
+        CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, (k_persist_iter<LBK_OBJ_QUAD_TRIDIAG, true>), LB_BLOCK, c->persist_lds));
+        po = std::min(po, o);
+        CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, (k_persist_iter<LBK_OBJ_QUAD_SEPARABLE, true>), LB_BLOCK, c->persist_lds));
+        po = std::min(po, o);
+        c->persist_gmax = std::min(po, cap) * cus;
+#else
+        int po = 0;
+#endif
+        // the persistent two-loop (LBFGS_PERSIST=2) without the commit's registers; its LDS
+        // reservation lets exactly `cap` workgroups onto a CU, so the dispatcher spreads the resident
+        // grid evenly (without it two workgroups can share a CU while another idles; A/B
+        // LBFGS_PERSIST_LDS=0). A kernel the reservation cannot be granted to turns the mode off.
+        bool lds_ok = true;
+        if (c->persist_lds) {
+            lds_ok &= hipFuncSetAttribute((const void*)k_persist_twoloop<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                          c->persist_lds) == hipSuccess;
+            lds_ok &= hipFuncSetAttribute((const void*)k_persist_twoloop<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                          c->persist_lds) == hipSuccess;
+#if LBK_PERSIST_ITER
+#define PSET(O)                                                                                                            \
+    lds_ok &= hipFuncSetAttribute((const void*)k_persist_iter<O, true>, hipFuncAttributeMaxDynamicSharedMemorySize,         \
+                                  c->persist_lds) == hipSuccess;                                                           \
+    lds_ok &= hipFuncSetAttribute((const void*)k_persist_iter<O, false>, hipFuncAttributeMaxDynamicSharedMemorySize,        \
+                                  c->persist_lds) == hipSuccess
             PSET(LBK_OBJ_ROSENBROCK);
             PSET(LBK_OBJ_QUAD_TRIDIAG);
             PSET(LBK_OBJ_QUAD_SEPARABLE);
 #undef PSET
+#endif
             (void)hipGetLastError();
         }
+        CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, k_persist_twoloop<true>, LB_BLOCK, c->persist_lds));
+        po = o;
+        CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, k_persist_twoloop<false>, LB_BLOCK, c->persist_lds));
+        po = std::min(po, o);
+        c->persist2_gmax = lds_ok ? std::min(po, cap) * cus : 0;
+        if (!lds_ok) c->persist_gmax = 0;
     }
     c->persist_on = 0;
     if (const char* e = getenv("LBFGS_PERSIST")) c->persist_on = atoi(e);  // 1: whole iteration, 2: two-loop
@@ -788,6 +811,12 @@ int lbk_twoloop_persist(lbk_ctx* c, int h, const double* g, double* q, double* r
                         int slot_a0, int slot_b0) {
     const int nb = lbk_twoloop_ok(c, h) ? persist_grid(c, 2, c->persist2_gmax) : 0;
     if (!nb) return -1;
+    // p0_ref's slot is read directly (slot_total) by the kernel: a stage 2 still pending for it
+    // (deferred, or a folded exchange) must land first
+    {
+        const int rc = flush_pending(c);
+        if (rc) return rc;
+    }
     SmallArgs a;
     memset(&a, 0, sizeof a);
     a.h = h;
@@ -910,6 +939,7 @@ int lbk_small_iter(lbk_ctx* c, int obj, int h, const double* g, double* q, doubl
         }
         c->coop_base += (unsigned long long)passes;
         geo.rev = 0;
+#if LBK_PERSIST_ITER
         if (persist) {
             a.partials = c->partials;
             a.pcnt = c->persist_cnt;
@@ -925,6 +955,7 @@ int lbk_small_iter(lbk_ctx* c, int obj, int h, const double* g, double* q, doubl
                 });
             });
         }
+#endif
         const int nb = (int)c->geo.nseg;
         return launch(c, LBK_K_SMALL_ITER, vec, -1, [&] {
             switch (obj) {

@@ -477,10 +477,14 @@ __device__ __forceinline__ void reduce_publish(double (&acc)[K], const Geo& geo,
     // wave per SIMD of registers)
     if constexpr (K <= LBK_KMAX) {
     if (red.ll) {
-        // collect: the partial as flagged words, no wait; the group's last-dispatched workgroup
-        // (highest block index: the group's last segment, or its first when the walk is
-        // reversed) forms the group tree from them. It waits only for workgroups dispatched
-        // before it, none of which waits on anything, so the wait always ends.
+        // collect: the partial as flagged words, no wait; one workgroup per group - the one on
+        // the group's last segment in walk order (highest block index of the group: its last
+        // segment, or its first when the walk is reversed) - forms the group tree from them.
+        // Forward progress does not rest on dispatch order (on a multi-XCD part workgroups go
+        // round-robin over the XCDs, so there is none across the grid): a launch has at most
+        // LBK_GROUPS = 8 waiting collectors and every other workgroup is wait-free, so the
+        // producers always find CUs and every wait ends. On a GPU time-shared with other work the
+        // wait is bounded by the collect timeout (LBFGS_COLLECT_TIMEOUT, 10 s), then NaN + error.
         if (t == 0) {
 #pragma unroll
             for (int k = 0; k < K; ++k)
@@ -1762,6 +1766,38 @@ struct OpVfCommit {
 #pragma unroll
         for (int l = 0; l < 2 * HB; ++l)
             if (l < 2 * B.h) r.b[l] = ldv<NT>(B.b[l] + i);
+        form(r);
+    }
+    // LDS-DMA form (stream_vf_dma): basis vectors l < ND of the row already sit in this wave's
+    // LDS rows (lane's 16 B at dma + l * 128 + 2 lane), the rest and x, g come from memory
+    template <int ND>
+    __device__ void load_dma(Row& r, int64_t i, const double* dma, int lane) const {
+        r.x = ldx<NT>(x + i);
+        r.g = ldx<NT>(g + i);
+#pragma unroll
+        for (int l = 0; l < 2 * HB; ++l) {
+            if (l < 2 * B.h) {
+                if (l < ND)
+                    r.b[l] = *reinterpret_cast<const double2*>(dma + l * 128 + 2 * lane);
+                else
+                    r.b[l] = ldv<NT>(B.b[l] + i);
+            }
+        }
+    }
+    // DMA of the basis rows l < min(ND, 2h) of local element i (this lane's 16 B) into the wave's
+    // LDS rows: one wave-instruction per 1-KiB row, no registers (global_load_lds_dwordx4)
+    template <int ND>
+    __device__ void dma_row(int64_t i, double* dma) const {
+#pragma unroll
+        for (int l = 0; l < ND; ++l)
+            if (l < 2 * B.h)
+                __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(B.b[l] + i),
+                                                 (__attribute__((address_space(3))) void*)(dma + l * 128), 16, 0,
+                                                 NT ? 2 /* nt */ : 0);
+    }
+    // d, z = x + alpha d and the candidate points from the loaded row (every basis product
+    // rounded, l ascending, then g: the ORC_CANON_VF order)
+    __device__ void form(Row& r) const {
         double2 d = make_double2(0.0, 0.0);
 #pragma unroll
         for (int l = 0; l < 2 * HB; ++l) {
@@ -1932,14 +1968,90 @@ __device__ __forceinline__ void stream_vf(const Op& op, const Seg& s, const Geo&
     if (last_lane && pvalid) op.finish(pz_m, pz_c, zedge, px, pg, park[s.w], pi, pe, pzc, zedge_c, acc);
 }
 
-template <int OBJ, int HB, bool NT>
+// The same walk over a full segment with the next row's basis in flight (LBFGS_VF_DMA): the row's
+// first ND basis vectors travel by LDS-DMA into this wave's ND KiB of LDS, issued as soon as the
+// current row's copies have been read out of it, so they stream during the current row's
+// objective, stores and Gram reductions without holding registers (the commit's 2h + 2 rows and
+// 40 Gram accumulators fill 252 VGPRs: one row of register loads in flight, 2 waves per SIMD,
+// DESIGN.md §4). Same rows, same lanes, same operation order as stream_vf: the same bits.
+#define LBK_VF_DMA_MAX 18  // basis rows per wave in LDS: 4 waves x 18 KiB + the static 2 KiB keep 2 workgroups per CU
+#define LBK_VF_DMA_HB 6    // smallest history bucket with the DMA form
+template <int HB>
+constexpr int vf_dma_nd() {
+    return 2 * HB < LBK_VF_DMA_MAX ? 2 * HB : LBK_VF_DMA_MAX;
+}
+template <int ND, int K, class Op>
+__device__ __forceinline__ void stream_vf_dma(const Op& op, const Seg& s, const Geo& geo, double (&acc)[K],
+                                              double* dma_wg) {
+    constexpr int NB = Op::NB > 0 ? Op::NB : 1;
+    __shared__ double park[4][NB];
+    const int nrow = (int)(s.len >> 7);  // a full segment: whole rows
+    const int R = (nrow + 3) / 4;
+    const int r0 = s.w * R;
+    const int r1 = min(r0 + R, nrow);
+    if (r0 >= r1) return;
+    const bool last_lane = s.lane == 63;
+    double* dma = dma_wg + (size_t)s.w * ND * 128;
+    op.template dma_row<ND>(s.lb + (int64_t)r0 * 128 + 2 * s.lane, dma);
+    const double2 xd = op.xd_at(s.lane == 0 ? s.lb + (int64_t)r0 * 128 - 1 : s.lb + (int64_t)r1 * 128);
+    const double zedge = xd.x + op.alpha * xd.y;
+    double zedge_c[LBK_VF_NA], pzc[LBK_VF_NA], zfc[LBK_VF_NA];
+#pragma unroll
+    for (int j = 0; j < LBK_VF_NA; ++j) {
+        zedge_c[j] = xd.x + op.ac[j] * xd.y;
+        pzc[j] = 0.0;
+    }
+    double zl = zedge;
+    double pz_m = 0.0, pz_c = 0.0, px = 0.0, pg = 0.0;
+    int64_t pi = 0, pe = 0;
+    bool pvalid = false;
+    for (int row = r0; row < r1; ++row) {
+        const int64_t o = (int64_t)row * 128 + 2 * s.lane;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this row's DMA has landed
+        typename Op::Row r;
+        op.template load_dma<ND>(r, s.lb + o, dma, s.lane);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // ... and been read out: the rows are free
+        if (row + 1 < r1) op.template dma_row<ND>(s.lb + o + 128, dma);
+        op.form(r);
+        const double zfirst = __shfl(r.z.x, 0, 64);
+#pragma unroll
+        for (int j = 0; j < LBK_VF_NA; ++j) zfc[j] = __shfl(r.zc[j].x, 0, 64);
+        if (last_lane && row > r0 && pvalid) op.finish(pz_m, pz_c, zfirst, px, pg, park[s.w], pi, pe, pzc, zfc, acc);
+        r.zh = zl;
+        op.template apply<true>(r, s.lb + o, s.sbeg + o, true, !last_lane, acc);
+        if (last_lane) {
+            pz_m = r.z.x;
+            pz_c = r.z.y;
+#pragma unroll
+            for (int j = 0; j < LBK_VF_NA; ++j) pzc[j] = r.zc[j].y;
+            px = r.x.y;
+            pg = r.g.y;
+            op.park(r, park[s.w]);
+            pi = s.lb + o + 1;
+            pe = s.sbeg + o + 1;
+            pvalid = true;
+        }
+        zl = __shfl(r.z.y, 63, 64);
+    }
+    if (last_lane && pvalid) op.finish(pz_m, pz_c, zedge, px, pg, park[s.w], pi, pe, pzc, zedge_c, acc);
+}
+
+template <int OBJ, int HB, bool NT, bool DMA = false>
 __global__ __launch_bounds__(LB_BLOCK) void k_vf_commit(OpVfCommit<OBJ, HB, NT> op, Geo geo, Red red) {
     constexpr int K = OpVfCommit<OBJ, HB, NT>::K;
     const Seg s = seg_setup(geo);
     double acc[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) acc[k] = 0.0;
-    stream_vf(op, s, geo, acc);
+    if constexpr (DMA && HB > 0) {
+        extern __shared__ __attribute__((aligned(16))) double vf_dma_lds[];
+        if (s.len == geo.L)
+            stream_vf_dma<vf_dma_nd<HB>()>(op, s, geo, acc, vf_dma_lds);
+        else
+            stream_vf(op, s, geo, acc);
+    } else {
+        stream_vf(op, s, geo, acc);
+    }
     reduce_publish<K>(acc, geo, red);
 }
 
@@ -2595,6 +2707,13 @@ __device__ __forceinline__ int persist_twoloop(const SmallArgs& a, const Geo& ge
     return pass;
 }
 
+// The whole iteration in one persistent launch (LBFGS_PERSIST=1) lost its A/B at every size
+// (0.95-0.97x the launch sequence at n = 1e8): compiled only into A/B variant
+// builds (-DLBK_PERSIST_ITER=1, tools/build_variant.sh), not into the shipped library.
+#ifndef LBK_PERSIST_ITER
+#define LBK_PERSIST_ITER 0
+#endif
+#if LBK_PERSIST_ITER
 template <int OBJ, bool NT>
 __global__ __launch_bounds__(LB_BLOCK) void k_persist_iter(SmallArgs a, Geo geo) {
     __shared__ double lds[4][8];
@@ -2619,6 +2738,7 @@ __global__ __launch_bounds__(LB_BLOCK) void k_persist_iter(SmallArgs a, Geo geo)
                           geo, a, pass++, SL(a.slot_c), HS(a.slot_c), nullptr, t8, lds, gv, last_flag);
     coop_publish(a, 1, rho_top, gamma);
 }
+#endif  // LBK_PERSIST_ITER
 
 // The persistent two-loop alone (LBFGS_PERSIST=2; the north star's "persistent-block fused
 // two-loop"): one resident grid runs all 2h (or 2h - 1) two-loop passes of an iteration, the
@@ -2822,6 +2942,7 @@ struct lbk_ctx {
     int defer_max;
     // collect-mode stage 2 (kred): on, the launch being set up uses it, flagged partials, tags
     int collect_on, collect_now;
+    double collect_timeout_s;  // a collector's wait before it gives up (LBFGS_COLLECT_TIMEOUT, 10 s)
     unsigned long long* coll_ll;
     unsigned coll_seq;
     int defer_now;        // the launch in progress defers its stage 2
@@ -2875,6 +2996,7 @@ struct lbk_ctx {
     // LBFGS_CU_PARTITION (sharded, tests and one-card rehearsals): the solver stream runs on this
     // rank's own cu_count CUs, disjoint from every other rank's, as if each rank had a GPU
     int cu_part, cu_count;
+    int vf_dma;  // LBFGS_VF_DMA: the vector-free commit's next basis row by LDS-DMA (stream_vf_dma)
 };
 
 namespace {
@@ -2986,7 +3108,7 @@ Red kred(lbk_ctx* c, int slot, int K = 1) {
         r.ll = c->coll_ll;
         r.seq = ++c->coll_seq;
         r.err = c->coop_err_d;
-        r.timeout = (unsigned long long)(2.0 * c->wall_khz * 1e3);
+        r.timeout = (unsigned long long)(c->collect_timeout_s * c->wall_khz * 1e3);
         c->collect_now = 1;
     }
     const int si = slot < LBK_NSLOTS ? slot : LBK_NSLOTS + slot - LBK_WSLOT0;

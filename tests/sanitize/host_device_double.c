@@ -133,6 +133,15 @@ int lbk_exchange_bench(lbk_ctx* c, int b, int ks, int it, double* us) {
     (void)c, (void)b, (void)ks, (void)it, (void)us;
     return -1;
 }
+int lbk_cu_partition(const lbk_ctx* c) {
+    (void)c;
+    return 0;
+}
+int lbk_stream_probe(lbk_ctx* c, double* q, const double* y, const double* s, int launches, double* us) {
+    (void)c, (void)q, (void)y, (void)s, (void)launches;
+    *us = 0.0;  /* no device: nothing to time */
+    return 0;
+}
 
 /* ---- memory: ghost cells at [-1] and [n] (zero), as lbk_vec_alloc's layout ---- */
 double* lbk_vec_alloc(lbk_ctx* c) {

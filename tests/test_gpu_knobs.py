@@ -5,7 +5,11 @@ or in which direction it walks). Round 3 found in-launch tickets on one rank rel
 after the first of several groups (LBFGS_TICKET=1 at mid n: NaN trajectories); this matrix is the
 net for that class of interaction bug. Sizes cover each stage-2 regime of the default path:
 cooperative (<= 256 segments), deferred (<= 1024), reduce kernel (> 1024, 512- and 640-element
-segments)."""
+segments).
+
+The variants are the shipped forms (DESIGN.md §3 lists each stage-2 form's forward-progress
+assumption and the test here that would catch a violation); LBFGS_PERSIST=1 is compiled out of the
+shipped library (LBK_PERSIST_ITER) and must leave the default path untouched."""
 import os
 import sys
 
@@ -20,7 +24,8 @@ pytestmark = pytest.mark.gpu
 
 KNOBS = ["LBFGS_TICKET", "LBFGS_DEFER", "LBFGS_REV", "LBFGS_NT", "LBFGS_DIRECT", "LBFGS_COOP",
          "LBFGS_PERSIST", "LBFGS_PINGPONG", "LBFGS_SPEC", "LBFGS_BATCH", "LBFGS_SMALL_SEGS",
-         "LBFGS_PERSIST_WG", "LBFGS_PERSIST_OWN", "LBFGS_PERSIST_ALT", "LBFGS_PERSIST_LDS", "LBFGS_COLLECT"]
+         "LBFGS_PERSIST_WG", "LBFGS_PERSIST_OWN", "LBFGS_PERSIST_ALT", "LBFGS_PERSIST_LDS", "LBFGS_COLLECT",
+         "LBFGS_COLLECT_TIMEOUT"]
 
 VARIANTS = {
     "ticket1": {"LBFGS_TICKET": "1"},
@@ -32,7 +37,7 @@ VARIANTS = {
     "nt1": {"LBFGS_NT": "1"},
     "direct0": {"LBFGS_DIRECT": "0"},
     "coop0": {"LBFGS_COOP": "0"},
-    "persist1": {"LBFGS_PERSIST": "1"},
+    "persist1_not_shipped": {"LBFGS_PERSIST": "1"},  # compiled out of the library: the default path runs
     "persist2": {"LBFGS_PERSIST": "2"},
     "persist2_wg1_stride": {"LBFGS_PERSIST": "2", "LBFGS_PERSIST_WG": "1", "LBFGS_PERSIST_OWN": "stride"},
     "persist2_alt0_lds0_nt1": {"LBFGS_PERSIST": "2", "LBFGS_PERSIST_ALT": "0", "LBFGS_PERSIST_LDS": "0",
@@ -46,7 +51,8 @@ VARIANTS = {
     "ticket1_direct0": {"LBFGS_TICKET": "1", "LBFGS_DIRECT": "0"},
     "ticket1_rev0_nt0": {"LBFGS_TICKET": "1", "LBFGS_REV": "0", "LBFGS_NT": "0"},
     "ticket1_pingpong1": {"LBFGS_TICKET": "1", "LBFGS_PINGPONG": "1"},
-    "persist1_coop0_nt1": {"LBFGS_PERSIST": "1", "LBFGS_COOP": "0", "LBFGS_NT": "1"},
+    "persist2_coop0_nt1": {"LBFGS_PERSIST": "2", "LBFGS_COOP": "0", "LBFGS_NT": "1"},
+    "collect_timeout": {"LBFGS_COLLECT": "1", "LBFGS_COLLECT_TIMEOUT": "30"},
     "defer_all_rev0_pingpong1": {"LBFGS_DEFER": "8192", "LBFGS_TICKET": "0", "LBFGS_REV": "0",
                                  "LBFGS_PINGPONG": "1"},
     "coop0_spec0_batch0": {"LBFGS_COOP": "0", "LBFGS_SPEC": "0", "LBFGS_BATCH": "0"},
