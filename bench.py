@@ -438,9 +438,10 @@ def _measure(a, D, ctx, x0, rank, world, uid, unfused, vector_free, box_probe):
     probe = None
     if box_probe and not a.no_box_probe and res["status"] == "running":
         probe = run(ctx.stream_probe, 20)
-        gb = D.allreduce(probe["gbps"] if probe and probe["gbps"] else 0.0, "min")
+        mine = probe["gbps"] if probe and probe["gbps"] else 0.0
+        gmin, gsum = D.allreduce(mine, "min"), D.allreduce(mine, "sum")
         vote("box probe")
-        probe = dict(probe, gbps_min_over_ranks=gb) if probe else None
+        probe = dict(probe, gbps_min_over_ranks=gmin, gbps_sum_over_ranks=gsum) if probe else None
     # roofline region: the same kind of steps again with a HIP event pair around every launch
     # on the solver stream (per-kernel durations; the events add a few us per launch, which
     # is why they are kept out of the timed region above)
@@ -682,11 +683,13 @@ def reference_parity(traj, live, fixture, fsrc):
 def box_fields(probe, value, achieved_gbps, world):
     """This box's HBM rate for the two-loop passes' access pattern (lbfgs_stream_probe: 20 launches
     of a 3 R + 1 W stream over the solver's own q, y, s in the passes' geometry and cache policy,
-    right after the timed steps; sharded: the slowest rank's) and the line's value against it, so
-    lines from different boxes compare by the code rather than by the box."""
+    right after the timed steps, every rank at once) and the line's value against it, so lines
+    from different boxes compare by the code rather than by the box. The box rate
+    of a sharded line is the sum of its ranks' concurrent probes: the aggregate of N GPUs, or the
+    one card's rate when the ranks share it (a rehearsal)."""
     if not probe or not probe.get("gbps"):
         return {"box_copy_tbps": None}
-    gb = probe.get("gbps_min_over_ranks") or probe["gbps"]
+    gb = probe.get("gbps_sum_over_ranks") or probe["gbps"]
     return {"box_copy_tbps": round(gb / 1e3, 4),
             "value_per_box_tbps": round(value / (gb / 1e3), 4),
             "hbm_frac_of_box": round(achieved_gbps / gb, 4),
@@ -694,7 +697,8 @@ def box_fields(probe, value, achieved_gbps, world):
                           "avg_launch_us": round(probe["avg_launch_us"], 2), "launches": 20,
                           "bytes_per_launch": probe["bytes_per_launch"],
                           "rank0_gbps": round(probe["gbps"], 1),
-                          "over": "slowest rank" if world > 1 else "one GPU"}}
+                          "slowest_rank_gbps": round(probe.get("gbps_min_over_ranks") or probe["gbps"], 1),
+                          "over": f"sum of {world} ranks' concurrent probes" if world > 1 else "one GPU"}}
 
 
 def roofline(prof, n, world):

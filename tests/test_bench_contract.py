@@ -72,11 +72,17 @@ def test_committed_pmc_summaries_record_their_library(bench):
 
 
 def test_box_fields(bench):
-    p = {"avg_launch_us": 500.0, "bytes_per_launch": 3.2e9, "gbps": 6400.0, "gbps_min_over_ranks": 6400.0}
+    p = {"avg_launch_us": 500.0, "bytes_per_launch": 3.2e9, "gbps": 6400.0, "gbps_min_over_ranks": 6400.0,
+         "gbps_sum_over_ranks": 6400.0}
     f = bench.box_fields(p, 90.0, 5900.0, 1)
     assert f["box_copy_tbps"] == 6.4 and f["value_per_box_tbps"] == pytest.approx(90.0 / 6.4, rel=1e-3)
     assert f["hbm_frac_of_box"] == pytest.approx(5900.0 / 6400.0, rel=1e-3)
     assert bench.box_fields(None, 90.0, 5900.0, 1) == {"box_copy_tbps": None}
+    # sharded: the ranks' concurrent probes add up to the box (8 GPUs, or one shared card)
+    p8 = dict(p, gbps_min_over_ranks=5800.0, gbps_sum_over_ranks=8 * 6000.0)
+    f8 = bench.box_fields(p8, 700.0, 40000.0, 8)
+    assert f8["box_copy_tbps"] == 48.0 and f8["hbm_frac_of_box"] == pytest.approx(40000.0 / 48000.0, rel=1e-3)
+    assert f8["box_probe"]["slowest_rank_gbps"] == 5800.0
 
 
 def test_cpu_baseline_runner(bench):
