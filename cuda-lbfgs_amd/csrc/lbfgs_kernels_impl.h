@@ -1768,19 +1768,33 @@ struct OpVfCommit {
             if (l < 2 * B.h) r.b[l] = ldv<NT>(B.b[l] + i);
         form(r);
     }
-    // LDS-DMA form (stream_vf_dma): basis vectors l < ND of the row already sit in this wave's
-    // LDS rows (lane's 16 B at dma + l * 128 + 2 lane), the rest and x, g come from memory
+    // LDS-DMA form (stream_vf_dma): basis vectors l < ND of a row travel by DMA into this wave's
+    // LDS rows (lane's 16 B at dma + l * 128 + 2 lane); x, g and the basis vectors from ND on are
+    // register loads, issued a row ahead (RegRow)
     template <int ND>
-    __device__ void load_dma(Row& r, int64_t i, const double* dma, int lane) const {
-        r.x = ldx<NT>(x + i);
-        r.g = ldx<NT>(g + i);
+    struct RegRow {
+        double2 x, g;
+        double2 b[2 * HB > ND ? 2 * HB - ND : 1];
+    };
+    template <int ND>
+    __device__ void reg_row(RegRow<ND>& n, int64_t i) const {
+        n.x = ldx<NT>(x + i);
+        n.g = ldx<NT>(g + i);
+#pragma unroll
+        for (int l = ND; l < 2 * HB; ++l)
+            if (l < 2 * B.h) n.b[l - ND] = ldv<NT>(B.b[l] + i);
+    }
+    template <int ND>
+    __device__ void take_row(Row& r, const RegRow<ND>& n, const double* dma, int lane) const {
+        r.x = n.x;
+        r.g = n.g;
 #pragma unroll
         for (int l = 0; l < 2 * HB; ++l) {
             if (l < 2 * B.h) {
                 if (l < ND)
                     r.b[l] = *reinterpret_cast<const double2*>(dma + l * 128 + 2 * lane);
                 else
-                    r.b[l] = ldv<NT>(B.b[l] + i);
+                    r.b[l] = n.b[l - ND];
             }
         }
     }
@@ -1974,8 +1988,16 @@ __device__ __forceinline__ void stream_vf(const Op& op, const Seg& s, const Geo&
 // objective, stores and Gram reductions without holding registers (the commit's 2h + 2 rows and
 // 40 Gram accumulators fill 252 VGPRs: one row of register loads in flight, 2 waves per SIMD,
 // DESIGN.md §4). Same rows, same lanes, same operation order as stream_vf: the same bits.
+// Measured slower than the register form: compiled only into A/B variant builds
+// (-DLBK_VF_DMA=1, tools/build_variant.sh), where LBFGS_VF_DMA=1 selects it.
+#ifndef LBK_VF_DMA
+#define LBK_VF_DMA 0
+#endif
 #define LBK_VF_DMA_MAX 18  // basis rows per wave in LDS: 4 waves x 18 KiB + the static 2 KiB keep 2 workgroups per CU
 #define LBK_VF_DMA_HB 6    // smallest history bucket with the DMA form
+#ifndef LBK_VF_DMA_WAIT0
+#define LBK_VF_DMA_WAIT0 0  // A/B: wait for every outstanding access (the previous row's stores too)
+#endif
 template <int HB>
 constexpr int vf_dma_nd() {
     return 2 * HB < LBK_VF_DMA_MAX ? 2 * HB : LBK_VF_DMA_MAX;
@@ -1992,7 +2014,9 @@ __device__ __forceinline__ void stream_vf_dma(const Op& op, const Seg& s, const 
     if (r0 >= r1) return;
     const bool last_lane = s.lane == 63;
     double* dma = dma_wg + (size_t)s.w * ND * 128;
+    typename Op::template RegRow<ND> nx;
     op.template dma_row<ND>(s.lb + (int64_t)r0 * 128 + 2 * s.lane, dma);
+    op.template reg_row<ND>(nx, s.lb + (int64_t)r0 * 128 + 2 * s.lane);
     const double2 xd = op.xd_at(s.lane == 0 ? s.lb + (int64_t)r0 * 128 - 1 : s.lb + (int64_t)r1 * 128);
     const double zedge = xd.x + op.alpha * xd.y;
     double zedge_c[LBK_VF_NA], pzc[LBK_VF_NA], zfc[LBK_VF_NA];
@@ -2007,11 +2031,25 @@ __device__ __forceinline__ void stream_vf_dma(const Op& op, const Seg& s, const 
     bool pvalid = false;
     for (int row = r0; row < r1; ++row) {
         const int64_t o = (int64_t)row * 128 + 2 * s.lane;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this row's DMA has landed
+        // this row's DMA and register loads have landed. Both were issued in the previous
+        // iteration ahead of its stores - apply's 4 (x_new, g_new, s, y) and, from its second row
+        // on, finish's 4 for lane 63 - which are at least that many vector-memory instructions
+        // however the compiler forms them (it cannot move them above the loads: both touch global
+        // memory it cannot tell apart); so waiting until at most that many are outstanding never
+        // waits on the stores and always covers this row. The first row also waits for xd_at.
+        if (LBK_VF_DMA_WAIT0 || row == r0)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else if (row == r0 + 1)
+            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
         typename Op::Row r;
-        op.template load_dma<ND>(r, s.lb + o, dma, s.lane);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // ... and been read out: the rows are free
-        if (row + 1 < r1) op.template dma_row<ND>(s.lb + o + 128, dma);
+        op.template take_row<ND>(r, nx, dma, s.lane);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the LDS rows are read out: free for the next DMA
+        if (row + 1 < r1) {
+            op.template dma_row<ND>(s.lb + o + 128, dma);
+            op.template reg_row<ND>(nx, s.lb + o + 128);
+        }
         op.form(r);
         const double zfirst = __shfl(r.z.x, 0, 64);
 #pragma unroll

@@ -55,7 +55,7 @@ int vf_commit_hb(lbk_ctx* c, int obj, int h, const double* x, const double* g, c
         OBJ_DISPATCH(obj, {
             OpVfCommit<O_, HB, NT_> op{x, g, B, alpha, {cand[0]}, xn, gn, so, yo, geo.n, geo.n_loc};
             bool done = false;
-            if constexpr (HB >= LBK_VF_DMA_HB) {  // (smaller buckets hold fewer rows: no DMA form compiled)
+            if constexpr (LBK_VF_DMA && HB >= LBK_VF_DMA_HB) {  // variant builds only
                 if (dma) {
                     static bool attr = false;  // per instantiation: allow its dynamic LDS (> 64 KiB)
                     if (!attr) {

@@ -193,6 +193,14 @@ int main(int argc, char** argv) {
         {"vf_22r4w_u2_occ2", 22, 4, launch<22, 4, 2, true, true, 0, 0, false, 0, false, 60>, false},
         {"vf_22r4w_u2_run_occ2", 22, 4, launch<22, 4, 2, true, true, 0, 0, false, 0, true, 60>, false},
         {"vf_22r4w_u1_occ1", 22, 4, launch<22, 4, 1, true, true, 0, 0, false, 0, false, 100>, false},
+        // round 4: two-loop passes in pairs (the first of a pair keeps q in registers and stores
+        // nothing, the second recomputes it from the pair's source and stores q two steps on):
+        // 3R + 0W then 4R + 1W move the same 8 vectors as two 3R + 1W passes with one write fewer
+        {"pairA_3r0w_u4_alt", 3, 0, launch<3, 0, 4, true, true, 1, 0, false>, true},
+        {"pairB_4r1w_u4_inpl_alt", 4, 1, launch<4, 1, 4, true, true, 1, 1, true>, true},
+        {"pairB_4r1w_u4_outpl_alt", 4, 1, launch<4, 1, 4, true, true, 1, 1, false>, true},
+        {"pairM_3r1w_u8_alt", 3, 1, launch<3, 1, 8, true, true, 1, 1, false>, true},
+        {"commit5_5r4w_u4_alt", 5, 4, launch<5, 4, 4, true, true, 1, 0, false>, true},
     };
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
