@@ -82,9 +82,7 @@ enum {
     LBK_K_DOT = 0, LBK_K_AXPY_DOT, LBK_K_MID, LBK_K_AXPY2_DOT, LBK_K_LAST, LBK_K_NEGDOT,
     LBK_K_EVAL, LBK_K_TRIAL_F, LBK_K_TRIAL_FG, LBK_K_COMMIT, LBK_K_POINT, LBK_K_CHECKSUM,
     LBK_K_UPDATE, LBK_K_VF_COMMIT, LBK_K_VF_DIR, LBK_K_SMALL_ITER, LBK_K_GROUP_REDUCE,
-    LBK_K_EXCHANGE /* sharded: a reduction exchange (mailbox kernel or RCCL all-gather) */,
-    /* the second pass of a pair (lbk_*_pair; the first counts as its loop's single pass) */
-    LBK_K_AXPY_DOT_PAIR, LBK_K_MID_PAIR, LBK_K_AXPY2_DOT_PAIR, LBK_K_COUNT
+    LBK_K_EXCHANGE /* sharded: a reduction exchange (mailbox kernel or RCCL all-gather) */, LBK_K_COUNT
 };
 
 typedef struct {
@@ -166,22 +164,6 @@ int lbk_axpy2_dot(lbk_ctx* c, double* r, const double* rin, const double* s, con
                   int ref_beta, int ref_alpha, int slot);
 int lbk_last(lbk_ctx* c, double* dout, const double* r, const double* s, const double* g,
              double rho, int ref_beta, int ref_alpha, int slot);
-/* Passes in pairs (LBFGS_PAIR): two consecutive steps of a loop as two launches, the
- * first storing nothing, the second recomputing the first's output from the pair's source and
- * storing its own; the same slots and the same vectors as the two single passes.
- *   axpy_dot_pair:  q_i = qin - a_{i+1} y_{i+1} (s_i . q_i -> slot1), q_{i-1} = q_i - a_i y_i
- *                   -> qout (s_{i-1} . q_{i-1} -> slot0); a_{i+1} = rho1 total(ref1), a_i = rho0 total(slot1)
- *   mid_pair:       q_0 = qin - a_1 y_1 (s_0 . q_0 -> slot_a), r = (q_0 - a_0 y_0) gamma -> rout (-> slot_b)
- *   axpy2_dot_pair: r_{i+1} = rin + s_i (a_i - b_i) (y_{i+1} . r_{i+1} -> slot1), r_{i+2} = r_{i+1} +
- *                   s_{i+1} (a_{i+1} - b_{i+1}) -> rout (y_{i+2} . r_{i+2} -> slot2) */
-int lbk_axpy_dot_pair(lbk_ctx* c, double* qout, const double* qin, const double* y1, const double* s1,
-                      const double* y0, const double* s0, double rho1, int ref1, double rho0, int slot1, int slot0);
-int lbk_mid_pair(lbk_ctx* c, double* rout, const double* qin, const double* y1, const double* s0, const double* y0,
-                 double rho1, int ref1, double rho0, double gamma, int slot_a, int slot_b);
-int lbk_axpy2_dot_pair(lbk_ctx* c, double* rout, const double* rin, const double* s0, const double* y1,
-                       const double* s1, const double* y2, double rho0, int ref_beta0, int ref_alpha0, double rho1,
-                       int ref_alpha1, int slot1, int slot2);
-int lbk_pair_on(const lbk_ctx* c); /* LBFGS_PAIR */
 int lbk_negdot(lbk_ctx* c, double* dout, const double* g, int slot);
 int lbk_eval(lbk_ctx* c, int obj, const double* x, double* gout, int slot);  /* f, g.g */
 int lbk_trial(lbk_ctx* c, int obj, const double* x, const double* d, double alpha,

@@ -1292,62 +1292,25 @@ static int iterate(lbfgs_ctx* c) {
                 const double* qsrc = c->g;
                 double* qb[2] = {c->q, c->pingpong ? c->q2 : c->q};
                 int qi = 0;
-                /* LBFGS_PAIR: consecutive passes in pairs, the first storing nothing (lbk_*_pair;
-                 * the same slots, vectors and bits as the single passes) */
-                const int pairs = lbk_pair_on(c->dev);
-                int mid_pair = 0;
-                for (int i = h - 2; i >= 0;) {
-                    if (pairs && i == 0) { /* the last first-loop pass pairs with the middle step */
-                        mid_pair = 1;
-                        break;
-                    }
+                for (int i = h - 2; i >= 0; --i) {
                     double* qout = qb[qi];
                     qi ^= 1;
-                    if (pairs) {
-                        DEV(lbk_axpy_dot_pair(c->dev, qout, qsrc, c->Y[c->ring[i + 1]], c->S[c->ring[i]],
-                                              c->Y[c->ring[i]], c->S[c->ring[i - 1]], rho[i + 1], refA[i + 1], rho[i],
-                                              SLOT_A0 + i, SLOT_A0 + i - 1));
-                        c->passes++;
-                        refA[i] = REF(SLOT_A0 + i, 0);
-                        refA[i - 1] = REF(SLOT_A0 + i - 1, 0);
-                        i -= 2;
-                    } else {
-                        DEV(lbk_axpy_dot(c->dev, qout, qsrc, c->Y[c->ring[i + 1]], c->S[c->ring[i]], rho[i + 1],
-                                         refA[i + 1], SLOT_A0 + i));
-                        refA[i] = REF(SLOT_A0 + i, 0);
-                        i -= 1;
-                    }
+                    DEV(lbk_axpy_dot(c->dev, qout, qsrc, c->Y[c->ring[i + 1]], c->S[c->ring[i]], rho[i + 1],
+                                     refA[i + 1], SLOT_A0 + i));
+                    refA[i] = REF(SLOT_A0 + i, 0);
                     qsrc = qout;
                 }
-                if (mid_pair) {
-                    DEV(lbk_mid_pair(c->dev, c->r, qsrc, c->Y[c->ring[1]], c->S[c->ring[0]], c->Y[c->ring[0]], rho[1],
-                                     refA[1], rho[0], gamma, SLOT_A0, SLOT_B0(m)));
-                    c->passes++;
-                    refA[0] = REF(SLOT_A0, 0);
-                } else {
-                    DEV(lbk_mid(c->dev, c->r, qsrc, c->Y[c->ring[0]], rho[0], gamma, refA[0], SLOT_B0(m)));
-                }
+                DEV(lbk_mid(c->dev, c->r, qsrc, c->Y[c->ring[0]], rho[0], gamma, refA[0], SLOT_B0(m)));
                 refB[0] = REF(SLOT_B0(m), 0);
                 double* rb[2] = {c->r, c->pingpong ? c->r2 : c->r};
                 int ri = 1;
                 const double* rcur = c->r;
-                for (int i = 0; i + 1 < h;) {
+                for (int i = 0; i + 1 < h; ++i) {
                     double* rout = rb[ri];
                     ri ^= 1;
-                    if (pairs && i + 2 < h) { /* (the last pass stays single: its r feeds the commit) */
-                        DEV(lbk_axpy2_dot_pair(c->dev, rout, rcur, c->S[c->ring[i]], c->Y[c->ring[i + 1]],
-                                               c->S[c->ring[i + 1]], c->Y[c->ring[i + 2]], rho[i], refB[i], refA[i],
-                                               rho[i + 1], refA[i + 1], SLOT_B0(m) + i + 1, SLOT_B0(m) + i + 2));
-                        c->passes++;
-                        refB[i + 1] = REF(SLOT_B0(m) + i + 1, 0);
-                        refB[i + 2] = REF(SLOT_B0(m) + i + 2, 0);
-                        i += 2;
-                    } else {
-                        DEV(lbk_axpy2_dot(c->dev, rout, rcur, c->S[c->ring[i]], c->Y[c->ring[i + 1]], rho[i], refB[i],
-                                          refA[i], SLOT_B0(m) + i + 1));
-                        refB[i + 1] = REF(SLOT_B0(m) + i + 1, 0);
-                        i += 1;
-                    }
+                    DEV(lbk_axpy2_dot(c->dev, rout, rcur, c->S[c->ring[i]], c->Y[c->ring[i + 1]], rho[i], refB[i],
+                                      refA[i], SLOT_B0(m) + i + 1));
+                    refB[i + 1] = REF(SLOT_B0(m) + i + 1, 0);
                     rcur = rout;
                 }
                 c->rc = rcur;

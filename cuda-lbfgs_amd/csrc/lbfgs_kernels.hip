@@ -162,10 +162,6 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
     if (const char* e = getenv("LBFGS_XGMI_MIRROR")) c->xg_mirror = atoi(e) != 0;
     c->vf_dma = 0;
     if (const char* e = getenv("LBFGS_VF_DMA")) c->vf_dma = atoi(e) != 0;
-    // two-loop passes in pairs (lbk_*_pair): one vector write fewer per pair, the same
-    // bytes and bits. A/B: LBFGS_PAIR=0/1
-    c->pair_on = 0;
-    if (const char* e = getenv("LBFGS_PAIR")) c->pair_on = atoi(e) != 0;
     *out = c;
 #define CK(expr)                                                                             \
     do {                                                                                     \
@@ -688,127 +684,6 @@ int lbk_axpy2_dot(lbk_ctx* c, double* rr, const double* rin, const double* s, co
             NT_DISPATCH(c, hipLaunchKernelGGL((k_axpy2_dot<NT_, true>), dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, rr, rin, s, ynext, rho, pb, pa, g, r, fs));
         else
             NT_DISPATCH(c, hipLaunchKernelGGL(k_axpy2_dot<NT_>, dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, rr, rin, s, ynext, rho, pb, pa, g, r, fs));
-    });
-}
-
-// ---- passes in pairs (LBFGS_PAIR) ----
-int lbk_pair_on(const lbk_ctx* c) { return c->pair_on; }
-
-int lbk_axpy_dot_pair(lbk_ctx* c, double* qout, const double* qin, const double* y1, const double* s1,
-                      const double* y0, const double* s0, double rho1, int ref1, double rho0, int slot1, int slot0) {
-    {  // the first pass: s_i . q_i, q_i not stored
-        Geo g = kgeo(c);
-        g.ppart = take_pending(c, ref1);
-        const FoldSrc fs = take_fold(c, ref1);
-        Red r = kred_deferrable(c, slot1);
-        fold_producer(c, r, false);
-        const double* pa = sref(c, ref1);
-        const int rc = launch(c, LBK_K_AXPY_DOT, 3, slot1, [&] {
-            if (r.fp.peers || fs.mbx)
-                NT_DISPATCH(c, hipLaunchKernelGGL((k_axpy_dot<NT_, true, false>), dim3(nblocks(c)), dim3(LB_BLOCK), 0,
-                                                  c->stream, nullptr, qin, y1, s1, rho1, pa, g, r, fs));
-            else
-                NT_DISPATCH(c, hipLaunchKernelGGL((k_axpy_dot<NT_, false, false>), dim3(nblocks(c)), dim3(LB_BLOCK), 0,
-                                                  c->stream, nullptr, qin, y1, s1, rho1, pa, g, r, fs));
-        });
-        if (rc) return rc;
-    }
-    const int ref0 = slot1 * LBK_KMAX;
-    Geo g = kgeo(c);
-    g.ppart = take_pending(c, ref0);
-    const FoldSrc fs = take_fold(c, ref0);
-    Red r = kred_deferrable(c, slot0);
-    fold_producer(c, r, false);
-    const double* p1 = sref(c, ref1);
-    const double* p0 = sref(c, ref0);
-    return launch(c, LBK_K_AXPY_DOT_PAIR, 5, slot0, [&] {
-        if (r.fp.peers || fs.mbx)
-            NT_DISPATCH(c, hipLaunchKernelGGL((k_axpy_dot2<NT_, true>), dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream,
-                                              qout, qin, y1, y0, s0, rho1, p1, rho0, p0, g, r, fs));
-        else
-            NT_DISPATCH(c, hipLaunchKernelGGL(k_axpy_dot2<NT_>, dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, qout,
-                                              qin, y1, y0, s0, rho1, p1, rho0, p0, g, r, fs));
-    });
-}
-
-int lbk_mid_pair(lbk_ctx* c, double* rout, const double* qin, const double* y1, const double* s0, const double* y0,
-                 double rho1, int ref1, double rho0, double gamma, int slot_a, int slot_b) {
-    {  // the first loop's last pass: s_0 . q_0, q_0 not stored
-        Geo g = kgeo(c);
-        g.ppart = take_pending(c, ref1);
-        const FoldSrc fs = take_fold(c, ref1);
-        Red r = kred_deferrable(c, slot_a);
-        fold_producer(c, r, false);
-        const double* pa = sref(c, ref1);
-        const int rc = launch(c, LBK_K_AXPY_DOT, 3, slot_a, [&] {
-            if (r.fp.peers || fs.mbx)
-                NT_DISPATCH(c, hipLaunchKernelGGL((k_axpy_dot<NT_, true, false>), dim3(nblocks(c)), dim3(LB_BLOCK), 0,
-                                                  c->stream, nullptr, qin, y1, s0, rho1, pa, g, r, fs));
-            else
-                NT_DISPATCH(c, hipLaunchKernelGGL((k_axpy_dot<NT_, false, false>), dim3(nblocks(c)), dim3(LB_BLOCK), 0,
-                                                  c->stream, nullptr, qin, y1, s0, rho1, pa, g, r, fs));
-        });
-        if (rc) return rc;
-    }
-    const int ref0 = slot_a * LBK_KMAX;
-    Geo g = kgeo(c);
-    g.ppart = take_pending(c, ref0);
-    const FoldSrc fs = take_fold(c, ref0);
-    Red r = kred_deferrable(c, slot_b);
-    fold_producer(c, r, true);
-    const double* p1 = sref(c, ref1);
-    const double* p0 = sref(c, ref0);
-    if (c->geo.world > 1) g.edge_slot = r.slot;
-    return launch(c, LBK_K_MID_PAIR, 4, slot_b, [&] {
-        if (r.fp.peers || fs.mbx)
-            NT_DISPATCH(c, hipLaunchKernelGGL((k_mid2<NT_, true>), dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, rout,
-                                              qin, y1, y0, rho1, p1, rho0, gamma, p0, g, r, fs));
-        else
-            NT_DISPATCH(c, hipLaunchKernelGGL(k_mid2<NT_>, dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, rout, qin,
-                                              y1, y0, rho1, p1, rho0, gamma, p0, g, r, fs));
-    });
-}
-
-int lbk_axpy2_dot_pair(lbk_ctx* c, double* rout, const double* rin, const double* s0, const double* y1,
-                       const double* s1, const double* y2, double rho0, int ref_beta0, int ref_alpha0, double rho1,
-                       int ref_alpha1, int slot1, int slot2) {
-    {  // the first pass: y_{i+1} . r_{i+1}, r_{i+1} not stored
-        Geo g = kgeo(c);
-        g.ppart = take_pending(c, ref_beta0);
-        const FoldSrc fs = take_fold(c, ref_beta0);
-        Red r = kred_deferrable(c, slot1);
-        fold_producer(c, r, true);
-        const double* pb = sref(c, ref_beta0);
-        const double* pa = sref(c, ref_alpha0);
-        if (c->geo.world > 1) g.edge_slot = r.slot;
-        const int rc = launch(c, LBK_K_AXPY2_DOT, 3, slot1, [&] {
-            if (r.fp.peers || fs.mbx)
-                NT_DISPATCH(c, hipLaunchKernelGGL((k_axpy2_dot<NT_, true, false>), dim3(nblocks(c)), dim3(LB_BLOCK), 0,
-                                                  c->stream, nullptr, rin, s0, y1, rho0, pb, pa, g, r, fs));
-            else
-                NT_DISPATCH(c, hipLaunchKernelGGL((k_axpy2_dot<NT_, false, false>), dim3(nblocks(c)), dim3(LB_BLOCK), 0,
-                                                  c->stream, nullptr, rin, s0, y1, rho0, pb, pa, g, r, fs));
-        });
-        if (rc) return rc;
-    }
-    const int ref_beta1 = slot1 * LBK_KMAX;
-    Geo g = kgeo(c);
-    g.ppart = take_pending(c, ref_beta1);
-    const FoldSrc fs = take_fold(c, ref_beta1);
-    Red r = kred_deferrable(c, slot2);
-    fold_producer(c, r, true);
-    const double* pb0 = sref(c, ref_beta0);
-    const double* pa0 = sref(c, ref_alpha0);
-    const double* pb1 = sref(c, ref_beta1);
-    const double* pa1 = sref(c, ref_alpha1);
-    if (c->geo.world > 1) g.edge_slot = r.slot;
-    return launch(c, LBK_K_AXPY2_DOT_PAIR, 5, slot2, [&] {
-        if (r.fp.peers || fs.mbx)
-            NT_DISPATCH(c, hipLaunchKernelGGL((k_axpy2_dot2<NT_, true>), dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream,
-                                              rout, rin, s0, s1, y2, rho0, pb0, pa0, rho1, pb1, pa1, g, r, fs));
-        else
-            NT_DISPATCH(c, hipLaunchKernelGGL(k_axpy2_dot2<NT_>, dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, rout,
-                                              rin, s0, s1, y2, rho0, pb0, pa0, rho1, pb1, pa1, g, r, fs));
     });
 }
 

@@ -956,8 +956,7 @@ struct OpDot {  // acc += a . b
     }
 };
 
-// ST = false: the first pass of a pair (PAIR below) stores nothing, its q stays in registers
-template <bool NT, bool ST = true>
+template <bool NT>
 struct OpAxpyDot {  // q = qin - alpha y;  acc += s . q       (lbfgs.cpp:133-137)
     double* qout;
     const double* qin;
@@ -978,42 +977,6 @@ struct OpAxpyDot {  // q = qin - alpha y;  acc += s . q       (lbfgs.cpp:133-137
         double2 qn;
         qn.x = r.q.x - alpha * r.y.x;
         qn.y = r.q.y - alpha * r.y.y;
-        if constexpr (ST) st2w<MASK, NT>(qout + i, qn, v0, v1);
-        acc[0] = fma2<MASK>(r.s, qn, acc[0], v0, v1);
-    }
-};
-
-// PAIR (LBFGS_PAIR): two consecutive passes of a loop as a pair. The first streams as a single pass
-// but stores nothing (ST = false); the second reads the pair's SOURCE vector again with both
-// operands and recomputes the first pass's output in registers - the same operations on the same
-// values, so the same bits - before its own step, and stores the result two steps on. The pair
-// moves the same bytes as two single passes (3 R + 0 W, then 4 R + 1 W, against 2 x (3 R + 1 W))
-// with one vector write fewer: HBM turns a write around slower than it streams a read.
-template <bool NT>
-struct OpAxpyDot2 {  // q1 = qin - a1 y1;  q = q1 - alpha y0;  acc += s . q
-    double* qout;
-    const double* qin;
-    const double* __restrict__ y1;
-    const double* __restrict__ y0;
-    const double* __restrict__ s;
-    double a1, alpha;  // a1: the pair's first step (complete slot), alpha: its second (the first pass's reduction)
-    __device__ void set_coef(double a) { alpha = a; }
-    struct Row {
-        double2 q, y1, y0, s;
-    };
-    __device__ void load(Row& r, int64_t i) const {
-        r.q = ldw<NT>(qin + i);
-        r.y1 = ldv<NT>(y1 + i);
-        r.y0 = ldv<NT>(y0 + i);
-        r.s = ldv<NT>(s + i);
-    }
-    template <bool MASK>
-    __device__ void apply(Row& r, int64_t i, int64_t, bool v0, bool v1, double (&acc)[1]) const {
-        double2 q1, qn;
-        q1.x = r.q.x - a1 * r.y1.x;
-        q1.y = r.q.y - a1 * r.y1.y;
-        qn.x = q1.x - alpha * r.y0.x;
-        qn.y = q1.y - alpha * r.y0.y;
         st2w<MASK, NT>(qout + i, qn, v0, v1);
         acc[0] = fma2<MASK>(r.s, qn, acc[0], v0, v1);
     }
@@ -1059,40 +1022,7 @@ struct OpMid {  // r = (qin - alpha0 y0) * gamma;  acc += y0 . r      (:134-137,
     }
 };
 
-// PAIR: the first loop's last pass (q0 = q1 - a1 y1, stored by nobody) and the middle step
 template <bool NT>
-struct OpMid2 {  // q0 = qin - a1 y1;  r = (q0 - alpha0 y0) * gamma;  acc += y0 . r
-    double* __restrict__ rout;
-    const double* __restrict__ qin;
-    const double* __restrict__ y1;
-    const double* __restrict__ y0;
-    double a1, alpha, gamma;
-    double* edge_slot;
-    int64_t n_loc;
-    int g_lo, g_hi;
-    __device__ void set_coef(double a) { alpha = a; }
-    struct Row {
-        double2 q, y1, y0;
-    };
-    __device__ void load(Row& r, int64_t i) const {
-        r.q = ldw<NT>(qin + i);
-        r.y1 = ldv<NT>(y1 + i);
-        r.y0 = ldv<NT>(y0 + i);
-    }
-    template <bool MASK>
-    __device__ void apply(Row& r, int64_t i, int64_t, bool v0, bool v1, double (&acc)[1]) const {
-        double2 q0, rr;
-        q0.x = r.q.x - a1 * r.y1.x;
-        q0.y = r.q.y - a1 * r.y1.y;
-        rr.x = (q0.x - alpha * r.y0.x) * gamma;
-        rr.y = (q0.y - alpha * r.y0.y) * gamma;
-        st2w<MASK, NT>(rout + i, rr, v0, v1);
-        publish_edges(edge_slot, i, n_loc, g_lo, g_hi, rr, v0, v1);
-        acc[0] = fma2<MASK>(r.y0, rr, acc[0], v0, v1);
-    }
-};
-
-template <bool NT, bool ST = true>
 struct OpAxpy2Dot {  // r += s (alpha - beta);  acc += ynext . r      (:159-164)
     double* r;        // out (== rin in place, or the other buffer of a ping-pong pair)
     const double* rin;
@@ -1116,41 +1046,6 @@ struct OpAxpy2Dot {  // r += s (alpha - beta);  acc += ynext . r      (:159-164)
         double2 rn;
         rn.x = w.r.x + w.s.x * coef;
         rn.y = w.r.y + w.s.y * coef;
-        if constexpr (ST) st2w<MASK, NT>(r + i, rn, v0, v1);
-        publish_edges(edge_slot, i, n_loc, g_lo, g_hi, rn, v0, v1);
-        acc[0] = fma2<MASK>(w.y, rn, acc[0], v0, v1);
-    }
-};
-
-// PAIR: two second-loop steps, the first one's r recomputed in registers
-template <bool NT>
-struct OpAxpy2Dot2 {  // r1 = rin + s0 c0;  r = r1 + s1 coef;  acc += y2 . r
-    double* r;
-    const double* rin;
-    const double* __restrict__ s0;
-    const double* __restrict__ s1;
-    const double* __restrict__ y2;
-    double c0, coef;  // c0: the pair's first step (complete slots), coef: its second
-    double* edge_slot;
-    int64_t n_loc;
-    int g_lo, g_hi;
-    __device__ void set_coef(double c) { coef = c; }
-    struct Row {
-        double2 r, s0, s1, y;
-    };
-    __device__ void load(Row& w, int64_t i) const {
-        w.r = ldw<NT>(rin + i);
-        w.s0 = ldv<NT>(s0 + i);
-        w.s1 = ldv<NT>(s1 + i);
-        w.y = ldv<NT>(y2 + i);
-    }
-    template <bool MASK>
-    __device__ void apply(Row& w, int64_t i, int64_t, bool v0, bool v1, double (&acc)[1]) const {
-        double2 r1, rn;
-        r1.x = w.r.x + w.s0.x * c0;
-        r1.y = w.r.y + w.s0.y * c0;
-        rn.x = r1.x + w.s1.x * coef;
-        rn.y = r1.y + w.s1.y * coef;
         st2w<MASK, NT>(r + i, rn, v0, v1);
         publish_edges(edge_slot, i, n_loc, g_lo, g_hi, rn, v0, v1);
         acc[0] = fma2<MASK>(w.y, rn, acc[0], v0, v1);
@@ -1286,39 +1181,19 @@ __global__ __launch_bounds__(LB_BLOCK) void k_dot(const double* __restrict__ a, 
 // FOLD: sharded over the mailboxes, the source arrives folded (src_total polls) and the result is
 // pushed folded. A folded producer whose source came through a slot (or the reverse) does not
 // occur: the two-loop's passes fold as a chain.
-template <bool NT, bool FOLD = false, bool ST = true>
+template <bool NT, bool FOLD = false>
 __global__ __launch_bounds__(LB_BLOCK) void k_axpy_dot(double* qout, const double* qin, const double* __restrict__ y,
                                                        const double* __restrict__ sv, double rho,
                                                        const double* __restrict__ prev, Geo geo, Red red, FoldSrc fs) {
-    using Op = OpAxpyDot<NT, ST>;
     if constexpr (FOLD) {
         if (fs.mbx) {
-            run_pass_prefetch<Op, 1>(Op{qout, qin, y, sv, 0.0}, geo, red,
-                                     [&] { return rho * src_total_mailbox(prev, geo, fs); });
+            run_pass_prefetch<OpAxpyDot<NT>, 1>(OpAxpyDot<NT>{qout, qin, y, sv, 0.0}, geo, red,
+                                                [&] { return rho * src_total_mailbox(prev, geo, fs); });
             return;
         }
     }
     const double alpha = rho * src_total(prev, geo);
-    run_pass<Op, 1, FOLD>(Op{qout, qin, y, sv, alpha}, geo, red);
-}
-
-// PAIR, the first loop's second pass: alpha1 = rho1 * total(prev1) (complete: the pair's first pass
-// consumed it), alpha0 = rho0 * total(prev0) (the first pass's reduction)
-template <bool NT, bool FOLD = false>
-__global__ __launch_bounds__(LB_BLOCK) void k_axpy_dot2(double* qout, const double* qin, const double* __restrict__ y1,
-                                                        const double* __restrict__ y0, const double* __restrict__ sv,
-                                                        double rho1, const double* __restrict__ prev1, double rho0,
-                                                        const double* __restrict__ prev0, Geo geo, Red red, FoldSrc fs) {
-    const double a1 = rho1 * slot_total(prev1);
-    if constexpr (FOLD) {
-        if (fs.mbx) {
-            run_pass_prefetch<OpAxpyDot2<NT>, 1>(OpAxpyDot2<NT>{qout, qin, y1, y0, sv, a1, 0.0}, geo, red,
-                                                 [&] { return rho0 * src_total_mailbox(prev0, geo, fs); });
-            return;
-        }
-    }
-    const double alpha = rho0 * src_total(prev0, geo);
-    run_pass<OpAxpyDot2<NT>, 1, FOLD>(OpAxpyDot2<NT>{qout, qin, y1, y0, sv, a1, alpha}, geo, red);
+    run_pass<OpAxpyDot<NT>, 1, FOLD>(OpAxpyDot<NT>{qout, qin, y, sv, alpha}, geo, red);
 }
 
 template <bool NT, bool FOLD = false>
@@ -1338,76 +1213,27 @@ __global__ __launch_bounds__(LB_BLOCK) void k_mid(double* __restrict__ rout, con
                                  geo, red);
 }
 
-// PAIR: the first loop's last pass (its q0 in registers) and the middle step
-template <bool NT, bool FOLD = false>
-__global__ __launch_bounds__(LB_BLOCK) void k_mid2(double* __restrict__ rout, const double* __restrict__ qin,
-                                                   const double* __restrict__ y1, const double* __restrict__ y0,
-                                                   double rho1, const double* __restrict__ prev1, double rho0,
-                                                   double gamma, const double* __restrict__ prev0, Geo geo, Red red,
-                                                   FoldSrc fs) {
-    const double a1 = rho1 * slot_total(prev1);
-    if constexpr (FOLD) {
-        if (fs.mbx) {
-            run_pass_prefetch<OpMid2<NT>, 1>(
-                OpMid2<NT>{rout, qin, y1, y0, a1, 0.0, gamma, geo.edge_slot, geo.n_loc, geo.g_lo, geo.g_hi}, geo, red,
-                [&] { return rho0 * src_total_mailbox(prev0, geo, fs); });
-            return;
-        }
-    }
-    const double alpha = rho0 * src_total(prev0, geo);
-    run_pass<OpMid2<NT>, 1, FOLD>(
-        OpMid2<NT>{rout, qin, y1, y0, a1, alpha, gamma, geo.edge_slot, geo.n_loc, geo.g_lo, geo.g_hi}, geo, red);
-}
-
 // beta = rho * total(pb), alpha = rho * total(pa)
-template <bool NT, bool FOLD = false, bool ST = true>
+template <bool NT, bool FOLD = false>
 __global__ __launch_bounds__(LB_BLOCK) void k_axpy2_dot(double* r, const double* rin, const double* __restrict__ sv,
                                                         const double* __restrict__ yn, double rho,
                                                         const double* __restrict__ pb, const double* __restrict__ pa,
                                                         Geo geo, Red red, FoldSrc fs) {
-    using Op = OpAxpy2Dot<NT, ST>;
     if constexpr (FOLD) {
         if (fs.mbx) {
-            run_pass_prefetch<Op, 1>(Op{r, rin, sv, yn, 0.0, geo.edge_slot, geo.n_loc, geo.g_lo, geo.g_hi}, geo, red,
-                                     [&] {
-                                         const double beta = rho * src_total_mailbox(pb, geo, fs);
-                                         const double alpha = rho * slot_total(pa);
-                                         return alpha - beta;
-                                     });
-            return;
-        }
-    }
-    const double beta = rho * src_total(pb, geo);
-    const double alpha = rho * slot_total(pa);
-    run_pass<Op, 1, FOLD>(Op{r, rin, sv, yn, alpha - beta, geo.edge_slot, geo.n_loc, geo.g_lo, geo.g_hi}, geo, red);
-}
-
-// PAIR, the second loop's second pass: c0 = rho0 (total(pa0) - ...) as the pair's first pass formed
-// it (both slots complete now), coef = alpha1 - beta1 with beta1 the first pass's reduction
-template <bool NT, bool FOLD = false>
-__global__ __launch_bounds__(LB_BLOCK) void k_axpy2_dot2(double* r, const double* rin, const double* __restrict__ s0,
-                                                         const double* __restrict__ s1, const double* __restrict__ y2,
-                                                         double rho0, const double* __restrict__ pb0,
-                                                         const double* __restrict__ pa0, double rho1,
-                                                         const double* __restrict__ pb1, const double* __restrict__ pa1,
-                                                         Geo geo, Red red, FoldSrc fs) {
-    const double c0 = rho0 * slot_total(pa0) - rho0 * slot_total(pb0);
-    if constexpr (FOLD) {
-        if (fs.mbx) {
-            run_pass_prefetch<OpAxpy2Dot2<NT>, 1>(
-                OpAxpy2Dot2<NT>{r, rin, s0, s1, y2, c0, 0.0, geo.edge_slot, geo.n_loc, geo.g_lo, geo.g_hi}, geo, red,
-                [&] {
-                    const double beta = rho1 * src_total_mailbox(pb1, geo, fs);
-                    const double alpha = rho1 * slot_total(pa1);
+            run_pass_prefetch<OpAxpy2Dot<NT>, 1>(
+                OpAxpy2Dot<NT>{r, rin, sv, yn, 0.0, geo.edge_slot, geo.n_loc, geo.g_lo, geo.g_hi}, geo, red, [&] {
+                    const double beta = rho * src_total_mailbox(pb, geo, fs);
+                    const double alpha = rho * slot_total(pa);
                     return alpha - beta;
                 });
             return;
         }
     }
-    const double beta = rho1 * src_total(pb1, geo);
-    const double alpha = rho1 * slot_total(pa1);
-    run_pass<OpAxpy2Dot2<NT>, 1, FOLD>(
-        OpAxpy2Dot2<NT>{r, rin, s0, s1, y2, c0, alpha - beta, geo.edge_slot, geo.n_loc, geo.g_lo, geo.g_hi}, geo, red);
+    const double beta = rho * src_total(pb, geo);
+    const double alpha = rho * slot_total(pa);
+    run_pass<OpAxpy2Dot<NT>, 1, FOLD>(
+        OpAxpy2Dot<NT>{r, rin, sv, yn, alpha - beta, geo.edge_slot, geo.n_loc, geo.g_lo, geo.g_hi}, geo, red);
 }
 
 template <bool NT>
@@ -3209,7 +3035,6 @@ struct lbk_ctx {
     // rank's own cu_count CUs, disjoint from every other rank's, as if each rank had a GPU
     int cu_part, cu_count;
     int vf_dma;  // LBFGS_VF_DMA: the vector-free commit's next basis row by LDS-DMA (stream_vf_dma)
-    int pair_on;  // LBFGS_PAIR: two-loop passes in pairs (lbk_*_pair)
 };
 
 namespace {

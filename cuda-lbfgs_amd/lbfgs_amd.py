@@ -23,7 +23,7 @@ FLAG_VERBOSE, FLAG_QUIET, FLAG_TRACE, FLAG_UNFUSED, FLAG_VECTOR_FREE = 1, 2, 4, 
 FLAG_REFERENCE_CALLS = 32
 KERNELS = ["dot", "axpy_dot", "mid", "axpy2_dot", "last", "negdot", "eval", "trial_f",
            "trial_fg", "commit", "point", "checksum", "update", "vf_commit", "vf_dir", "small_iter",
-           "group_reduce", "exchange", "axpy_dot_pair", "mid_pair", "axpy2_dot_pair"]
+           "group_reduce", "exchange"]
 
 
 class LbfgsError(RuntimeError):

@@ -288,9 +288,6 @@ enum {
     /* sharded runs: each reduction's exchange between ranks (the xGMI mailbox kernel, waiting
      * for the peers included, or the RCCL all-gather); bytes 0 */
     LBFGS_KERNEL_EXCHANGE,
-    /* two-loop passes in pairs (LBFGS_PAIR): the second pass of each pair (the first, which
-     * stores nothing, counts as its loop's single-pass kind) */
-    LBFGS_KERNEL_AXPY_DOT_PAIR, LBFGS_KERNEL_MID_PAIR, LBFGS_KERNEL_AXPY2_DOT_PAIR,
     LBFGS_KERNEL_COUNT
 };
 void lbfgs_prof_enable(lbfgs_ctx* ctx, int on);

@@ -271,22 +271,6 @@ int lbk_mid(lbk_ctx* c, double* rout, const double* qin, const double* y0, doubl
     ACCOUNT(3);
     return 0;
 }
-/* passes in pairs (LBFGS_PAIR): the double runs the two single passes through a scratch vector,
- * which gives the device pair's slots and vectors */
-int lbk_pair_on(const lbk_ctx* c) {
-    (void)c;
-    const char* e = getenv("LBFGS_PAIR");
-    return e && atoi(e) != 0;
-}
-int lbk_axpy_dot_pair(lbk_ctx* c, double* qout, const double* qin, const double* y1, const double* s1,
-                      const double* y0, const double* s0, double rho1, int ref1, double rho0, int slot1, int slot0) {
-    double* t = (double*)malloc(sizeof(double) * (size_t)(c->geo.n > 0 ? c->geo.n : 1));
-    if (!t) return -4;
-    int rc = lbk_axpy_dot(c, t, qin, y1, s1, rho1, ref1, slot1);
-    if (!rc) rc = lbk_axpy_dot(c, qout, t, y0, s0, rho0, slot1 * LBK_KMAX, slot0);
-    free(t);
-    return rc;
-}
 static double coef_ab(lbk_ctx* c, double rho, int ref_beta, int ref_alpha) {
     const double beta = rho * ref_total(c, ref_beta);
     const double alpha = rho * ref_total(c, ref_alpha);
@@ -300,25 +284,6 @@ int lbk_axpy2_dot(lbk_ctx* c, double* r, const double* rin, const double* s, con
     put(c, slot, 0, ynext, r, c->geo.n, 0);
     ACCOUNT(4);
     return 0;
-}
-int lbk_mid_pair(lbk_ctx* c, double* rout, const double* qin, const double* y1, const double* s0, const double* y0,
-                 double rho1, int ref1, double rho0, double gamma, int slot_a, int slot_b) {
-    double* t = (double*)malloc(sizeof(double) * (size_t)(c->geo.n > 0 ? c->geo.n : 1));
-    if (!t) return -4;
-    int rc = lbk_axpy_dot(c, t, qin, y1, s0, rho1, ref1, slot_a);
-    if (!rc) rc = lbk_mid(c, rout, t, y0, rho0, gamma, slot_a * LBK_KMAX, slot_b);
-    free(t);
-    return rc;
-}
-int lbk_axpy2_dot_pair(lbk_ctx* c, double* rout, const double* rin, const double* s0, const double* y1,
-                       const double* s1, const double* y2, double rho0, int ref_beta0, int ref_alpha0, double rho1,
-                       int ref_alpha1, int slot1, int slot2) {
-    double* t = (double*)malloc(sizeof(double) * (size_t)(c->geo.n > 0 ? c->geo.n : 1));
-    if (!t) return -4;
-    int rc = lbk_axpy2_dot(c, t, rin, s0, y1, rho0, ref_beta0, ref_alpha0, slot1);
-    if (!rc) rc = lbk_axpy2_dot(c, rout, t, s1, y2, rho1, slot1 * LBK_KMAX, ref_alpha1, slot2);
-    free(t);
-    return rc;
 }
 int lbk_last(lbk_ctx* c, double* dout, const double* r, const double* s, const double* g, double rho, int ref_beta,
              int ref_alpha, int slot) {

@@ -25,7 +25,7 @@ pytestmark = pytest.mark.gpu
 KNOBS = ["LBFGS_TICKET", "LBFGS_DEFER", "LBFGS_REV", "LBFGS_NT", "LBFGS_DIRECT", "LBFGS_COOP",
          "LBFGS_PERSIST", "LBFGS_PINGPONG", "LBFGS_SPEC", "LBFGS_BATCH", "LBFGS_SMALL_SEGS",
          "LBFGS_PERSIST_WG", "LBFGS_PERSIST_OWN", "LBFGS_PERSIST_ALT", "LBFGS_PERSIST_LDS", "LBFGS_COLLECT",
-         "LBFGS_COLLECT_TIMEOUT", "LBFGS_PAIR"]
+         "LBFGS_COLLECT_TIMEOUT"]
 
 VARIANTS = {
     "ticket1": {"LBFGS_TICKET": "1"},
@@ -47,11 +47,6 @@ VARIANTS = {
     "collect1_rev0_nt1": {"LBFGS_COLLECT": "1", "LBFGS_REV": "0", "LBFGS_NT": "1"},
     "collect1_defer0_batch0": {"LBFGS_COLLECT": "1", "LBFGS_DEFER": "0", "LBFGS_BATCH": "0"},
     "spec0": {"LBFGS_SPEC": "0"},
-    "pair1": {"LBFGS_PAIR": "1"},
-    "pair0": {"LBFGS_PAIR": "0"},
-    "pair1_ticket1_rev0": {"LBFGS_PAIR": "1", "LBFGS_TICKET": "1", "LBFGS_REV": "0"},
-    "pair1_collect1_pingpong1": {"LBFGS_PAIR": "1", "LBFGS_COLLECT": "1", "LBFGS_PINGPONG": "1"},
-    "pair1_defer_all_nt1": {"LBFGS_PAIR": "1", "LBFGS_DEFER": "8192", "LBFGS_TICKET": "0", "LBFGS_NT": "1"},
     "batch0": {"LBFGS_BATCH": "0"},
     "ticket1_direct0": {"LBFGS_TICKET": "1", "LBFGS_DIRECT": "0"},
     "ticket1_rev0_nt0": {"LBFGS_TICKET": "1", "LBFGS_REV": "0", "LBFGS_NT": "0"},

@@ -39,12 +39,8 @@ def built():
     return SAN
 
 
-@pytest.mark.parametrize("pair", ["0", "1"])
-def test_driver_and_shim_under_asan_ubsan(built, pair):
-    """pair "1": the two-loop passes in pairs (LBFGS_PAIR; the double runs each pair as its two
-    single passes, so the driver's pairing and slot bookkeeping are what is checked)"""
-    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1", UBSAN_OPTIONS="print_stacktrace=1",
-               LBFGS_PAIR=pair)
+def test_driver_and_shim_under_asan_ubsan(built):
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1", UBSAN_OPTIONS="print_stacktrace=1")
     p = subprocess.run([os.path.join(built, "_build", "san_driver")], capture_output=True, text=True, timeout=600,
                        env=env)
     tail = p.stdout[-1500:] + p.stderr[-3000:]
