@@ -160,8 +160,6 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
     // the ranks share the card; the saved copy is ~1 % of an 8-GPU iteration at best: opt-in
     c->xg_mirror = 0;
     if (const char* e = getenv("LBFGS_XGMI_MIRROR")) c->xg_mirror = atoi(e) != 0;
-    c->vf_dma = 0;
-    if (const char* e = getenv("LBFGS_VF_DMA")) c->vf_dma = atoi(e) != 0;
     *out = c;
 #define CK(expr)                                                                             \
     do {                                                                                     \

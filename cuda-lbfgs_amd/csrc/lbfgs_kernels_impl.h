@@ -1768,47 +1768,6 @@ struct OpVfCommit {
             if (l < 2 * B.h) r.b[l] = ldv<NT>(B.b[l] + i);
         form(r);
     }
-    // LDS-DMA form (stream_vf_dma): basis vectors l < ND of a row travel by DMA into this wave's
-    // LDS rows (lane's 16 B at dma + l * 128 + 2 lane); x, g and the basis vectors from ND on are
-    // register loads, issued a row ahead (RegRow)
-    template <int ND>
-    struct RegRow {
-        double2 x, g;
-        double2 b[2 * HB > ND ? 2 * HB - ND : 1];
-    };
-    template <int ND>
-    __device__ void reg_row(RegRow<ND>& n, int64_t i) const {
-        n.x = ldx<NT>(x + i);
-        n.g = ldx<NT>(g + i);
-#pragma unroll
-        for (int l = ND; l < 2 * HB; ++l)
-            if (l < 2 * B.h) n.b[l - ND] = ldv<NT>(B.b[l] + i);
-    }
-    template <int ND>
-    __device__ void take_row(Row& r, const RegRow<ND>& n, const double* dma, int lane) const {
-        r.x = n.x;
-        r.g = n.g;
-#pragma unroll
-        for (int l = 0; l < 2 * HB; ++l) {
-            if (l < 2 * B.h) {
-                if (l < ND)
-                    r.b[l] = *reinterpret_cast<const double2*>(dma + l * 128 + 2 * lane);
-                else
-                    r.b[l] = n.b[l - ND];
-            }
-        }
-    }
-    // DMA of the basis rows l < min(ND, 2h) of local element i (this lane's 16 B) into the wave's
-    // LDS rows: one wave-instruction per 1-KiB row, no registers (global_load_lds_dwordx4)
-    template <int ND>
-    __device__ void dma_row(int64_t i, double* dma) const {
-#pragma unroll
-        for (int l = 0; l < ND; ++l)
-            if (l < 2 * B.h)
-                __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(B.b[l] + i),
-                                                 (__attribute__((address_space(3))) void*)(dma + l * 128), 16, 0,
-                                                 NT ? 2 /* nt */ : 0);
-    }
     // d, z = x + alpha d and the candidate points from the loaded row (every basis product
     // rounded, l ascending, then g: the ORC_CANON_VF order)
     __device__ void form(Row& r) const {
@@ -1982,114 +1941,16 @@ __device__ __forceinline__ void stream_vf(const Op& op, const Seg& s, const Geo&
     if (last_lane && pvalid) op.finish(pz_m, pz_c, zedge, px, pg, park[s.w], pi, pe, pzc, zedge_c, acc);
 }
 
-// The same walk over a full segment with the next row's basis in flight (LBFGS_VF_DMA): the row's
-// first ND basis vectors travel by LDS-DMA into this wave's ND KiB of LDS, issued as soon as the
-// current row's copies have been read out of it, so they stream during the current row's
-// objective, stores and Gram reductions without holding registers (the commit's 2h + 2 rows and
-// 40 Gram accumulators fill 252 VGPRs: one row of register loads in flight, 2 waves per SIMD,
-// DESIGN.md §4). Same rows, same lanes, same operation order as stream_vf: the same bits.
-// Measured slower than the register form: compiled only into A/B variant builds
-// (-DLBK_VF_DMA=1, tools/build_variant.sh), where LBFGS_VF_DMA=1 selects it.
-#ifndef LBK_VF_DMA
-#define LBK_VF_DMA 0
-#endif
-#define LBK_VF_DMA_MAX 18  // basis rows per wave in LDS: 4 waves x 18 KiB + the static 2 KiB keep 2 workgroups per CU
-#define LBK_VF_DMA_HB 6    // smallest history bucket with the DMA form
-#ifndef LBK_VF_DMA_WAIT0
-#define LBK_VF_DMA_WAIT0 0  // A/B: wait for every outstanding access (the previous row's stores too)
-#endif
-template <int HB>
-constexpr int vf_dma_nd() {
-    return 2 * HB < LBK_VF_DMA_MAX ? 2 * HB : LBK_VF_DMA_MAX;
-}
-template <int ND, int K, class Op>
-__device__ __forceinline__ void stream_vf_dma(const Op& op, const Seg& s, const Geo& geo, double (&acc)[K],
-                                              double* dma_wg) {
-    constexpr int NB = Op::NB > 0 ? Op::NB : 1;
-    __shared__ double park[4][NB];
-    const int nrow = (int)(s.len >> 7);  // a full segment: whole rows
-    const int R = (nrow + 3) / 4;
-    const int r0 = s.w * R;
-    const int r1 = min(r0 + R, nrow);
-    if (r0 >= r1) return;
-    const bool last_lane = s.lane == 63;
-    double* dma = dma_wg + (size_t)s.w * ND * 128;
-    typename Op::template RegRow<ND> nx;
-    op.template dma_row<ND>(s.lb + (int64_t)r0 * 128 + 2 * s.lane, dma);
-    op.template reg_row<ND>(nx, s.lb + (int64_t)r0 * 128 + 2 * s.lane);
-    const double2 xd = op.xd_at(s.lane == 0 ? s.lb + (int64_t)r0 * 128 - 1 : s.lb + (int64_t)r1 * 128);
-    const double zedge = xd.x + op.alpha * xd.y;
-    double zedge_c[LBK_VF_NA], pzc[LBK_VF_NA], zfc[LBK_VF_NA];
-#pragma unroll
-    for (int j = 0; j < LBK_VF_NA; ++j) {
-        zedge_c[j] = xd.x + op.ac[j] * xd.y;
-        pzc[j] = 0.0;
-    }
-    double zl = zedge;
-    double pz_m = 0.0, pz_c = 0.0, px = 0.0, pg = 0.0;
-    int64_t pi = 0, pe = 0;
-    bool pvalid = false;
-    for (int row = r0; row < r1; ++row) {
-        const int64_t o = (int64_t)row * 128 + 2 * s.lane;
-        // this row's DMA and register loads have landed. Both were issued in the previous
-        // iteration ahead of its stores - apply's 4 (x_new, g_new, s, y) and, from its second row
-        // on, finish's 4 for lane 63 - which are at least that many vector-memory instructions
-        // however the compiler forms them (it cannot move them above the loads: both touch global
-        // memory it cannot tell apart); so waiting until at most that many are outstanding never
-        // waits on the stores and always covers this row. The first row also waits for xd_at.
-        if (LBK_VF_DMA_WAIT0 || row == r0)
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        else if (row == r0 + 1)
-            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        else
-            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        typename Op::Row r;
-        op.template take_row<ND>(r, nx, dma, s.lane);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the LDS rows are read out: free for the next DMA
-        if (row + 1 < r1) {
-            op.template dma_row<ND>(s.lb + o + 128, dma);
-            op.template reg_row<ND>(nx, s.lb + o + 128);
-        }
-        op.form(r);
-        const double zfirst = __shfl(r.z.x, 0, 64);
-#pragma unroll
-        for (int j = 0; j < LBK_VF_NA; ++j) zfc[j] = __shfl(r.zc[j].x, 0, 64);
-        if (last_lane && row > r0 && pvalid) op.finish(pz_m, pz_c, zfirst, px, pg, park[s.w], pi, pe, pzc, zfc, acc);
-        r.zh = zl;
-        op.template apply<true>(r, s.lb + o, s.sbeg + o, true, !last_lane, acc);
-        if (last_lane) {
-            pz_m = r.z.x;
-            pz_c = r.z.y;
-#pragma unroll
-            for (int j = 0; j < LBK_VF_NA; ++j) pzc[j] = r.zc[j].y;
-            px = r.x.y;
-            pg = r.g.y;
-            op.park(r, park[s.w]);
-            pi = s.lb + o + 1;
-            pe = s.sbeg + o + 1;
-            pvalid = true;
-        }
-        zl = __shfl(r.z.y, 63, 64);
-    }
-    if (last_lane && pvalid) op.finish(pz_m, pz_c, zedge, px, pg, park[s.w], pi, pe, pzc, zedge_c, acc);
-}
-
-template <int OBJ, int HB, bool NT, bool DMA = false>
+// (Two forms that stream the next row's basis by LDS-DMA while the current row computes were
+// measured slower, 1.7 % and 7 %, and removed: DESIGN.md §4.4, profiles/r04/vf_dma_ab/.)
+template <int OBJ, int HB, bool NT>
 __global__ __launch_bounds__(LB_BLOCK) void k_vf_commit(OpVfCommit<OBJ, HB, NT> op, Geo geo, Red red) {
     constexpr int K = OpVfCommit<OBJ, HB, NT>::K;
     const Seg s = seg_setup(geo);
     double acc[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) acc[k] = 0.0;
-    if constexpr (DMA && HB > 0) {
-        extern __shared__ __attribute__((aligned(16))) double vf_dma_lds[];
-        if (s.len == geo.L)
-            stream_vf_dma<vf_dma_nd<HB>()>(op, s, geo, acc, vf_dma_lds);
-        else
-            stream_vf(op, s, geo, acc);
-    } else {
-        stream_vf(op, s, geo, acc);
-    }
+    stream_vf(op, s, geo, acc);
     reduce_publish<K>(acc, geo, red);
 }
 
@@ -3034,7 +2895,6 @@ struct lbk_ctx {
     // LBFGS_CU_PARTITION (sharded, tests and one-card rehearsals): the solver stream runs on this
     // rank's own cu_count CUs, disjoint from every other rank's, as if each rank had a GPU
     int cu_part, cu_count;
-    int vf_dma;  // LBFGS_VF_DMA: the vector-free commit's next basis row by LDS-DMA (stream_vf_dma)
 };
 
 namespace {

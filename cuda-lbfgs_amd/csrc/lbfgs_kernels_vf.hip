@@ -48,29 +48,11 @@ int vf_commit_hb(lbk_ctx* c, int obj, int h, const double* x, const double* g, c
     Red r = kred(c, wslot);
     const VfBasis<HB> B = vf_basis<HB>(h, S, Y, cs, cy, cg);
     constexpr int K = LBK_VF_YB + 4 * HB + LBK_VF_NA;
-    // LBFGS_VF_DMA: the next row's basis by LDS-DMA (stream_vf_dma), ND KiB of LDS per wave
-    constexpr size_t dma_lds = HB > 0 ? (size_t)4 * vf_dma_nd<HB>() * 128 * sizeof(double) : 0;
-    const bool dma = c->vf_dma && h > 0;
     const int rc = launch(c, LBK_K_VF_COMMIT, 2.0 * h + 6.0, wslot, [&] {
         OBJ_DISPATCH(obj, {
             OpVfCommit<O_, HB, NT_> op{x, g, B, alpha, {cand[0]}, xn, gn, so, yo, geo.n, geo.n_loc};
-            bool done = false;
-            if constexpr (LBK_VF_DMA && HB >= LBK_VF_DMA_HB) {  // variant builds only
-                if (dma) {
-                    static bool attr = false;  // per instantiation: allow its dynamic LDS (> 64 KiB)
-                    if (!attr) {
-                        (void)hipFuncSetAttribute((const void*)k_vf_commit<O_, HB, NT_, true>,
-                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)dma_lds);
-                        attr = true;
-                    }
-                    hipLaunchKernelGGL((k_vf_commit<O_, HB, NT_, true>), dim3(geo_blocks(c, geo)), dim3(LB_BLOCK),
-                                       dma_lds, c->stream, op, geo, r);
-                    done = true;
-                }
-            }
-            if (!done)
-                hipLaunchKernelGGL((k_vf_commit<O_, HB, NT_>), dim3(geo_blocks(c, geo)), dim3(LB_BLOCK), 0, c->stream,
-                                   op, geo, r);
+            hipLaunchKernelGGL((k_vf_commit<O_, HB, NT_>), dim3(geo_blocks(c, geo)), dim3(LB_BLOCK), 0, c->stream, op,
+                               geo, r);
         });
         return 0;
     }, K, false, &geo);

@@ -193,47 +193,3 @@ def test_vector_free_geometry_edges_bit_exact(monkeypatch, n, ticket):
     assert np.array_equal(bits(r["tr_gnorm"]), bits(o["gnorm"]))
     assert np.array_equal(r["tr_c1"], o["c1"]) and np.array_equal(r["tr_c2"], o["c2"])
     assert np.array_equal(bits(r["x"]), bits(o["x"]))
-
-
-VFDMA_LIB = os.path.join(ROOT, "cuda-lbfgs_amd", "liblbfgs_hip_vfdma.so")
-_DMA_RUN = """
-import os, sys, numpy as np
-sys.path.insert(0, os.path.join({root!r}, "cuda-lbfgs_amd"))
-import lbfgs_amd as L
-n, m, obj, ls, iters, out = {n}, {m}, {obj!r}, {ls!r}, {iters}, {out!r}
-x0 = L.x0_uniform(n, 11, -2.0, 2.0)
-with L.Context(n, m) as c:
-    r = c.minimize(obj, x0, ls, iters, trace=True, vector_free=True)
-np.savez(out, tr_f=r["tr_f"], tr_gnorm=r["tr_gnorm"], x=r["x"], tr_c1=r["tr_c1"], tr_c2=r["tr_c2"],
-         iterations=r["iterations"], messages=r["messages"], info=L.build_info()[0])
-"""
-
-
-@pytest.mark.skipif(not os.path.exists(VFDMA_LIB), reason="variant build: tools/build_variant.sh vfdma -DLBK_VF_DMA=1")
-@pytest.mark.parametrize("n,m,obj,ls,iters", [
-    (3_000_017, 10, "rosenbrock", "backtracking", 16),    # HB 6..10: 12..18 basis rows by DMA, 2 by registers
-    (4_000_003, 20, "quad_tridiag", "wolfe", 26),        # HB 12..20: 18 by DMA, up to 22 by registers
-    (12_000_001, 7, "rosenbrock", "interpolation", 12),  # HB 8, longer segments, a short last segment
-])
-def test_vector_free_lds_dma_variant_bit_exact(tmp_path, n, m, obj, ls, iters):
-    """The LDS-DMA form of the vector-free commit (variant build, LBFGS_VF_DMA=1):
-    the next basis row travels by LDS-DMA on full segments; same rows, lanes and operation order,
-    so the same bits as the shipped register form (this process) and the oracle."""
-    import subprocess
-
-    out = str(tmp_path / "dma.npz")
-    env = dict(os.environ, LBFGS_LIB=VFDMA_LIB, LBFGS_VF_DMA="1")
-    subprocess.run([sys.executable, "-c", _DMA_RUN.format(root=ROOT, n=n, m=m, obj=obj, ls=ls, iters=iters, out=out)],
-                   env=env, check=True, timeout=300)
-    b = dict(np.load(out))
-    assert "+vfdma" in str(b["info"])
-    x0 = L.x0_uniform(n, 11, -2.0, 2.0)
-    with L.Context(n, m) as c:
-        a = c.minimize(obj, x0, ls, iters, trace=True, vector_free=True)
-    for key in ("tr_f", "tr_gnorm", "x"):
-        assert np.array_equal(bits(a[key]), bits(b[key])), key
-    assert np.array_equal(a["tr_c1"], b["tr_c1"]) and np.array_equal(a["tr_c2"], b["tr_c2"])
-    assert a["messages"] == str(b["messages"]) and a["iterations"] == int(b["iterations"])
-    if n == 3_000_017:
-        o = O.lbfgs(obj, O.x0_uniform(n, 11, -2.0, 2.0), ls, m, iters, 1e-5, mode=O.CANON, vector_free=True)
-        assert np.array_equal(bits(b["tr_f"]), bits(o["f"])) and np.array_equal(bits(b["x"]), bits(o["x"]))
