@@ -340,7 +340,8 @@ void print_cuda_progress(lbfgs_ctx* c, int status) {
 }
 
 vector<double> run(const FnF& f, const FnG& grad, const vector<double>& x0, int ls, int max_iterations,
-                   int m, double tolerance, bool verbose, const lbfgs_constants& k, bool cuda_progress = false) {
+                   int m, double tolerance, bool verbose, const lbfgs_constants& k, bool cuda_progress = false,
+                   bool cuda_compat = false) {
     const int64_t n = (int64_t)x0.size();
     if (n < 1) throw std::invalid_argument("x0 must not be empty");
     const int obj = identify(f, grad, (int)n);
@@ -366,6 +367,12 @@ vector<double> run(const FnF& f, const FnG& grad, const vector<double>& x0, int 
         const lbfgs_amd::DenseQuadF* df = dense_f(f);
         if (lbfgs_set_dense_quadratic(c, df->A->data(), df->b->data()) != 0)
             throw std::runtime_error(std::string("lbfgs_set_dense_quadratic failed: ") + lbfgs_last_error(c));
+    }
+    if (cuda_compat) {  // the CUDA path's own semantics; the library prints its stdout as it goes
+        if (obj >= LBFGS_OBJ_HOST)
+            throw std::invalid_argument("LBFGS_CUDA_COMPAT runs the device objectives (rosenbrock, the quadratics)");
+        flags |= LBFGS_FLAG_CUDA_COMPAT;
+        cuda_progress = false;
     }
     if (cuda_progress) {
         flags |= LBFGS_FLAG_TRACE | LBFGS_FLAG_QUIET;
@@ -395,7 +402,11 @@ vector<double> LBFGS_CUDA(const FnF f, const FnG grad, const vector<double> x0, 
     lbfgs_constants k;
     lbfgs_constants_cuda(&k);  // parallel-implementation/constants.h (C2 = 0.7)
     const char* p = std::getenv("LBFGS_CUDA_PROGRESS");
-    return run(f, grad, x0, ls, max_iterations, m, tolerance, false, k, p && std::atoi(p) != 0);
+    // LBFGS_CUDA_COMPAT=1: L-BFGS.cu's own semantics (LBFGS_FLAG_CUDA_COMPAT) instead of the
+    // sequential LBFGS's with the CUDA constants
+    const char* cc = std::getenv("LBFGS_CUDA_COMPAT");
+    return run(f, grad, x0, ls, max_iterations, m, tolerance, false, k, p && std::atoi(p) != 0,
+               cc && std::atoi(cc) != 0);
 }
 
 vector<double> LBFGS_CUDA(const FnF f, const FnG grad, const vector<double> x0, const int max_iterations,

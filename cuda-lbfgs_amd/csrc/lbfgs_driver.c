@@ -21,6 +21,7 @@
  * separately in the canonical reduction order (oracle/lbfgs_oracle.c, ORC_CANON).
  */
 #define _POSIX_C_SOURCE 199309L
+#include <float.h>
 #include <math.h>
 #include <stdarg.h>
 #include <stdio.h>
@@ -149,6 +150,11 @@ struct lbfgs_ctx {
     /* counters */
     int64_t trials_f, trials_fg, commits, passes;
     int h_min, h_max; /* pairs stored at the top of the iterations of the current call */
+    /* LBFGS_FLAG_CUDA_COMPAT: the CUDA path's per-ring-slot alpha and rho (kept across iterations
+     * as L-BFGS.cu's vector<double> alpha(m), rho(m)), its stale line-search gradient g0 */
+    int cuda;
+    double cu_alpha[MMAX], cu_rho[MMAX];
+    double* g0c;
     /* messages / trace */
     char* msg;
     int msg_len, msg_cap;
@@ -269,7 +275,7 @@ int lbfgs_unique_id(void* out128) { return lbk_unique_id(out128) == 0 ? 0 : LBFG
 int lbfgs_device_count(void) { return lbk_device_count(); }
 
 static void free_vectors(lbfgs_ctx* c) {
-    double** v[] = {&c->x, &c->g, &c->xn, &c->gn, &c->d, &c->q, &c->r, &c->gt, &c->q2, &c->r2};
+    double** v[] = {&c->x, &c->g, &c->xn, &c->gn, &c->d, &c->q, &c->r, &c->gt, &c->q2, &c->r2, &c->g0c};
     for (size_t i = 0; i < sizeof v / sizeof v[0]; ++i) {
         lbk_vec_free(c->dev, *v[i]);
         *v[i] = NULL;
@@ -1677,6 +1683,301 @@ static int iterate_vf(lbfgs_ctx* c) {
 }
 
 /* ------------------------------------------------------------------------------------------ */
+/* ------------------------------------------------------------------------------------------
+ * LBFGS_FLAG_CUDA_COMPAT: LBFGS_CUDA of parallel-implementation/L-BFGS.cu:195-358 with the
+ * line searches of parallel-implementation/line_search.cpp, on device vectors. The reference
+ * reads every cuBLAS dot back to the host (host-pointer mode); so does this path (one fetch per
+ * dot), and its line searches run on the host over device evaluations: f(x + a d) and
+ * g(x + a d) . d by the trial kernel, f(x) by the objective kernel, g0 . d as a canonical dot.
+ * ---------------------------------------------------------------------------------------- */
+static int cu_dot(lbfgs_ctx* c, const double* a, const double* b, double* out) {
+    DEV(lbk_dot(c->dev, a, b, SLOT_MISC(c->m)));
+    DEVNC(lbk_fetch(c->dev, SLOT_MISC(c->m), 1, out));
+    return 0;
+}
+
+static int cu_fx(lbfgs_ctx* c, double* f) { /* f(x): the objective kernel, its gradient into scratch */
+    double t[2];
+    DEV(lbk_eval(c->dev, c->obj, c->x, c->gt, SLOT_TRIAL(c->m)));
+    DEVNC(lbk_fetch(c->dev, SLOT_TRIAL(c->m), 2, t));
+    *f = t[0];
+    c->trials_f++;
+    return 0;
+}
+
+static int cu_ft(lbfgs_ctx* c, double a, double* f, double* gnd) { /* f(x + a d) [, g(x + a d) . d] */
+    double t[2];
+    DEV(lbk_trial(c->dev, c->obj, c->x, c->d, a, gnd ? c->gt : NULL, SLOT_TRIAL(c->m)));
+    DEVNC(lbk_fetch(c->dev, SLOT_TRIAL(c->m), gnd ? 2 : 1, t));
+    *f = t[0];
+    if (gnd) {
+        *gnd = t[1];
+        c->trials_fg++;
+    } else {
+        c->trials_f++;
+    }
+    return 0;
+}
+
+#define CU(call)                    \
+    do {                            \
+        const int rc_ = (call);     \
+        if (rc_) return rc_;        \
+    } while (0)
+
+static int cu_backtracking(lbfgs_ctx* c, double gd, double* out) { /* line_search.cpp:21-40 */
+    const lbfgs_constants* K = &c->K;
+    double fx, ft, alpha = K->initial_step;
+    CU(cu_fx(c, &fx)); /* the reference re-evaluates f(x) per trial: the same value */
+    for (;;) {
+        CU(cu_ft(c, alpha, &ft, NULL));
+        if (!(fx - ft < K->c1 * alpha * gd)) break;
+        alpha *= K->backtracking_alpha;
+        if (alpha < K->backtracking_tol) break;
+    }
+    *out = alpha < 1e-4 ? 0.5 : alpha;
+    return 0;
+}
+
+static int cu_backtracking_wolfe(lbfgs_ctx* c, double gd, double* out) { /* :42-147, its own constants */
+    const double C1 = 1e-4, C2 = 0.9, TOL = 1e-10;
+    double alpha = 1.0, f_current, alpha_lo = 0.0, alpha_hi = DBL_MAX;
+    double ca[24], cf[24]; /* the search's cache of f by alpha */
+    int nc = 0, iter = 0;
+    CU(cu_fx(c, &f_current));
+    while (iter++ < 20) {
+        int hit = -1;
+        for (int j = 0; j < nc; ++j)
+            if (ca[j] == alpha) hit = j;
+        double f_new;
+        if (hit >= 0) {
+            f_new = cf[hit];
+        } else {
+            CU(cu_ft(c, alpha, &f_new, NULL));
+            if (nc < 24) {
+                ca[nc] = alpha;
+                cf[nc++] = f_new;
+            }
+        }
+        if (f_new <= f_current + C1 * alpha * gd) {
+            double fg, gnd;
+            CU(cu_ft(c, alpha, &fg, &gnd)); /* grad(x_new) . d */
+            if (gnd >= C2 * gd) break;
+            alpha_lo = alpha;
+        } else {
+            alpha_hi = alpha;
+        }
+        if (alpha_hi < DBL_MAX)
+            alpha = (alpha_lo + alpha_hi) / 2.0;
+        else
+            alpha = 2.0 * alpha_lo;
+        if (alpha < TOL) break;
+    }
+    *out = alpha;
+    return 0;
+}
+
+static double cu_cubic(double a0, double a1, double p0, double dp0, double p1, double dp1) { /* :10-15 */
+    const double d1 = dp0 + dp1 - 3 * (p1 - p0) / (a1 - a0);
+    const double d2 = copysign(sqrt(d1 * d1 - dp0 * dp1), a1 - a0);
+    return a0 + (a1 - a0) * (dp0 + d2 - d1) / (dp0 - dp1 + 2 * d2);
+}
+
+static double cu_quad(double a0, double p0, double dp0, double p1) { /* :17-20 */
+    return a0 - 0.5 * dp0 * a0 * a0 / (p1 - p0 - dp0 * a0);
+}
+
+static int cu_interpolation(lbfgs_ctx* c, double gd, double* out) { /* :149-213 */
+    const lbfgs_constants* K = &c->K;
+    double f_x, alpha = K->initial_step, alpha_prev = 0.0, f_prev;
+    CU(cu_fx(c, &f_x));
+    f_prev = f_x;
+    int it = 0;
+    while (it++ < 20) {
+        double f_new;
+        CU(cu_ft(c, alpha, &f_new, NULL));
+        if (f_new <= f_x + K->c1 * alpha * gd) {
+            *out = alpha;
+            return 0;
+        }
+        if (alpha < K->wolfe_interp_min) {
+            *out = K->wolfe_interp_min;
+            return 0;
+        }
+        if (alpha_prev > 0) {
+            const double delta = alpha - alpha_prev;
+            if (fabs(delta) < 1e-10) {
+                alpha *= 0.5;
+            } else {
+                const double ga = (f_new - f_x - gd * alpha) / (alpha * alpha);
+                alpha = cu_cubic(alpha_prev, alpha, f_prev, gd, f_new, ga);
+                if (alpha < 0.1 * alpha_prev || alpha > 0.9 * alpha_prev) alpha = alpha_prev * 0.5;
+            }
+        } else {
+            alpha = cu_quad(alpha, f_new, gd, f_x);
+            if (alpha < 0.1 * K->initial_step || alpha > 0.9 * K->initial_step) alpha = K->initial_step * 0.5;
+        }
+        alpha_prev = alpha;
+        f_prev = f_new;
+    }
+    *out = alpha < 1e-4 ? 0.5 : alpha;
+    return 0;
+}
+
+/* :216-275: endpoints sorted, the midpoint whenever a step is not finite or the cubic has no
+ * real minimiser, the result kept 10 % inside the bracket */
+static double cu_safe_cubic(double a0, double a1, double p0, double dp0, double p1, double dp1) {
+    if (a0 > a1) {
+        double t = a0;
+        a0 = a1;
+        a1 = t;
+        t = p0;
+        p0 = p1;
+        p1 = t;
+        t = dp0;
+        dp0 = dp1;
+        dp1 = t;
+    }
+    const double d1 = dp0 + dp1 - 3 * (p1 - p0) / (a1 - a0);
+    if (isnan(d1) || isinf(d1)) return 0.5 * (a0 + a1);
+    const double disc = d1 * d1 - dp0 * dp1;
+    if (disc < 0) return 0.5 * (a0 + a1);
+    const double d2 = copysign(sqrt(disc), a1 - a0);
+    const double den = dp0 - dp1 + 2 * d2;
+    if (fabs(den) < 1e-10) return 0.5 * (a0 + a1);
+    const double r = a0 + (a1 - a0) * (dp0 + d2 - d1) / den;
+    if (isnan(r) || isinf(r)) return 0.5 * (a0 + a1);
+    const double lo = a0 + 0.1 * (a1 - a0), hi = a1 - 0.1 * (a1 - a0);
+    const double mn = (r < hi) ? r : hi; /* std::min(hi, r) */
+    return (lo < mn) ? mn : lo;          /* std::max(lo, .) */
+}
+
+static int cu_wolfe(lbfgs_ctx* c, double gd, double* out) { /* :277-368 */
+    const lbfgs_constants* K = &c->K;
+    double f_x, alpha = K->initial_step;
+    CU(cu_fx(c, &f_x));
+    double alpha_lo = 0.0, alpha_hi = INFINITY, f_lo = f_x, dphi_lo = gd;
+    for (int iter = 0; iter < 20; ++iter) {
+        double f_new;
+        CU(cu_ft(c, alpha, &f_new, NULL));
+        if (f_new > f_x + K->c1 * alpha * gd || (f_new >= f_lo && iter > 0)) {
+            alpha_hi = alpha;
+            alpha = cu_safe_cubic(alpha_lo, alpha_hi, f_lo, dphi_lo, f_new, (f_new - f_x - gd * alpha) / (alpha * alpha));
+            continue;
+        }
+        double fg, dphi_new;
+        CU(cu_ft(c, alpha, &fg, &dphi_new)); /* grad(x_new) . d */
+        if (fabs(dphi_new) <= -K->c2 * gd) {
+            *out = alpha;
+            return 0;
+        }
+        if (dphi_new >= 0) {
+            alpha_hi = alpha;
+            alpha = cu_safe_cubic(alpha_lo, alpha_hi, f_lo, dphi_lo, f_new, dphi_new);
+        } else {
+            alpha_lo = alpha;
+            f_lo = f_new;
+            dphi_lo = dphi_new;
+            if (alpha_hi == INFINITY)
+                alpha *= 2;
+            else
+                alpha = cu_safe_cubic(alpha_lo, alpha_hi, f_lo, dphi_lo, f_new, dphi_new);
+        }
+        if (alpha < K->wolfe_interp_min) {
+            *out = K->wolfe_interp_min;
+            return 0;
+        }
+    }
+    *out = alpha;
+    return 0;
+}
+
+/* one iteration k of L-BFGS.cu:195-358; returns 1 when the solve ended */
+static int iterate_cuda(lbfgs_ctx* c) {
+    const int k = c->k, m = c->m;
+    if (k == 0) {
+        DEV(lbk_elementwise(c->dev, 2, c->d, c->g, NULL, 0.0)); /* negateVector :208 */
+    } else {
+        DEVNC(lbk_copy(c->dev, c->q, c->g)); /* :212 */
+        const int lo = k - m > 0 ? k - m : 0;
+        for (int i = k - 1; i >= lo; --i) { /* :216-235 */
+            const int sl = i % m;
+            if (c->sy[sl] <= 1e-10) continue; /* alpha[sl], rho[sl] keep their last values */
+            c->cu_rho[sl] = 1.0 / c->sy[sl];
+            double sq;
+            CU(cu_dot(c, c->S[sl], c->q, &sq));
+            c->cu_alpha[sl] = c->cu_rho[sl] * sq;
+            DEV(lbk_elementwise(c->dev, 3, c->q, c->q, c->Y[sl], -c->cu_alpha[sl])); /* daxpy */
+        }
+        const int last = (k - 1) % m; /* :237-262 */
+        const double ys = c->sy[last], yy = c->yy[last];
+        const double gamma = (yy > 0 && ys > 1e-10) ? ys / yy : 1.0;
+        DEV(lbk_elementwise(c->dev, 0, c->r, c->q, NULL, gamma)); /* scaleByRho */
+        for (int i = lo; i < k; ++i) { /* :264-274 */
+            const int sl = i % m;
+            double yr;
+            CU(cu_dot(c, c->Y[sl], c->r, &yr));
+            const double beta = c->cu_rho[sl] * yr;
+            const double diff = c->cu_alpha[sl] - beta;
+            DEV(lbk_elementwise(c->dev, 3, c->r, c->r, c->S[sl], diff));
+        }
+        DEV(lbk_elementwise(c->dev, 2, c->d, c->r, NULL, 0.0)); /* :276 */
+    }
+    /* the line search with the iteration-0 gradient (:199, :293) */
+    double gd, step;
+    CU(cu_dot(c, c->g0c, c->d, &gd));
+    switch (c->ls) {
+        case LBFGS_LS_BACKTRACKING: CU(cu_backtracking(c, gd, &step)); break;
+        case LBFGS_LS_INTERPOLATION: CU(cu_interpolation(c, gd, &step)); break;
+        case LBFGS_LS_WOLFE: CU(cu_wolfe(c, gd, &step)); break;
+        default: CU(cu_backtracking_wolfe(c, gd, &step)); break;
+    }
+    if (step < 1e-10) { /* :295-306 */
+        say(c, "Warning: Line search failed at iteration %d\n", k);
+        c->status = LBFGS_STATUS_LS_FAILED;
+        return 1;
+    }
+    say(c, "alpha: %g\n", step); /* :308 */
+    DEV(lbk_point(c->dev, c->xn, c->x, c->d, step)); /* updateSolution :310 */
+    double t[2];
+    DEV(lbk_eval(c->dev, c->obj, c->xn, c->gn, SLOT_COMMIT0)); /* grad(x_new) :323, f(x_new) :348 */
+    DEVNC(lbk_fetch(c->dev, SLOT_COMMIT0, 2, t));
+    const int sl = k % m; /* updateVectors :332, whatever s.y */
+    DEV(lbk_elementwise(c->dev, 3, c->S[sl], c->xn, c->x, -1.0));
+    DEV(lbk_elementwise(c->dev, 3, c->Y[sl], c->gn, c->g, -1.0));
+    CU(cu_dot(c, c->S[sl], c->Y[sl], &c->sy[sl])); /* the next iteration's ddot(s, y) and ddot(y, y) */
+    CU(cu_dot(c, c->Y[sl], c->Y[sl], &c->yy[sl]));
+    {
+        double* tp = c->x; /* :335-340 */
+        c->x = c->xn;
+        c->xn = tp;
+        tp = c->g;
+        c->g = c->gn;
+        c->gn = tp;
+    }
+    c->commits++;
+    c->f_cur = t[0];
+    c->gg = t[1];
+    const double norm_g = sqrt(t[1]); /* :342-345 */
+    say(c, "Iteration %d: norm_g = %g\n", k, norm_g);
+    say(c, "Optimum value: %g\n", t[0]);
+    if (c->flags & LBFGS_FLAG_TRACE) {
+        CU(trace_push(c, t[0], norm_g, 1));
+        c->tr_a[c->tr_len - 1] = step;
+    }
+    const int h = k + 1 < m ? k + 1 : m; /* ring slots written */
+    if (c->h_min < 0 || h < c->h_min) c->h_min = h;
+    if (h > c->h_max) c->h_max = h;
+    c->k++;
+    if (norm_g <= c->tol) { /* :353-357 */
+        say(c, "Convergence achieved at iteration %d\n", k);
+        c->status = LBFGS_STATUS_CONVERGED;
+        return 1;
+    }
+    return 0;
+}
+#undef CU
+
 int lbfgs_solver_init(lbfgs_ctx* c, int objective, const lbfgs_host_fn* cb, int line_search,
                       const lbfgs_constants* k, const double* x0_host, double tolerance,
                       unsigned flags) {
@@ -1738,6 +2039,13 @@ int lbfgs_solver_init(lbfgs_ctx* c, int objective, const lbfgs_host_fn* cb, int 
             if (!c->Gss || !c->Gsy || !c->Gyy || !c->Gsg || !c->Gyg) return LBFGS_ERR_NOMEM;
         }
     }
+    c->cuda = (flags & LBFGS_FLAG_CUDA_COMPAT) != 0;
+    if (c->cuda) {
+        if (c->unfused || c->vf || objective >= LBFGS_OBJ_HOST || c->geo->world != 1) return LBFGS_ERR_BAD_ARG;
+        if (!c->g0c && !(c->g0c = lbk_vec_alloc(c->dev))) return LBFGS_ERR_NOMEM;
+        memset(c->cu_alpha, 0, sizeof c->cu_alpha); /* L-BFGS.cu:191-192: vector<double> alpha(m), rho(m) */
+        memset(c->cu_rho, 0, sizeof c->cu_rho);
+    }
     c->obj = objective;
     c->ls = line_search;
     if (k)
@@ -1780,6 +2088,10 @@ int lbfgs_solver_init(lbfgs_ctx* c, int objective, const lbfgs_host_fn* cb, int 
         c->gg = t[1];
         if (c->vf) DEVNC(lbk_vf_ghost_init(c->dev, c->x, c->g, LBK_WSLOT0));
     }
+    if (c->cuda) { /* L-BFGS.cu:115, :199 - the host gradient every line search will be given */
+        DEVNC(lbk_copy(c->dev, c->g0c, c->g));
+        say(c, "Starting\n");
+    }
     c->inited = 1;
     return 0;
 }
@@ -1811,7 +2123,7 @@ int lbfgs_solver_step(lbfgs_ctx* c, int max_steps, lbfgs_result* out) {
         for (int s = 0; s < max_steps; ++s) {
             c->steps_left = max_steps - s - 1;
             TRACE_PUSH("lbfgs iteration");
-            int rc = c->vf ? iterate_vf(c) : iterate(c);
+            int rc = c->cuda ? iterate_cuda(c) : c->vf ? iterate_vf(c) : iterate(c);
             TRACE_POP();
             if (rc < 0) {
                 (void)spec_drop(c);
@@ -1845,10 +2157,12 @@ int lbfgs_minimize(lbfgs_ctx* c, int objective, const lbfgs_host_fn* cb, int lin
     if (rc) return rc;
     rc = lbfgs_solver_step(c, max_iterations, NULL); /* sets h_min / h_max for the whole solve */
     if (rc < 0) return rc;
-    if (!c->finished) { /* :201-202 */
-        rc = trace_push(c, c->f_cur, sqrt(c->gg), 1);
-        if (rc) return rc;
-        say(c, "Maximum iterations reached\n");
+    if (!c->finished) { /* :201-202 (the CUDA path's loop just ends, L-BFGS.cu:358-365) */
+        if (!c->cuda) {
+            rc = trace_push(c, c->f_cur, sqrt(c->gg), 1);
+            if (rc) return rc;
+            say(c, "Maximum iterations reached\n");
+        }
         c->status = LBFGS_STATUS_MAX_ITER;
         c->finished = 1;
     }
@@ -2017,6 +2331,7 @@ int lbfgs_line_search(lbfgs_ctx* c, int objective, const lbfgs_host_fn* cb, int 
     c->cand_valid = 0;
     c->tc_n = 0;
     c->trial_passes = 0;
+    c->cuda = 0;
     c->obj = objective;
     c->ls = line_search;
     if (k)

@@ -94,6 +94,19 @@ enum {
  * Default: one f and at most one grad call per distinct point (same iterates either way for a
  * deterministic objective). */
 #define LBFGS_FLAG_REFERENCE_CALLS 32u
+/* the CUDA path's semantics, LBFGS_CUDA of parallel-implementation/L-BFGS.cu:105-380, for callers
+ * that want its iterates rather than the sequential LBFGS's: the first-loop pairs with s.y <= 1e-10
+ * skipped (their alpha and rho kept from the last time the ring slot was used, :222-223), gamma = 1
+ * when y.y or s.y fail (:237-262), the ring slot k % m written unconditionally (:332), every line
+ * search given the iteration-0 gradient (:199,293), the line searches of
+ * parallel-implementation/line_search.cpp (their 0.5 floors, the bisection Wolfe search, the
+ * safeguarded cubic), convergence tested after the step with <= (:353), and its stdout lines
+ * ("alpha: ..", "Iteration k: norm_g = ..", "Optimum value: .."). Single rank, device objectives;
+ * every vector stays on the device, scalars round-trip per dot as the cuBLAS host-pointer calls do.
+ * Bit-exact with the oracle's restatement of that path (ORC_CANON); parity with the CUDA program
+ * itself is unpinned (no CUDA toolchain here), its line searches are pinned against
+ * line_search.cpp compiled here. Trace entry k = the state iteration k prints after its step. */
+#define LBFGS_FLAG_CUDA_COMPAT 64u
 
 typedef struct {
     double c1;                 /* C1 = 1e-4                  config.h:5 */

@@ -8,6 +8,7 @@
  */
 #include "lbfgs_oracle.h"
 
+#include <float.h>
 #include <math.h>
 #include <stdarg.h>
 #include <stdio.h>
@@ -921,6 +922,312 @@ done:
 #undef VGI
 
 /* ------------------------------------------------------------------------------------------
+ * The CUDA path (orc_opts.cuda = 1): LBFGS_CUDA of parallel-implementation/L-BFGS.cu:105-380 with
+ * the host line searches of parallel-implementation/line_search.cpp (its own versions: floors,
+ * a cached bisection Wolfe search, a safeguarded cubic). The line searches are pinned call for
+ * call against that file compiled here (oracle/ref_cuda_ls.cpp); the loop's cuBLAS dots and axpys
+ * cannot run here, so the loop is restated only ("parity unpinned": their summation order is
+ * cuBLAS's; ORC_SEQ sums left to right, ORC_CANON in the product's order).
+ * ---------------------------------------------------------------------------------------- */
+static double pls_dot(ctx_t* c, const double* a, const double* b) { return orc_dot(a, b, c->n, c->o->mode); }
+
+static double pls_backtracking(ctx_t* c, const double* x, const double* d, const double* g) {
+    const orc_opts* o = c->o; /* parallel line_search.cpp:21-40 (the sequential search plus a floor) */
+    double alpha = o->initial_step;
+    for (;;) {
+        double fx = F(c, x);
+        trial_point(x, d, alpha, c->n, c->tmp);
+        double ft = F(c, c->tmp);
+        double gd = pls_dot(c, g, d);
+        if (!(fx - ft < o->c1 * alpha * gd)) break;
+        alpha *= o->backtracking_alpha;
+        if (alpha < o->backtracking_tol) break;
+    }
+    if (alpha < 1e-4) return 0.5; /* :36-39 */
+    return alpha;
+}
+
+/* :42-147: constants of its own (C1 1e-4, C2 0.9, tolerance 1e-10); bisection between alpha_lo
+ * and alpha_hi, doubling while alpha_hi is unset; f values cached by alpha (a repeated alpha is
+ * not evaluated again) */
+#define PLS_CACHE 24
+static double pls_backtracking_wolfe(ctx_t* c, const double* x, const double* d, const double* g, double* gnew) {
+    const double C1 = 1e-4, C2 = 0.9, TOL = 1e-10;
+    double alpha = 1.0;
+    int iter = 0;
+    const double f_current = F(c, x);
+    const double gd = pls_dot(c, g, d);
+    double ca[PLS_CACHE], cf[PLS_CACHE];
+    int nc = 0;
+    double alpha_lo = 0.0, alpha_hi = DBL_MAX;
+    while (iter++ < 20) {
+        int hit = -1;
+        for (int j = 0; j < nc; ++j)
+            if (ca[j] == alpha) hit = j;
+        double f_new;
+        trial_point(x, d, alpha, c->n, c->tmp); /* x_new (the cached point has the same bits) */
+        if (hit >= 0) {
+            f_new = cf[hit];
+        } else {
+            f_new = F(c, c->tmp);
+            if (nc < PLS_CACHE) {
+                ca[nc] = alpha;
+                cf[nc++] = f_new;
+            }
+        }
+        if (f_new <= f_current + C1 * alpha * gd) {
+            G(c, c->tmp, gnew);
+            const double gnd = pls_dot(c, gnew, d);
+            if (gnd >= C2 * gd) break;
+            alpha_lo = alpha;
+        } else {
+            alpha_hi = alpha;
+        }
+        if (alpha_hi < DBL_MAX)
+            alpha = (alpha_lo + alpha_hi) / 2.0;
+        else
+            alpha = 2.0 * alpha_lo;
+        if (alpha < TOL) break;
+    }
+    return alpha;
+}
+
+static double pls_interpolation(ctx_t* c, const double* x, const double* d, const double* g) {
+    const orc_opts* o = c->o; /* :149-213 (the sequential search plus a floor after 20 trials) */
+    const double f_x = F(c, x);
+    const double gd = pls_dot(c, g, d);
+    double alpha = o->initial_step, alpha_prev = 0.0, f_prev = f_x;
+    int it = 0;
+    while (it++ < 20) {
+        trial_point(x, d, alpha, c->n, c->tmp);
+        double f_new = F(c, c->tmp);
+        if (f_new <= f_x + o->c1 * alpha * gd) return alpha;
+        if (alpha < o->wolfe_interp_min) return o->wolfe_interp_min;
+        if (alpha_prev > 0) {
+            double delta = alpha - alpha_prev;
+            if (fabs(delta) < 1e-10) {
+                alpha *= 0.5;
+            } else {
+                double ga = (f_new - f_x - gd * alpha) / (alpha * alpha);
+                alpha = cubic_interp(alpha_prev, alpha, f_prev, gd, f_new, ga);
+                if (alpha < 0.1 * alpha_prev || alpha > 0.9 * alpha_prev) alpha = alpha_prev * 0.5;
+            }
+        } else {
+            alpha = quad_interp(alpha, 0.0, f_new, gd, f_x);
+            if (alpha < 0.1 * o->initial_step || alpha > 0.9 * o->initial_step) alpha = o->initial_step * 0.5;
+        }
+        alpha_prev = alpha;
+        f_prev = f_new;
+    }
+    if (alpha < 1e-4) return 0.5; /* :209-212 */
+    return alpha;
+}
+
+/* :216-275 safeCubicInterpolate: sorted endpoints, the midpoint whenever a step is not finite
+ * or the cubic has no real minimiser, and the result kept 10 % inside the bracket */
+static double pls_safe_cubic(double a0, double a1, double p0, double dp0, double p1, double dp1) {
+    if (a0 > a1) {
+        double t = a0; a0 = a1; a1 = t;
+        t = p0; p0 = p1; p1 = t;
+        t = dp0; dp0 = dp1; dp1 = t;
+    }
+    const double d1 = dp0 + dp1 - 3 * (p1 - p0) / (a1 - a0);
+    if (isnan(d1) || isinf(d1)) return 0.5 * (a0 + a1);
+    const double disc = d1 * d1 - dp0 * dp1;
+    if (disc < 0) return 0.5 * (a0 + a1);
+    const double d2 = copysign(sqrt(disc), a1 - a0);
+    const double den = dp0 - dp1 + 2 * d2;
+    if (fabs(den) < 1e-10) return 0.5 * (a0 + a1);
+    const double r = a0 + (a1 - a0) * (dp0 + d2 - d1) / den;
+    if (isnan(r) || isinf(r)) return 0.5 * (a0 + a1);
+    const double lo = a0 + 0.1 * (a1 - a0), hi = a1 - 0.1 * (a1 - a0);
+    const double mn = (r < hi) ? r : hi;   /* std::min(hi, r) */
+    return (lo < mn) ? mn : lo;            /* std::max(lo, min) */
+}
+
+static double pls_wolfe(ctx_t* c, const double* x, const double* d, const double* g, double* gnew) {
+    const orc_opts* o = c->o; /* :277-368 */
+    const double f_x = F(c, x);
+    const double gd = pls_dot(c, g, d);
+    double alpha = o->initial_step;
+    double alpha_lo = 0.0, alpha_hi = INFINITY, f_lo = f_x, dphi_lo = gd;
+    for (int iter = 0; iter < 20; ++iter) {
+        trial_point(x, d, alpha, c->n, c->tmp);
+        double f_new = F(c, c->tmp);
+        if (f_new > f_x + o->c1 * alpha * gd || (f_new >= f_lo && iter > 0)) {
+            alpha_hi = alpha;
+            alpha = pls_safe_cubic(alpha_lo, alpha_hi, f_lo, dphi_lo, f_new,
+                                   (f_new - f_x - gd * alpha) / (alpha * alpha));
+            continue;
+        }
+        G(c, c->tmp, gnew);
+        double dphi_new = pls_dot(c, gnew, d);
+        if (fabs(dphi_new) <= -o->c2 * gd) return alpha;
+        if (dphi_new >= 0) {
+            alpha_hi = alpha;
+            alpha = pls_safe_cubic(alpha_lo, alpha_hi, f_lo, dphi_lo, f_new, dphi_new);
+        } else {
+            alpha_lo = alpha;
+            f_lo = f_new;
+            dphi_lo = dphi_new;
+            if (alpha_hi == INFINITY)
+                alpha *= 2;
+            else
+                alpha = pls_safe_cubic(alpha_lo, alpha_hi, f_lo, dphi_lo, f_new, dphi_new);
+        }
+        if (alpha < o->wolfe_interp_min) return o->wolfe_interp_min;
+    }
+    return alpha;
+}
+
+static double pls_run(ctx_t* c, int ls, const double* x, const double* d, const double* g, double* gnew) {
+    switch (ls) {
+        case ORC_LS_BACKTRACKING: return pls_backtracking(c, x, d, g);
+        case ORC_LS_INTERPOLATION: return pls_interpolation(c, x, d, g);
+        case ORC_LS_WOLFE: return pls_wolfe(c, x, d, g, gnew);
+        default: return pls_backtracking_wolfe(c, x, d, g, gnew);
+    }
+}
+
+int orc_cuda_line_search(const orc_opts* o, const double* x, const double* d, const double* g, double* alpha,
+                         double* flog, int64_t flog_cap, int64_t* flog_n, uint64_t* glog, int64_t glog_cap,
+                         int64_t* glog_n) {
+    ctx_t C;
+    memset(&C, 0, sizeof C);
+    C.o = o;
+    C.n = o->n;
+    C.flog = flog;
+    C.flog_cap = flog_cap;
+    C.glog = glog;
+    C.glog_cap = glog_cap;
+    C.tmp = (double*)malloc(sizeof(double) * (size_t)o->n);
+    double* gnew = (double*)malloc(sizeof(double) * (size_t)o->n);
+    if (!C.tmp || !gnew) return -1;
+    *alpha = pls_run(&C, o->ls, x, d, g, gnew);
+    if (flog_n) *flog_n = C.flog_n;
+    if (glog_n) *glog_n = C.glog_n;
+    free(C.tmp);
+    free(gnew);
+    return 0;
+}
+
+/* L-BFGS.cu:195-358. Trace entry k is the state the iteration prints after its step: f(x_{k+1})
+ * ("Optimum value"), |g_{k+1}| ("norm_g"), alpha_k, the x_{k+1} checksums. */
+static int orc_lbfgs_cuda(const orc_opts* o, const double* x0, double* x_out, double* tr_f, double* tr_gnorm,
+                          double* tr_alpha, uint64_t* tr_c1, uint64_t* tr_c2, int64_t* tr_nf, int trace_cap,
+                          ctx_t* C, orc_result* res) {
+    const int64_t n = o->n;
+    const int m = o->m, mode = o->mode;
+    const size_t vb = sizeof(double) * (size_t)n;
+    double *x = malloc(vb), *g = malloc(vb), *d = malloc(vb), *q = malloc(vb), *r = malloc(vb), *xn = malloc(vb),
+           *gn = malloc(vb), *g0 = malloc(vb), *gt = malloc(vb);
+    C->tmp = malloc(vb);
+    double** S = calloc((size_t)m, sizeof(double*));
+    double** Y = calloc((size_t)m, sizeof(double*));
+    double* alpha = calloc((size_t)m, sizeof(double)); /* vector<double> alpha(m), rho(m): zeros */
+    double* rho = calloc((size_t)m, sizeof(double));
+    for (int i = 0; i < m; ++i) {
+        S[i] = calloc((size_t)n, sizeof(double));
+        Y[i] = calloc((size_t)n, sizeof(double));
+    }
+    say(C, "Starting\n"); /* :115 */
+    memcpy(x, x0, vb);
+    G(C, x0, g0); /* :199 - the host gradient, never updated: every line search gets it */
+    memcpy(g, g0, vb);
+    int status = ORC_MAX_ITER, ntr = 0, k;
+    int64_t skips = 0;
+    for (k = 0; k < o->maxit; ++k) {
+        if (k == 0) {
+            for (int64_t i = 0; i < n; ++i) d[i] = -g[i]; /* :208 */
+        } else {
+            memcpy(q, g, vb); /* :212 */
+            const int lo = k - m > 0 ? k - m : 0;
+            for (int i = k - 1; i >= lo; --i) { /* :216-235 */
+                const int sl = i % m;
+                const double sy = orc_dot(S[sl], Y[sl], n, mode);
+                if (sy <= 1e-10) { /* alpha[sl], rho[sl] keep their last values */
+                    skips++;
+                    continue;
+                }
+                rho[sl] = 1.0 / sy;
+                const double sq = orc_dot(S[sl], q, n, mode);
+                alpha[sl] = rho[sl] * sq;
+                const double na = -alpha[sl];
+                for (int64_t j = 0; j < n; ++j) q[j] = q[j] + na * Y[sl][j]; /* cublasDaxpy */
+            }
+            {
+                const int last = (k - 1) % m; /* :237-262 */
+                const double ys = orc_dot(S[last], Y[last], n, mode);
+                const double yy = orc_dot(Y[last], Y[last], n, mode);
+                const double gamma = (yy > 0 && ys > 1e-10) ? ys / yy : 1.0;
+                for (int64_t j = 0; j < n; ++j) r[j] = q[j] * gamma; /* scaleByRho */
+            }
+            for (int i = lo; i < k; ++i) { /* :264-274 */
+                const int sl = i % m;
+                const double yr = orc_dot(Y[sl], r, n, mode);
+                const double beta = rho[sl] * yr;
+                const double diff = alpha[sl] - beta;
+                for (int64_t j = 0; j < n; ++j) r[j] = r[j] + diff * S[sl][j];
+            }
+            for (int64_t j = 0; j < n; ++j) d[j] = -r[j]; /* :276 */
+        }
+        const double step = pls_run(C, o->ls, x, d, g0, gt); /* :293, the stale gradient */
+        if (step < 1e-10) { /* :295-306 */
+            say(C, "Warning: Line search failed at iteration %d\n", k);
+            status = ORC_LS_FAILED;
+            goto done;
+        }
+        say(C, "alpha: %g\n", step); /* :308 */
+        for (int64_t j = 0; j < n; ++j) xn[j] = x[j] + step * d[j]; /* updateSolution :310 */
+        G(C, xn, gn); /* :323 */
+        {
+            const int sl = k % m; /* updateVectors :332, unconditionally */
+            for (int64_t j = 0; j < n; ++j) {
+                S[sl][j] = xn[j] - x[j];
+                Y[sl][j] = gn[j] - g[j];
+            }
+        }
+        memcpy(x, xn, vb); /* :335-340 */
+        memcpy(g, gn, vb);
+        const double norm_g = sqrt(orc_dot(g, g, n, mode)); /* :342-345 */
+        const double fv = F(C, xn);                          /* :348 */
+        say(C, "Iteration %d: norm_g = %g\n", k, norm_g);
+        say(C, "Optimum value: %g\n", fv);
+        if (ntr < trace_cap) {
+            tr_f[ntr] = fv;
+            tr_gnorm[ntr] = norm_g;
+            tr_alpha[ntr] = step;
+            orc_checksum(x, n, &tr_c1[ntr], &tr_c2[ntr]);
+            tr_nf[ntr] = C->nf;
+        }
+        ntr++;
+        if (norm_g <= o->tol) { /* :353-357 */
+            say(C, "Convergence achieved at iteration %d\n", k);
+            status = ORC_CONVERGED;
+            k++;
+            goto done;
+        }
+    }
+done:
+    if (x_out) memcpy(x_out, x, vb);
+    if (res) {
+        res->iters = k;
+        res->status = status;
+        res->ntrace = ntr;
+        res->nf = C->nf;
+        res->ng = C->ng;
+        res->skips = skips;
+    }
+    free(x); free(g); free(d); free(q); free(r); free(xn); free(gn); free(g0); free(gt); free(C->tmp);
+    for (int i = 0; i < m; ++i) {
+        free(S[i]);
+        free(Y[i]);
+    }
+    free(S); free(Y); free(alpha); free(rho);
+    return 0;
+}
+
+/* ------------------------------------------------------------------------------------------
  * LBFGS — lbfgs.cpp:17-203.
  * ---------------------------------------------------------------------------------------- */
 int orc_lbfgs(const orc_opts* o, const double* x0, double* x_out,
@@ -943,6 +1250,12 @@ int orc_lbfgs(const orc_opts* o, const double* x0, double* x_out,
     C.msg = msg;
     C.msg_cap = msg_cap;
     if (msg && msg_cap > 0) msg[0] = 0;
+    if (o->cuda) {
+        int rc = orc_lbfgs_cuda(o, x0, x_out, tr_f, tr_gnorm, tr_alpha, tr_c1, tr_c2, tr_nf, trace_cap, &C, res);
+        if (flog_n) *flog_n = C.flog_n;
+        if (glog_n) *glog_n = C.glog_n;
+        return rc;
+    }
     if (o->vf) {
         if (m > 64) return -1;
         int rc = orc_lbfgs_vf(o, x0, x_out, tr_f, tr_gnorm, tr_alpha, tr_c1, tr_c2, tr_nf, trace_cap, &C, res);

@@ -52,11 +52,15 @@ typedef struct {
     /* 1: vector-free (Gram-matrix) variant of the product's LBFGS_FLAG_VECTOR_FREE mode,
      * restated in ORC_CANON order (not a reference algorithm; its own parity contract) */
     int vf;
+    /* 1: the CUDA path - LBFGS_CUDA of parallel-implementation/L-BFGS.cu:105-380 with the line
+     * searches of parallel-implementation/line_search.cpp (the product's LBFGS_FLAG_CUDA_COMPAT) */
+    int cuda;
 } orc_opts;
 
 typedef struct {
     int iters, status, ntrace;
     int64_t nf, ng;
+    int64_t skips; /* the CUDA path: first-loop pairs skipped for s.y <= 1e-10 (L-BFGS.cu:222-223) */
 } orc_result;
 
 /* x0 exactly as std::mt19937(seed) + std::uniform_real_distribution<double>(lo, hi)
@@ -92,6 +96,12 @@ int orc_lbfgs(const orc_opts* o, const double* x0, double* x_out,
               char* msg, int msg_cap, orc_result* res);
 
 void orc_checksum(const double* x, int64_t n, uint64_t* c1, uint64_t* c2);
+
+/* one line search of parallel-implementation/line_search.cpp (orc_opts.ls, constants in o; the
+ * CUDA path's searches) from x along d with gradient g; f / grad calls logged as in orc_lbfgs */
+int orc_cuda_line_search(const orc_opts* o, const double* x, const double* d, const double* g, double* alpha,
+                         double* flog, int64_t flog_cap, int64_t* flog_n, uint64_t* glog, int64_t glog_cap,
+                         int64_t* glog_n);
 
 /* two-loop recursion alone for history S/Y[0..h-1] (oldest first); writes d, returns g.d */
 double orc_twoloop(const double* g, const double* const* S, const double* const* Y, int h,

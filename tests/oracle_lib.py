@@ -34,7 +34,7 @@ class Opts(C.Structure):
                 ("backtracking_alpha", C.c_double), ("backtracking_tol", C.c_double),
                 ("wolfe_interp_min", C.c_double),
                 ("host_f", C.c_void_p), ("host_g", C.c_void_p), ("host_user", C.c_void_p),
-                ("vf", C.c_int)]
+                ("vf", C.c_int), ("cuda", C.c_int)]
 
 
 HOST_F = C.CFUNCTYPE(C.c_double, C.POINTER(C.c_double), C.c_int64, C.c_void_p)
@@ -55,7 +55,7 @@ def host_callbacks(f, grad):
 
 class Result(C.Structure):
     _fields_ = [("iters", C.c_int), ("status", C.c_int), ("ntrace", C.c_int),
-                ("nf", C.c_int64), ("ng", C.c_int64)]
+                ("nf", C.c_int64), ("ng", C.c_int64), ("skips", C.c_int64)]
 
 
 _lib = None
@@ -145,7 +145,7 @@ def np_checksum(x):
 
 
 def lbfgs(obj, x0, ls, m, maxit, tol, mode=CANON, consts=None, log_calls=False, verbose=False,
-          f=None, grad=None, vector_free=False):
+          f=None, grad=None, vector_free=False, cuda=False):
     """Run the oracle; returns a dict with x, trace arrays, call logs and messages.
     obj="host" takes the objective from the Python callables f(x) and grad(x)."""
     x0 = np.ascontiguousarray(x0, np.float64)
@@ -154,7 +154,7 @@ def lbfgs(obj, x0, ls, m, maxit, tol, mode=CANON, consts=None, log_calls=False, 
     if consts:
         k.update(consts)
     o = Opts(obj=OBJ[obj], ls=LS[ls], mode=mode, verbose=int(verbose), n=n, m=m, maxit=maxit,
-             tol=tol, vf=int(vector_free), **k)
+             tol=tol, vf=int(vector_free), cuda=int(cuda), **k)
     cbs = None
     if obj == "host":
         cbs = host_callbacks(f, grad)
@@ -178,9 +178,35 @@ def lbfgs(obj, x0, ls, m, maxit, tol, mode=CANON, consts=None, log_calls=False, 
     nt = res.ntrace
     return dict(x=x, f=trf[:nt].copy(), gnorm=trg[:nt].copy(), alpha=tra[:nt].copy(),
                 c1=tc1[:nt].copy(), c2=tc2[:nt].copy(), nf=tnf[:nt].copy(),
-                iters=res.iters, status=STATUS[res.status], nf_total=res.nf, ng_total=res.ng,
+                iters=res.iters, status=STATUS[res.status], nf_total=res.nf, ng_total=res.ng, skips=res.skips,
                 flog=flog[:fn.value].copy(), glog=glog[:gn.value].reshape(-1, 3).copy(),
                 messages=msg.value.decode())
+
+
+# parallel-implementation/constants.h:5-17 (the CUDA path's constants: C2 = 0.7)
+CONSTANTS_H = dict(CONFIG_H, c2=0.7)
+
+
+def cuda_line_search(ls, x, d, g, mode=SEQ, obj="rosenbrock"):
+    """One line search of parallel-implementation/line_search.cpp restated (orc_cuda_line_search),
+    constants.h constants: (alpha, f-call values, grad-call log rows (c1, c2, |g| bits))."""
+    L = lib()
+    L.orc_cuda_line_search.argtypes = [C.POINTER(Opts), np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS"),
+                                       np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS"),
+                                       np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS"),
+                                       C.POINTER(C.c_double),
+                                       np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS"), C.c_int64,
+                                       C.POINTER(C.c_int64),
+                                       np.ctypeslib.ndpointer(dtype=np.uint64, flags="C_CONTIGUOUS"), C.c_int64,
+                                       C.POINTER(C.c_int64)]
+    x, d, g = (np.ascontiguousarray(v, np.float64) for v in (x, d, g))
+    o = Opts(obj=OBJ[obj], ls=LS[ls], mode=mode, verbose=0, n=len(x), m=1, maxit=1, tol=0.0, vf=0, cuda=1,
+             **CONSTANTS_H)
+    flog, glog = np.empty(256), np.empty(3 * 64, np.uint64)
+    a, fn, gn = C.c_double(), C.c_int64(), C.c_int64()
+    assert L.orc_cuda_line_search(C.byref(o), x, d, g, C.byref(a), flog, len(flog), C.byref(fn), glog, len(glog),
+                                  C.byref(gn)) == 0
+    return a.value, flog[:fn.value].copy(), glog[:gn.value].reshape(-1, 3).copy()
 
 
 _dense_refs = []
@@ -203,7 +229,7 @@ def load_golden(name):
 
 def golden_cases():
     return sorted(f[:-5] for f in os.listdir(GOLDEN)
-                  if f.endswith(".json") and not f.startswith(("kat_", "stress_")) and f != "horizons.json")
+                  if f.endswith(".json") and not f.startswith(("kat_", "stress_")) and f not in ("horizons.json", "cuda_ls.json"))
 
 
 def stress_cases():

@@ -343,3 +343,31 @@ def test_cuda_progress_lines(tmp_path):
     assert len(want) == 1 + 3 * 40
     r0 = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
     assert r0.returncode == 0 and "Starting" not in r0.stdout and "alpha: " not in r0.stdout
+
+
+@pytest.mark.gpu
+def test_cuda_compat_env(tmp_path):
+    """LBFGS_CUDA_COMPAT=1: LBFGS_CUDA runs L-BFGS.cu's own semantics (LBFGS_FLAG_CUDA_COMPAT) and
+    prints its stdout as the library goes; it equals the C ABI's cuda_compat run of the same solve,
+    which tests/test_gpu_cuda_compat.py pins to the oracle's restatement of the CUDA path"""
+    src = tmp_path / "p.cpp"
+    src.write_text(_PROGRESS_CALLER)
+    exe = tmp_path / "p"
+    subprocess.run(["g++", "-std=c++17", "-O2", "-I", os.path.join(ROOT, "include"), str(src), "-o",
+                    str(exe), "-L", PKG, "-l:liblbfgs_hip.so", "-Wl,-rpath," + PKG], check=True, capture_output=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, LBFGS_CUDA_COMPAT="1"))
+    assert r.returncode == 0, r.stderr
+    import sys
+
+    if PKG not in sys.path:
+        sys.path.insert(0, PKG)
+    import lbfgs_amd as LA
+
+    x0 = O.x0_uniform(1000, 42, -2.0, 2.0)
+    with LA.Context(1000, 5, device=0) as ctx:
+        t = ctx.minimize("rosenbrock", x0, "backtracking", 40, tolerance=1e-5, cuda_compat=True,
+                         consts=LA.constants("cuda"))
+    lines = r.stdout.splitlines()
+    assert lines[0] == "Starting" and lines[-1] == "END 1000"
+    assert lines[:-1] == t["messages"].splitlines()
