@@ -341,7 +341,7 @@ void print_cuda_progress(lbfgs_ctx* c, int status) {
 
 vector<double> run(const FnF& f, const FnG& grad, const vector<double>& x0, int ls, int max_iterations,
                    int m, double tolerance, bool verbose, const lbfgs_constants& k, bool cuda_progress = false,
-                   bool cuda_compat = false) {
+                   bool cuda_compat = false, bool cuda_variant = false) {
     const int64_t n = (int64_t)x0.size();
     if (n < 1) throw std::invalid_argument("x0 must not be empty");
     const int obj = identify(f, grad, (int)n);
@@ -371,7 +371,7 @@ vector<double> run(const FnF& f, const FnG& grad, const vector<double>& x0, int 
     if (cuda_compat) {  // the CUDA path's own semantics; the library prints its stdout as it goes
         if (obj >= LBFGS_OBJ_HOST)
             throw std::invalid_argument("LBFGS_CUDA_COMPAT runs the device objectives (rosenbrock, the quadratics)");
-        flags |= LBFGS_FLAG_CUDA_COMPAT;
+        flags |= LBFGS_FLAG_CUDA_COMPAT | (cuda_variant ? LBFGS_FLAG_CUDA_VARIANT : 0u);
         cuda_progress = false;
     }
     if (cuda_progress) {
@@ -396,24 +396,38 @@ vector<double> LBFGS(const FnF f, const FnG grad, const vector<double> x0, const
     return run(f, grad, x0, ls, max_iterations, m, tolerance, verbose, k);
 }
 
-vector<double> LBFGS_CUDA(const FnF f, const FnG grad, const vector<double> x0, const std::string line_search_method,
-                          const int max_iterations, const int m, const double tolerance) {
-    const int ls = line_search_id(line_search_method);
+namespace {
+vector<double> cuda_solve(const FnF& f, const FnG& grad, const vector<double>& x0, const std::string& method,
+                          int max_iterations, int m, double tolerance, bool variant) {
+    const int ls = line_search_id(method);
     lbfgs_constants k;
     lbfgs_constants_cuda(&k);  // parallel-implementation/constants.h (C2 = 0.7)
     const char* p = std::getenv("LBFGS_CUDA_PROGRESS");
-    // LBFGS_CUDA_COMPAT=1: L-BFGS.cu's own semantics (LBFGS_FLAG_CUDA_COMPAT) instead of the
-    // sequential LBFGS's with the CUDA constants
+    // LBFGS_CUDA_COMPAT=1: the CUDA program's own semantics (LBFGS_FLAG_CUDA_COMPAT: L-BFGS.cu's
+    // for the string form, the variant file's for the string-less one) instead of the sequential
+    // LBFGS's with the CUDA constants
     const char* cc = std::getenv("LBFGS_CUDA_COMPAT");
     return run(f, grad, x0, ls, max_iterations, m, tolerance, false, k, p && std::atoi(p) != 0,
-               cc && std::atoi(cc) != 0);
+               cc && std::atoi(cc) != 0, variant);
+}
+}  // namespace
+
+vector<double> LBFGS_CUDA(const FnF f, const FnG grad, const vector<double> x0, const std::string line_search_method,
+                          const int max_iterations, const int m, const double tolerance) {
+    return cuda_solve(f, grad, x0, line_search_method, max_iterations, m, tolerance, false);
+}
+
+vector<double> lbfgs_amd::cuda_variant(const FnF& f, const FnG& grad, const vector<double>& x0,
+                                       const std::string& variant, int max_iterations, int m, double tolerance) {
+    return cuda_solve(f, grad, x0, variant, max_iterations, m, tolerance, true);
 }
 
 vector<double> LBFGS_CUDA(const FnF f, const FnG grad, const vector<double> x0, const int max_iterations,
                           const int m, const double tolerance) {
     // the variant a caller built without -DLBFGS_CUDA_VARIANT runs (lbfgs.h): env, else backtracking
     const char* v = std::getenv("LBFGS_CUDA_VARIANT");
-    return LBFGS_CUDA(f, grad, x0, std::string(v && *v ? v : "backtracking"), max_iterations, m, tolerance);
+    return lbfgs_amd::cuda_variant(f, grad, x0, std::string(v && *v ? v : "backtracking"), max_iterations, m,
+                                   tolerance);
 }
 
 int lbfgs_amd::last_objective() { return g_last_objective; }

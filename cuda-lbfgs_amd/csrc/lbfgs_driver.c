@@ -152,7 +152,9 @@ struct lbfgs_ctx {
     int h_min, h_max; /* pairs stored at the top of the iterations of the current call */
     /* LBFGS_FLAG_CUDA_COMPAT: the CUDA path's per-ring-slot alpha and rho (kept across iterations
      * as L-BFGS.cu's vector<double> alpha(m), rho(m)), its stale line-search gradient g0 */
-    int cuda;
+    int cuda;          /* 1: LBFGS_FLAG_CUDA_COMPAT (L-BFGS.cu), 2: with LBFGS_FLAG_CUDA_VARIANT */
+    double cv_f0;      /* the variants' initial_f = f(x0) */
+    double cv_fhost;   /* f at their host copy x_host: the last trial point a search transferred */
     double cu_alpha[MMAX], cu_rho[MMAX];
     double* g0c;
     /* messages / trace */
@@ -1892,6 +1894,160 @@ static int cu_wolfe(lbfgs_ctx* c, double gd, double* out) { /* :277-368 */
     return 0;
 }
 
+/* ------------------------------------------------------------------------------------------
+ * LBFGS_FLAG_CUDA_VARIANT: the inline searches of the four variant files. Each trial transfers
+ * x + a d to the host copy x_host, so f(x_host) at the next iteration is the f of the last trial
+ * point transferred (cv_fhost), not f(x). ok = the search's line_search_success.
+ * ---------------------------------------------------------------------------------------- */
+static int cv_backtracking(lbfgs_ctx* c, double gd, double* out) { /* L-BFGS-Backtracking.cu:293-341 */
+    const double C1 = 1e-4, TOL = 1e-10; /* :153-156, the file's own constants */
+    double fx, ft, step = 1.0;
+    CU(cu_fx(c, &fx)); /* f(x_host), x_host freshly copied from d_x */
+    for (;;) {
+        CU(cu_ft(c, step, &ft, NULL));
+        if (ft <= fx + C1 * step * gd) break;
+        step *= 0.5;
+        if (step < TOL) {
+            step = 0.5;
+            break;
+        }
+    }
+    *out = step;
+    return 0;
+}
+
+static int cv_interpolation(lbfgs_ctx* c, double gd, double* out, int* ok) { /* L-BFGS-Interpolation.cu:259-342 */
+    const lbfgs_constants* K = &c->K;
+    const double f_x = c->cv_fhost;
+    double alpha = K->initial_step, alpha_prev = 0.0, f_prev = c->cv_f0;
+    *ok = 0;
+    for (int iter = 0; iter < 20; ++iter) {
+        double f_new;
+        CU(cu_ft(c, alpha, &f_new, NULL));
+        c->cv_fhost = f_new;
+        if (f_new <= f_x + K->c1 * alpha * gd) {
+            *ok = 1;
+            break;
+        }
+        if (alpha < K->wolfe_interp_min) {
+            alpha = K->wolfe_interp_min;
+            break;
+        }
+        if (alpha_prev > 0) {
+            const double delta = alpha - alpha_prev;
+            if (fabs(delta) < 1e-10) {
+                alpha *= 0.5;
+            } else {
+                const double ga = (f_new - f_x - gd * alpha) / (alpha * alpha);
+                double next = cu_cubic(alpha_prev, alpha, f_prev, gd, f_new, ga);
+                if (next < 0.1 * alpha_prev || next > 0.9 * alpha_prev) next = alpha_prev * 0.5;
+                alpha = next;
+            }
+        } else {
+            double next = cu_quad(alpha, f_new, gd, f_x);
+            if (next < 0.1 * K->initial_step || next > 0.9 * K->initial_step) next = K->initial_step * 0.5;
+            alpha = next;
+        }
+        alpha_prev = alpha; /* after the update (:335) */
+        f_prev = f_new;
+    }
+    if (alpha < 1e-4) alpha = 0.5; /* :339-342 */
+    *out = alpha;
+    return 0;
+}
+
+static int cv_wolfe(lbfgs_ctx* c, double gd, double* out, int* ok) { /* L-BFGS-Wolfe.cu:259-349 */
+    const lbfgs_constants* K = &c->K;
+    const double f_x = c->cv_fhost;
+    double alpha = K->initial_step, alpha_lo = 0.0, alpha_hi = INFINITY, f_lo = c->cv_f0, dphi_lo = gd;
+    *ok = 0;
+    for (int iter = 0; iter < 20; ++iter) {
+        double f_new;
+        CU(cu_ft(c, alpha, &f_new, NULL));
+        c->cv_fhost = f_new;
+        if (f_new > f_x + K->c1 * alpha * gd || (f_new >= f_lo && iter > 0)) {
+            alpha_hi = alpha;
+            alpha = cu_safe_cubic(alpha_lo, alpha_hi, f_lo, dphi_lo, f_new, (f_new - f_x - gd * alpha) / (alpha * alpha));
+            continue; /* past the WOLFE_INTERP_MIN floor */
+        }
+        double fg, dphi_new;
+        CU(cu_ft(c, alpha, &fg, &dphi_new)); /* grad(x_host) . d */
+        if (fabs(dphi_new) <= -K->c2 * gd) {
+            *ok = 1;
+            break;
+        }
+        if (dphi_new >= 0) {
+            alpha_hi = alpha;
+            alpha = cu_safe_cubic(alpha_lo, alpha_hi, f_lo, dphi_lo, f_new, dphi_new);
+        } else {
+            alpha_lo = alpha;
+            f_lo = f_new;
+            dphi_lo = dphi_new;
+            if (alpha_hi == INFINITY)
+                alpha *= 2;
+            else
+                alpha = cu_safe_cubic(alpha_lo, alpha_hi, f_lo, dphi_lo, f_new, dphi_new);
+        }
+        if (alpha < K->wolfe_interp_min) {
+            alpha = K->wolfe_interp_min;
+            break;
+        }
+    }
+    *out = alpha;
+    return 0;
+}
+
+static int cv_backtracking_wolfe(lbfgs_ctx* c, double gd, double* out, int* ok) { /* L-BFGS-Backtracking_Wolfe.cu:256-397 */
+    const double C1 = 1e-4, C2 = 0.9, TOL = 1e-10; /* :261-264, the file's own constants */
+    const double f_x = c->cv_fhost;
+    double alpha = 1.0, alpha_lo = 0.0, alpha_hi = DBL_MAX;
+    double ca[24], cf[24], cgd[24]; /* cache: f by alpha, and g(x + alpha d) . d once evaluated */
+    int cg[24], nc = 0;
+    *ok = 0;
+    for (int iter = 0; iter < 20; ++iter) {
+        int hit = -1;
+        for (int j = 0; j < nc; ++j)
+            if (ca[j] == alpha) hit = j;
+        if (hit < 0) {
+            double f_new;
+            CU(cu_ft(c, alpha, &f_new, NULL));
+            c->cv_fhost = f_new;
+            hit = nc++;
+            ca[hit] = alpha;
+            cf[hit] = f_new;
+            cg[hit] = 0;
+        }
+        if (cf[hit] <= f_x + C1 * alpha * gd) {
+            if (!cg[hit]) { /* x + alpha d transferred again, its gradient evaluated */
+                double fg;
+                c->cv_fhost = cf[hit];
+                CU(cu_ft(c, alpha, &fg, &cgd[hit]));
+                cg[hit] = 1;
+            }
+            if (cgd[hit] >= C2 * gd) {
+                *ok = 1;
+                break;
+            }
+            alpha_lo = alpha;
+        } else {
+            alpha_hi = alpha;
+        }
+        if (alpha_hi < DBL_MAX)
+            alpha = (alpha_lo + alpha_hi) / 2.0;
+        else
+            alpha = 2.0 * alpha_lo;
+        if (alpha < TOL) {
+            double f_t;
+            alpha = TOL;
+            CU(cu_ft(c, alpha, &f_t, NULL));
+            c->cv_fhost = f_t;
+            break;
+        }
+    }
+    *out = alpha;
+    return 0;
+}
+
 /* one iteration k of L-BFGS.cu:195-358; returns 1 when the solve ended */
 static int iterate_cuda(lbfgs_ctx* c) {
     const int k = c->k, m = c->m;
@@ -1923,21 +2079,40 @@ static int iterate_cuda(lbfgs_ctx* c) {
         }
         DEV(lbk_elementwise(c->dev, 2, c->d, c->r, NULL, 0.0)); /* :276 */
     }
-    /* the line search with the iteration-0 gradient (:199, :293) */
     double gd, step;
-    CU(cu_dot(c, c->g0c, c->d, &gd));
-    switch (c->ls) {
-        case LBFGS_LS_BACKTRACKING: CU(cu_backtracking(c, gd, &step)); break;
-        case LBFGS_LS_INTERPOLATION: CU(cu_interpolation(c, gd, &step)); break;
-        case LBFGS_LS_WOLFE: CU(cu_wolfe(c, gd, &step)); break;
-        default: CU(cu_backtracking_wolfe(c, gd, &step)); break;
+    if (c->cuda == 2) { /* the variants: the current gradient (d_g), their own searches */
+        int ok = 1;
+        CU(cu_dot(c, c->g, c->d, &gd));
+        switch (c->ls) {
+            case LBFGS_LS_BACKTRACKING: CU(cv_backtracking(c, gd, &step)); break;
+            case LBFGS_LS_INTERPOLATION: CU(cv_interpolation(c, gd, &step, &ok)); break;
+            case LBFGS_LS_WOLFE: CU(cv_wolfe(c, gd, &step, &ok)); break;
+            default: CU(cv_backtracking_wolfe(c, gd, &step, &ok)); break;
+        }
+        say(c, "alpha: %g\n", step);
+        if (c->ls == LBFGS_LS_BACKTRACKING) {
+            if (step < 1e-4) /* L-BFGS-Backtracking.cu:345-348 */
+                say(c, "Warning: Line search resulted in very small step size at iteration %d\n", k);
+        } else if (!ok && step < 1e-10) { /* e.g. L-BFGS-Wolfe.cu:353-366 */
+            say(c, "Warning: Line search failed at iteration %d\n", k);
+            c->status = LBFGS_STATUS_LS_FAILED;
+            return 1;
+        }
+    } else { /* the line search with the iteration-0 gradient (:199, :293) */
+        CU(cu_dot(c, c->g0c, c->d, &gd));
+        switch (c->ls) {
+            case LBFGS_LS_BACKTRACKING: CU(cu_backtracking(c, gd, &step)); break;
+            case LBFGS_LS_INTERPOLATION: CU(cu_interpolation(c, gd, &step)); break;
+            case LBFGS_LS_WOLFE: CU(cu_wolfe(c, gd, &step)); break;
+            default: CU(cu_backtracking_wolfe(c, gd, &step)); break;
+        }
+        if (step < 1e-10) { /* :295-306 */
+            say(c, "Warning: Line search failed at iteration %d\n", k);
+            c->status = LBFGS_STATUS_LS_FAILED;
+            return 1;
+        }
+        say(c, "alpha: %g\n", step); /* :308 */
     }
-    if (step < 1e-10) { /* :295-306 */
-        say(c, "Warning: Line search failed at iteration %d\n", k);
-        c->status = LBFGS_STATUS_LS_FAILED;
-        return 1;
-    }
-    say(c, "alpha: %g\n", step); /* :308 */
     DEV(lbk_point(c->dev, c->xn, c->x, c->d, step)); /* updateSolution :310 */
     double t[2];
     DEV(lbk_eval(c->dev, c->obj, c->xn, c->gn, SLOT_COMMIT0)); /* grad(x_new) :323, f(x_new) :348 */
@@ -2040,6 +2215,8 @@ int lbfgs_solver_init(lbfgs_ctx* c, int objective, const lbfgs_host_fn* cb, int 
         }
     }
     c->cuda = (flags & LBFGS_FLAG_CUDA_COMPAT) != 0;
+    if ((flags & LBFGS_FLAG_CUDA_VARIANT) && !c->cuda) return LBFGS_ERR_BAD_ARG;
+    if (c->cuda && (flags & LBFGS_FLAG_CUDA_VARIANT)) c->cuda = 2;
     if (c->cuda) {
         if (c->unfused || c->vf || objective >= LBFGS_OBJ_HOST || c->geo->world != 1) return LBFGS_ERR_BAD_ARG;
         if (!c->g0c && !(c->g0c = lbk_vec_alloc(c->dev))) return LBFGS_ERR_NOMEM;
@@ -2090,6 +2267,7 @@ int lbfgs_solver_init(lbfgs_ctx* c, int objective, const lbfgs_host_fn* cb, int 
     }
     if (c->cuda) { /* L-BFGS.cu:115, :199 - the host gradient every line search will be given */
         DEVNC(lbk_copy(c->dev, c->g0c, c->g));
+        c->cv_f0 = c->cv_fhost = c->f_cur; /* the variants' initial_f = f(x_host), x_host = x0 */
         say(c, "Starting\n");
     }
     c->inited = 1;

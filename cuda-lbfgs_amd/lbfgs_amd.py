@@ -21,7 +21,8 @@ LINE_SEARCHES = {"backtracking": 0, "interpolation": 1, "wolfe": 2, "backtrackin
 STATUS = {0: "converged", 1: "max_iter", 2: "ls_failed", 3: "running"}
 FLAG_VERBOSE, FLAG_QUIET, FLAG_TRACE, FLAG_UNFUSED, FLAG_VECTOR_FREE = 1, 2, 4, 8, 16
 FLAG_REFERENCE_CALLS = 32
-FLAG_CUDA_COMPAT = 64  # LBFGS_CUDA's semantics (parallel-implementation/L-BFGS.cu), include/lbfgs_hip.h
+FLAG_CUDA_COMPAT = 64
+FLAG_CUDA_VARIANT = 128  # LBFGS_CUDA's semantics (parallel-implementation/L-BFGS.cu), include/lbfgs_hip.h
 KERNELS = ["dot", "axpy_dot", "mid", "axpy2_dot", "last", "negdot", "eval", "trial_f",
            "trial_fg", "commit", "point", "checksum", "update", "vf_commit", "vf_dir", "small_iter",
            "group_reduce", "exchange"]
@@ -382,7 +383,7 @@ class Context:
     def minimize(self, objective, x0, line_search="backtracking", max_iterations=1000, m=None,
                  tolerance=1e-5, verbose=False, quiet=True, trace=False, consts=None,
                  f=None, grad=None, unfused=False, vector_free=False, reference_calls=False, out=None,
-                 cuda_compat=False):
+                 cuda_compat=False, cuda_variant=False):
         """out: a caller-owned float64 buffer of n for the result (else a new array; a fresh
         array's pages are first touched by the result's copy, which costs as much as the copy)"""
         assert m is None or m == self.m
@@ -395,7 +396,7 @@ class Context:
         flags = (FLAG_VERBOSE if verbose else 0) | (FLAG_QUIET if quiet else 0) | \
                 (FLAG_TRACE if trace else 0) | (FLAG_UNFUSED if unfused else 0) | \
                 (FLAG_VECTOR_FREE if vector_free else 0) | (FLAG_REFERENCE_CALLS if reference_calls else 0) | \
-                (FLAG_CUDA_COMPAT if cuda_compat else 0)
+                (FLAG_CUDA_COMPAT if cuda_compat else 0) | (FLAG_CUDA_VARIANT if cuda_variant else 0)
         cb = self._host_fn(f, grad) if objective == "host" else None
         k = consts if consts is not None else constants()
         rc = lib().lbfgs_minimize(self.h, OBJECTIVES[objective], C.byref(cb) if cb else None,

@@ -35,12 +35,22 @@ std::vector<double> LBFGS_CUDA(const std::function<double(std::vector<double>)> 
  * "interpolation", "backtracking_wolfe"), or at run time with the environment variable
  * LBFGS_CUDA_VARIANT; with neither it is "backtracking" (L-BFGS-Backtracking.cu). An unknown name
  * throws std::invalid_argument as the string form does. */
+namespace lbfgs_amd {
+/* the string-less LBFGS_CUDA of the variant file `variant` names: the string form's solve, or with
+ * the environment variable LBFGS_CUDA_COMPAT=1 that file's own loop and inline line search
+ * (LBFGS_FLAG_CUDA_COMPAT | LBFGS_FLAG_CUDA_VARIANT, lbfgs_hip.h) */
+std::vector<double> cuda_variant(const std::function<double(std::vector<double>)>& f,
+                                 const std::function<std::vector<double>(std::vector<double>)>& grad,
+                                 const std::vector<double>& x0, const std::string& variant, int max_iterations,
+                                 int m, double tolerance);
+}  // namespace lbfgs_amd
+
 #ifdef LBFGS_CUDA_VARIANT
 static inline std::vector<double> LBFGS_CUDA(const std::function<double(std::vector<double>)> f,
                                              const std::function<std::vector<double>(std::vector<double>)> grad,
                                              const std::vector<double> x0, const int max_iterations, const int m,
                                              const double tolerance) {
-    return LBFGS_CUDA(f, grad, x0, std::string(LBFGS_CUDA_VARIANT), max_iterations, m, tolerance);
+    return lbfgs_amd::cuda_variant(f, grad, x0, std::string(LBFGS_CUDA_VARIANT), max_iterations, m, tolerance);
 }
 #else
 std::vector<double> LBFGS_CUDA(const std::function<double(std::vector<double>)> f,

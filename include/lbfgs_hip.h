@@ -107,6 +107,15 @@ enum {
  * itself is unpinned (no CUDA toolchain here), its line searches are pinned against
  * line_search.cpp compiled here. Trace entry k = the state iteration k prints after its step. */
 #define LBFGS_FLAG_CUDA_COMPAT 64u
+/* with LBFGS_FLAG_CUDA_COMPAT: the string-less LBFGS_CUDA of the four variant files instead, each
+ * with its own inline line search (the line_search argument names the file): backtracking =
+ * L-BFGS-Backtracking.cu:293-348 (correct-sign Armijo, 0.5 when the step falls below 1e-10, the
+ * "very small step size" warning below 1e-4), interpolation = L-BFGS-Interpolation.cu:259-358,
+ * wolfe = L-BFGS-Wolfe.cu:259-366, backtracking_wolfe = L-BFGS-Backtracking_Wolfe.cu:256-415.
+ * Their searches take the current gradient, f(x) from the host copy of the last trial point the
+ * previous search transferred (x0 at k = 0), and the interpolation and Wolfe searches start
+ * f_prev / f_lo from f(x0) every iteration. Parity unpinned (the searches are inline in .cu files). */
+#define LBFGS_FLAG_CUDA_VARIANT 128u
 
 typedef struct {
     double c1;                 /* C1 = 1e-4                  config.h:5 */

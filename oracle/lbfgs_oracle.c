@@ -1111,6 +1111,165 @@ int orc_cuda_line_search(const orc_opts* o, const double* x, const double* d, co
     return 0;
 }
 
+/* ------------------------------------------------------------------------------------------
+ * The variant files (orc_opts.cuda = 2): the string-less LBFGS_CUDA of L-BFGS-Backtracking.cu,
+ * -Interpolation.cu, -Wolfe.cu and -Backtracking_Wolfe.cu, the same loop as L-BFGS.cu around an
+ * inline search of each file's own. Their searches get the current gradient (d_g); all but the
+ * backtracking file take f(x) as f(x_host), the host copy of the LAST trial point the previous
+ * search transferred (x0 at k = 0), and start f_prev / f_lo from f(x0) (initial_f) every time.
+ * vs->fhost is that f, vs->f0 = f(x0). ok = the file's line_search_success. Parity unpinned: the
+ * searches live in .cu files that cannot be built here.
+ * ---------------------------------------------------------------------------------------- */
+typedef struct {
+    double f0, fhost;
+} vstate_t;
+
+static double vls_backtracking(ctx_t* c, const double* x, const double* d, double gd) {
+    const double C1 = 1e-4, TOL = 1e-10; /* L-BFGS-Backtracking.cu:153-156 */
+    const double fx = F(c, x);            /* :304-309, x_host copied from d_x */
+    double step = 1.0;
+    for (;;) { /* :311-340 */
+        trial_point(x, d, step, c->n, c->tmp);
+        const double ft = F(c, c->tmp);
+        if (ft <= fx + C1 * step * gd) break;
+        step *= 0.5;
+        if (step < TOL) {
+            step = 0.5;
+            break;
+        }
+    }
+    return step;
+}
+
+static double vls_interpolation(ctx_t* c, vstate_t* vs, const double* x, const double* d, double gd, int* ok) {
+    const orc_opts* o = c->o; /* L-BFGS-Interpolation.cu:259-342 */
+    const double f_x = vs->fhost;
+    double alpha = o->initial_step, alpha_prev = 0.0, f_prev = vs->f0;
+    *ok = 0;
+    for (int iter = 0; iter < 20; ++iter) {
+        trial_point(x, d, alpha, c->n, c->tmp);
+        const double f_new = F(c, c->tmp);
+        vs->fhost = f_new;
+        if (f_new <= f_x + o->c1 * alpha * gd) {
+            *ok = 1;
+            break;
+        }
+        if (alpha < o->wolfe_interp_min) {
+            alpha = o->wolfe_interp_min;
+            break;
+        }
+        if (alpha_prev > 0) {
+            const double delta = alpha - alpha_prev;
+            if (fabs(delta) < 1e-10) {
+                alpha *= 0.5;
+            } else {
+                const double ga = (f_new - f_x - gd * alpha) / (alpha * alpha);
+                double next = cubic_interp(alpha_prev, alpha, f_prev, gd, f_new, ga);
+                if (next < 0.1 * alpha_prev || next > 0.9 * alpha_prev) next = alpha_prev * 0.5;
+                alpha = next;
+            }
+        } else {
+            double next = quad_interp(alpha, 0.0, f_new, gd, f_x);
+            if (next < 0.1 * o->initial_step || next > 0.9 * o->initial_step) next = o->initial_step * 0.5;
+            alpha = next;
+        }
+        alpha_prev = alpha; /* :335, after the update */
+        f_prev = f_new;
+    }
+    if (alpha < 1e-4) alpha = 0.5; /* :339-342 */
+    return alpha;
+}
+
+static double vls_wolfe(ctx_t* c, vstate_t* vs, const double* x, const double* d, double gd, double* gnew, int* ok) {
+    const orc_opts* o = c->o; /* L-BFGS-Wolfe.cu:259-349 */
+    const double f_x = vs->fhost;
+    double alpha = o->initial_step, alpha_lo = 0.0, alpha_hi = INFINITY, f_lo = vs->f0, dphi_lo = gd;
+    *ok = 0;
+    for (int iter = 0; iter < 20; ++iter) {
+        trial_point(x, d, alpha, c->n, c->tmp);
+        const double f_new = F(c, c->tmp);
+        vs->fhost = f_new;
+        if (f_new > f_x + o->c1 * alpha * gd || (f_new >= f_lo && iter > 0)) {
+            alpha_hi = alpha;
+            alpha = pls_safe_cubic(alpha_lo, alpha_hi, f_lo, dphi_lo, f_new, (f_new - f_x - gd * alpha) / (alpha * alpha));
+            continue;
+        }
+        G(c, c->tmp, gnew);
+        const double dphi_new = pls_dot(c, gnew, d);
+        if (fabs(dphi_new) <= -o->c2 * gd) {
+            *ok = 1;
+            break;
+        }
+        if (dphi_new >= 0) {
+            alpha_hi = alpha;
+            alpha = pls_safe_cubic(alpha_lo, alpha_hi, f_lo, dphi_lo, f_new, dphi_new);
+        } else {
+            alpha_lo = alpha;
+            f_lo = f_new;
+            dphi_lo = dphi_new;
+            if (alpha_hi == INFINITY)
+                alpha *= 2;
+            else
+                alpha = pls_safe_cubic(alpha_lo, alpha_hi, f_lo, dphi_lo, f_new, dphi_new);
+        }
+        if (alpha < o->wolfe_interp_min) {
+            alpha = o->wolfe_interp_min;
+            break;
+        }
+    }
+    return alpha;
+}
+
+static double vls_backtracking_wolfe(ctx_t* c, vstate_t* vs, const double* x, const double* d, double gd,
+                                     double* gnew, int* ok) {
+    const double C1 = 1e-4, C2 = 0.9, TOL = 1e-10; /* L-BFGS-Backtracking_Wolfe.cu:261-264 */
+    const double f_x = vs->fhost;
+    double alpha = 1.0, alpha_lo = 0.0, alpha_hi = DBL_MAX;
+    double ca[PLS_CACHE], cf[PLS_CACHE], cgd[PLS_CACHE]; /* cache / grad_cache by alpha */
+    int cg[PLS_CACHE], nc = 0;
+    *ok = 0;
+    for (int iter = 0; iter < 20; ++iter) { /* :279-397 */
+        int hit = -1;
+        for (int j = 0; j < nc; ++j)
+            if (ca[j] == alpha) hit = j;
+        if (hit < 0) {
+            trial_point(x, d, alpha, c->n, c->tmp);
+            hit = nc++;
+            ca[hit] = alpha;
+            cf[hit] = F(c, c->tmp);
+            cg[hit] = 0;
+            vs->fhost = cf[hit];
+        }
+        if (cf[hit] <= f_x + C1 * alpha * gd) {
+            if (!cg[hit]) { /* the point transferred again, its gradient evaluated and cached */
+                trial_point(x, d, alpha, c->n, c->tmp);
+                vs->fhost = cf[hit];
+                G(c, c->tmp, gnew);
+                cgd[hit] = pls_dot(c, gnew, d);
+                cg[hit] = 1;
+            }
+            if (cgd[hit] >= C2 * gd) {
+                *ok = 1;
+                break;
+            }
+            alpha_lo = alpha;
+        } else {
+            alpha_hi = alpha;
+        }
+        if (alpha_hi < DBL_MAX)
+            alpha = (alpha_lo + alpha_hi) / 2.0;
+        else
+            alpha = 2.0 * alpha_lo;
+        if (alpha < TOL) {
+            alpha = TOL;
+            trial_point(x, d, alpha, c->n, c->tmp);
+            vs->fhost = F(c, c->tmp);
+            break;
+        }
+    }
+    return alpha;
+}
+
 /* L-BFGS.cu:195-358. Trace entry k is the state the iteration prints after its step: f(x_{k+1})
  * ("Optimum value"), |g_{k+1}| ("norm_g"), alpha_k, the x_{k+1} checksums. */
 static int orc_lbfgs_cuda(const orc_opts* o, const double* x0, double* x_out, double* tr_f, double* tr_gnorm,
@@ -1134,6 +1293,8 @@ static int orc_lbfgs_cuda(const orc_opts* o, const double* x0, double* x_out, do
     memcpy(x, x0, vb);
     G(C, x0, g0); /* :199 - the host gradient, never updated: every line search gets it */
     memcpy(g, g0, vb);
+    vstate_t vs;
+    vs.f0 = vs.fhost = o->cuda == 2 ? F(C, x0) : 0.0; /* the variants' initial_f = f(x_host), :172-173 */
     int status = ORC_MAX_ITER, ntr = 0, k;
     int64_t skips = 0;
     for (k = 0; k < o->maxit; ++k) {
@@ -1171,13 +1332,34 @@ static int orc_lbfgs_cuda(const orc_opts* o, const double* x0, double* x_out, do
             }
             for (int64_t j = 0; j < n; ++j) d[j] = -r[j]; /* :276 */
         }
-        const double step = pls_run(C, o->ls, x, d, g0, gt); /* :293, the stale gradient */
-        if (step < 1e-10) { /* :295-306 */
-            say(C, "Warning: Line search failed at iteration %d\n", k);
-            status = ORC_LS_FAILED;
-            goto done;
+        double step;
+        if (o->cuda == 2) { /* a variant file's own search, on the current gradient */
+            const double gd = pls_dot(C, g, d);
+            int ok = 1;
+            switch (o->ls) {
+                case ORC_LS_BACKTRACKING: step = vls_backtracking(C, x, d, gd); break;
+                case ORC_LS_INTERPOLATION: step = vls_interpolation(C, &vs, x, d, gd, &ok); break;
+                case ORC_LS_WOLFE: step = vls_wolfe(C, &vs, x, d, gd, gt, &ok); break;
+                default: step = vls_backtracking_wolfe(C, &vs, x, d, gd, gt, &ok); break;
+            }
+            say(C, "alpha: %g\n", step);
+            if (o->ls == ORC_LS_BACKTRACKING) {
+                if (step < 1e-4) /* L-BFGS-Backtracking.cu:345-348 */
+                    say(C, "Warning: Line search resulted in very small step size at iteration %d\n", k);
+            } else if (!ok && step < 1e-10) { /* e.g. L-BFGS-Wolfe.cu:353-366 */
+                say(C, "Warning: Line search failed at iteration %d\n", k);
+                status = ORC_LS_FAILED;
+                goto done;
+            }
+        } else {
+            step = pls_run(C, o->ls, x, d, g0, gt); /* :293, the stale gradient */
+            if (step < 1e-10) { /* :295-306 */
+                say(C, "Warning: Line search failed at iteration %d\n", k);
+                status = ORC_LS_FAILED;
+                goto done;
+            }
+            say(C, "alpha: %g\n", step); /* :308 */
         }
-        say(C, "alpha: %g\n", step); /* :308 */
         for (int64_t j = 0; j < n; ++j) xn[j] = x[j] + step * d[j]; /* updateSolution :310 */
         G(C, xn, gn); /* :323 */
         {

@@ -54,7 +54,7 @@ typedef struct {
     int vf;
     /* 1: the CUDA path - LBFGS_CUDA of parallel-implementation/L-BFGS.cu:105-380 with the line
      * searches of parallel-implementation/line_search.cpp (the product's LBFGS_FLAG_CUDA_COMPAT) */
-    int cuda;
+    int cuda; /* 1: the CUDA path, L-BFGS.cu (orc_lbfgs_cuda); 2: the variant files' loops (their inline searches) */
 } orc_opts;
 
 typedef struct {

@@ -43,7 +43,8 @@ struct OracleRun {
 
 static OracleRun oracle(int obj, int ls, int64_t n, int m, int maxit, const std::vector<double>& x0,
                         double (*hf)(const double*, int64_t, void*) = nullptr,
-                        void (*hg)(const double*, int64_t, double*, void*) = nullptr, void* user = nullptr) {
+                        void (*hg)(const double*, int64_t, double*, void*) = nullptr, void* user = nullptr,
+                        int cuda = 0, double tol = 1e-5) {
     orc_opts o;
     std::memset(&o, 0, sizeof o);
     o.obj = obj;
@@ -52,9 +53,10 @@ static OracleRun oracle(int obj, int ls, int64_t n, int m, int maxit, const std:
     o.n = n;
     o.m = m;
     o.maxit = maxit;
-    o.tol = 1e-5;
+    o.tol = tol;
     o.c1 = 1e-4;
-    o.c2 = 0.9;
+    o.c2 = cuda ? 0.7 : 0.9; /* parallel-implementation/constants.h for the CUDA paths */
+    o.cuda = cuda;
     o.initial_step = 1.0;
     o.backtracking_alpha = 0.5;
     o.backtracking_tol = 1e-8;
@@ -158,6 +160,37 @@ static void device_objectives() {
     setenv("LBFGS_DOUBLE_SMALL", "0", 1);
     setenv("LBFGS_SPEC", "1", 1);
     setenv("LBFGS_DOUBLE_TWOLOOP", "0", 1);
+}
+
+// LBFGS_FLAG_CUDA_COMPAT: L-BFGS.cu's loop with line_search.cpp's searches (cuda 1) and the four
+// variant files' loops with their inline searches (cuda 2), against the oracle's restatements
+static void cuda_paths() {
+    const int64_t sizes[] = {1, 2, 5, 1000, 4097};
+    const int objs[] = {LBFGS_OBJ_ROSENBROCK, LBFGS_OBJ_QUAD_TRIDIAG, LBFGS_OBJ_QUAD_SEPARABLE};
+    lbfgs_constants k;
+    lbfgs_constants_cuda(&k);
+    for (int64_t n : sizes)
+        for (int obj : objs)
+            for (int ls = 0; ls < 4; ++ls)
+                for (int cuda = 1; cuda <= 2; ++cuda) {
+                    const int m = n < 10 ? 2 : 5, maxit = n > 10 ? 60 : 300;
+                    const double tol = 1e-10;
+                    const auto x0 = x0_for(n, 7 + (uint32_t)n);
+                    lbfgs_ctx* c = nullptr;
+                    EXPECT(lbfgs_ctx_create(&c, n, m, 0) == 0, "create n=%lld", (long long)n);
+                    if (!c) continue;
+                    std::vector<double> x(n);
+                    lbfgs_result res;
+                    const unsigned flags = LBFGS_FLAG_QUIET | LBFGS_FLAG_TRACE | LBFGS_FLAG_CUDA_COMPAT |
+                                           (cuda == 2 ? LBFGS_FLAG_CUDA_VARIANT : 0u);
+                    const int st = lbfgs_minimize(c, obj, nullptr, ls, &k, x0.data(), x.data(), maxit, tol, flags, &res);
+                    EXPECT(st >= 0, "cuda %d minimize n=%lld obj %d ls %d: %d %s", cuda, (long long)n, obj, ls, st,
+                           lbfgs_last_error(c));
+                    char tag[96];
+                    std::snprintf(tag, sizeof tag, "cuda=%d n=%lld obj=%d ls=%d", cuda, (long long)n, obj, ls);
+                    if (st >= 0) compare(tag, c, st, x, res, oracle(obj, ls, n, m, maxit, x0, nullptr, nullptr, nullptr, cuda, tol));
+                    lbfgs_ctx_destroy(c);
+                }
 }
 
 // host callbacks: the reference call sequence call for call, and one call per point by default
@@ -332,6 +365,7 @@ static void cxx_dropin() {
 
 int main() {
     device_objectives();
+    cuda_paths();
     host_callbacks();
     dense_objective();
     api_surface();

@@ -371,3 +371,54 @@ def test_cuda_compat_env(tmp_path):
     lines = r.stdout.splitlines()
     assert lines[0] == "Starting" and lines[-1] == "END 1000"
     assert lines[:-1] == t["messages"].splitlines()
+
+
+_STRINGLESS_CALLER = r'''
+#include <functions.h>
+#include <random>
+int main() {
+    std::mt19937 gen(42);
+    std::uniform_real_distribution<> dis(-2, 2);
+    std::vector<double> x0(1000);
+    for (double& v : x0) v = dis(gen);
+    std::vector<double> x = LBFGS_CUDA(rosenbrock, rosenbrock_grad, x0, 40, 5, 1e-5);
+    cout << "END " << x.size() << endl;
+    return 0;
+}
+'''
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("how", ["define", "env"])
+def test_cuda_compat_variant_stringless(tmp_path, how):
+    """LBFGS_CUDA_COMPAT=1 with the string-less LBFGS_CUDA: the variant file's own loop and search
+    (LBFGS_FLAG_CUDA_VARIANT), whether the variant is named by -DLBFGS_CUDA_VARIANT or by
+    LBFGS_CUDA_VARIANT; its stdout equals the C ABI's run of the same solve"""
+    src = tmp_path / "v.cpp"
+    src.write_text(_STRINGLESS_CALLER)
+    exe = tmp_path / "v"
+    cmd = ["g++", "-std=c++17", "-O2", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe), "-L", PKG,
+           "-l:liblbfgs_hip.so", "-Wl,-rpath," + PKG]
+    env = dict(os.environ, LBFGS_CUDA_COMPAT="1")
+    if how == "define":
+        cmd.insert(3, '-DLBFGS_CUDA_VARIANT="wolfe"')
+    else:
+        env["LBFGS_CUDA_VARIANT"] = "wolfe"
+    subprocess.run(cmd, check=True, capture_output=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0, r.stderr
+    import sys
+
+    if PKG not in sys.path:
+        sys.path.insert(0, PKG)
+    import lbfgs_amd as LA
+
+    x0 = O.x0_uniform(1000, 42, -2.0, 2.0)
+    with LA.Context(1000, 5, device=0) as ctx:
+        t = ctx.minimize("rosenbrock", x0, "wolfe", 40, tolerance=1e-5, cuda_compat=True, cuda_variant=True,
+                         consts=LA.constants("cuda"))
+        u = ctx.minimize("rosenbrock", x0, "wolfe", 40, tolerance=1e-5, cuda_compat=True,
+                         consts=LA.constants("cuda"))
+    lines = r.stdout.splitlines()
+    assert lines[-1] == "END 1000" and lines[:-1] == t["messages"].splitlines()
+    assert t["messages"] != u["messages"]  # not L-BFGS.cu's semantics

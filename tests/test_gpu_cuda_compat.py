@@ -68,6 +68,41 @@ def test_cuda_compat_bit_exact_vs_oracle(case):
     assert r["messages"] == o["messages"]
 
 
+# LBFGS_FLAG_CUDA_VARIANT: the four variant files' loops with their inline searches (current
+# gradient, f(x_host) of the last transferred trial point, initial_f in f_prev / f_lo). The n = 5
+# backtracking case prints L-BFGS-Backtracking.cu's "very small step size" warning.
+VARIANT_CASES = [
+    ("rosenbrock", 64, 5, "backtracking", 40, 1e-5, 42),
+    ("rosenbrock", 5, 2, "backtracking", 3000, 1e-14, 2),
+    ("rosenbrock", 1000, 10, "interpolation", 300, 1e-8, 42),
+    ("rosenbrock", 20, 3, "interpolation", 2000, 1e-13, 42),
+    ("rosenbrock", 1000, 10, "wolfe", 300, 1e-8, 42),
+    ("rosenbrock", 20, 3, "wolfe", 2000, 1e-13, 42),
+    ("rosenbrock", 1000, 10, "backtracking_wolfe", 300, 1e-8, 42),
+    ("rosenbrock", 2, 2, "backtracking_wolfe", 3000, 1e-14, 1),
+    ("quad_tridiag", 4000, 7, "wolfe", 100, 1e-8, 42),
+    ("quad_tridiag", 100_003, 5, "backtracking_wolfe", 40, 1e-8, 3),
+    ("quad_sep", 1000, 5, "interpolation", 30, 1e-5, 5),
+]
+
+
+@pytest.mark.parametrize("case", VARIANT_CASES, ids=[f"{c[0]}-n{c[1]}-m{c[2]}-{c[3]}" for c in VARIANT_CASES])
+def test_cuda_variant_bit_exact_vs_oracle(case):
+    obj, n, m, ls, maxit, tol, seed = case
+    x0 = O.x0_uniform(n, seed, -2.0, 2.0)
+    o = O.lbfgs(obj, x0, ls, m, maxit, tol, mode=O.CANON, cuda=2, consts=O.CONSTANTS_H)
+    with L.Context(n, m) as c:
+        r = c.minimize(obj, x0, ls, maxit, tolerance=tol, trace=True, cuda_compat=True, cuda_variant=True,
+                       consts=L.constants("cuda"))
+    assert r["status"] == o["status"] and r["iterations"] == o["iters"]
+    assert np.array_equal(bits(r["tr_f"]), bits(o["f"]))
+    assert np.array_equal(bits(r["tr_gnorm"]), bits(o["gnorm"]))
+    assert np.array_equal(bits(r["tr_alpha"]), bits(o["alpha"]))
+    assert np.array_equal(r["tr_c1"], o["c1"]) and np.array_equal(r["tr_c2"], o["c2"])
+    assert np.array_equal(bits(r["x"]), bits(o["x"]))
+    assert r["messages"] == o["messages"]
+
+
 def test_cuda_compat_refuses_what_the_cuda_path_lacks():
     """the CUDA path has no vector-free form, no host objective here and no sharding"""
     n = 257
@@ -78,6 +113,8 @@ def test_cuda_compat_refuses_what_the_cuda_path_lacks():
         with pytest.raises(L.LbfgsError):
             c.minimize("host", x0, "backtracking", 5, cuda_compat=True,
                        f=lambda x: float(np.sum(x * x)), grad=lambda x: 2 * x)
+        with pytest.raises(L.LbfgsError):  # the variant flag alone
+            c.minimize("rosenbrock", x0, "backtracking", 5, cuda_variant=True)
         # the context is still usable after a refusal
         r = c.minimize("rosenbrock", x0, "backtracking", 5, cuda_compat=True,
                        consts=L.constants("cuda"))

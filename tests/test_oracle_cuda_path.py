@@ -107,3 +107,39 @@ def test_cuda_path_skips_pairs(obj, n, m, ls, maxit, tol, want):
     x0 = O.x0_uniform(n, 42, -2.0, 2.0)
     r = O.lbfgs(obj, x0, ls, m, maxit, tol, mode=O.CANON, cuda=True, consts=O.CONSTANTS_H)
     assert r["skips"] == want
+
+
+@pytest.mark.parametrize("ls", ["backtracking", "interpolation", "wolfe", "backtracking_wolfe"])
+def test_cuda_variant_loop_messages(ls):
+    """the variant files (orc_opts.cuda = 2) print as L-BFGS.cu does; only L-BFGS-Backtracking.cu
+    adds "Warning: Line search resulted in very small step size at iteration k" (:345-348) and
+    never reports a failed search"""
+    x0 = O.x0_uniform(64, 42, -2.0, 2.0)
+    r = O.lbfgs("rosenbrock", x0, ls, 5, 12, 1e-5, mode=O.CANON, cuda=2, consts=O.CONSTANTS_H)
+    lines = r["messages"].strip().splitlines()
+    assert lines[0] == "Starting"
+    body = [ln for ln in lines[1:] if not ln.startswith("Warning: Line search resulted")]
+    for k in range(r["iters"]):
+        a, it, opt = body[3 * k: 3 * k + 3]
+        assert a.startswith("alpha: ") and it == f"Iteration {k}: norm_g = {r['gnorm'][k]:g}"
+        assert opt == f"Optimum value: {r['f'][k]:g}"
+
+
+def test_cuda_variant_backtracking_small_step_warning():
+    """L-BFGS-Backtracking.cu's own search (correct-sign Armijo, 0.5 below 1e-10) takes steps in
+    [1e-10, 1e-4) on this run and warns for each"""
+    x0 = O.x0_uniform(5, 2, -2.0, 2.0)
+    r = O.lbfgs("rosenbrock", x0, "backtracking", 2, 3000, 1e-14, mode=O.CANON, cuda=2, consts=O.CONSTANTS_H)
+    warn = [ln for ln in r["messages"].splitlines() if ln.startswith("Warning: Line search resulted")]
+    small = [a for a in r["alpha"] if a < 1e-4]
+    assert warn and len(warn) == len(small)
+    assert all(1e-10 <= a for a in r["alpha"])
+
+
+def test_cuda_variant_differs_from_cuda_path():
+    """the variants take the current gradient and their own searches: another trajectory than
+    L-BFGS.cu's from the second iteration on"""
+    x0 = O.x0_uniform(64, 42, -2.0, 2.0)
+    a = O.lbfgs("rosenbrock", x0, "wolfe", 5, 10, 1e-5, mode=O.CANON, cuda=1, consts=O.CONSTANTS_H)
+    b = O.lbfgs("rosenbrock", x0, "wolfe", 5, 10, 1e-5, mode=O.CANON, cuda=2, consts=O.CONSTANTS_H)
+    assert not np.array_equal(a["f"], b["f"])
