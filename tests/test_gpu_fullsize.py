@@ -96,6 +96,29 @@ def test_fullsize_parity(name):
         assert r["tr_c2"][1] == int(fx["reference"]["grad_c2"][1])
 
 
+@pytest.mark.parametrize("case", ["cuda_bt", "cuda_btw", "cuda_wolfe", "variant_wolfe"])
+def test_cuda_compat_fullsize(case):
+    """LBFGS_FLAG_CUDA_COMPAT at configs[2]'s size (n = 1e8, m = 10, 12 iterations): L-BFGS.cu with
+    line_search.cpp's backtracking, backtracking-Wolfe and Wolfe searches, and the Wolfe variant
+    file, bit for bit
+    with the oracle's canonical restatement (tests/golden/make_cuda_fullsize.py); parity with the
+    CUDA program itself is unpinned"""
+    fx = json.load(open(os.path.join(FULLSIZE, "cuda_n1e8.json")))
+    c_ = fx["cases"][case]
+    n, m = fx["n"], fx["m"]
+    x0 = L.x0_uniform(n, fx["seed"], -2.0, 2.0)
+    with L.Context(n, m) as c:
+        r = c.minimize(fx["objective"], x0, c_["method"], fx["iterations"], tolerance=fx["tol"], trace=True,
+                       cuda_compat=True, cuda_variant=c_["cuda"] == 2, consts=L.constants("cuda"))
+    del x0
+    assert r["status"] == c_["status"] and r["iterations"] == c_["iterations"]
+    assert np.array_equal(bits(r["tr_f"]), bits(f64(c_["f"])))
+    assert np.array_equal(bits(r["tr_gnorm"]), bits(f64(c_["gnorm"])))
+    assert np.array_equal(bits(r["tr_alpha"]), bits(f64(c_["alpha"])))
+    assert np.array_equal(r["tr_c1"], u64(c_["c1"])) and np.array_equal(r["tr_c2"], u64(c_["c2"]))
+    assert r["messages"] == c_["messages"]
+
+
 N9 = 10 ** 9
 
 

@@ -143,3 +143,22 @@ def test_cuda_variant_differs_from_cuda_path():
     a = O.lbfgs("rosenbrock", x0, "wolfe", 5, 10, 1e-5, mode=O.CANON, cuda=1, consts=O.CONSTANTS_H)
     b = O.lbfgs("rosenbrock", x0, "wolfe", 5, 10, 1e-5, mode=O.CANON, cuda=2, consts=O.CONSTANTS_H)
     assert not np.array_equal(a["f"], b["f"])
+
+
+def test_cuda_fullsize_fixture_is_consistent():
+    """tests/golden/fullsize/cuda_n1e8.json (the GPU's full-size CUDA-mode target): each case's
+    printed lines are its own trace, and L-BFGS.cu's loop differs from the variant files'"""
+    fx = json.load(open(os.path.join(HERE, "golden", "fullsize", "cuda_n1e8.json")))
+    assert (fx["n"], fx["m"], fx["iterations"]) == (10 ** 8, 10, 12)
+    for name, c in fx["cases"].items():
+        f, gn, al = f64(c["f"]), f64(c["gnorm"]), f64(c["alpha"])
+        assert len(f) == len(gn) == len(al) == len(c["c1"]) == c["iterations"] == 12, name
+        lines = c["messages"].strip().splitlines()
+        assert lines[0] == "Starting"
+        body = [ln for ln in lines[1:] if not ln.startswith("Warning: Line search resulted")]
+        for k in range(12):
+            assert body[3 * k] == f"alpha: {al[k]:g}", (name, k)
+            assert body[3 * k + 1] == f"Iteration {k}: norm_g = {gn[k]:g}", (name, k)
+            assert body[3 * k + 2] == f"Optimum value: {f[k]:g}", (name, k)
+    fs = [tuple(c["f"]) for c in fx["cases"].values()]
+    assert len(set(fs)) == len(fs) == 4  # four distinct trajectories
