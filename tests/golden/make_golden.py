@@ -62,6 +62,19 @@ STRESS = {
     "stress_qtri_tiny_bt": ("quad_tridiag", 10, 3, "backtracking", 30, 0.0, 42, -1e-155, 1e-155, 0),
     "stress_qtri_tiny_wolfe": ("quad_tridiag", 10, 3, "wolfe", 30, 0.0, 42, -1e-155, 1e-155, 0),
     "stress_qtri_tiny_btw": ("quad_tridiag", 10, 3, "backtracking_wolfe", 30, 0.0, 42, -1e-155, 1e-155, 0),
+    # edges of the loop itself: no iteration at all (maxit = 0), x0 at the minimiser (g = 0 exactly:
+    # converged before the first step), a tolerance every |g| meets, a one-pair history, a
+    # history longer than the run, n = 1 of the tridiagonal quadratic (both stencil edges at once),
+    # tolerance 0 (runs to the cap or a failed search)
+    "stress_edge_maxit0_bt": ("rosenbrock", 100, 5, "backtracking", 0, 1e-5, 42, -2.0, 2.0, 0),
+    "stress_edge_optimum_wolfe": ("rosenbrock", 50, 5, "wolfe", 10, 1e-5, 42, 1.0, 1.0, 0),
+    "stress_edge_qsep_optimum_interp": ("quad_sep", 10, 3, "interpolation", 10, 1e-5, 42, 1.0, 1.0, 0),
+    "stress_edge_hugetol_btw": ("rosenbrock", 200, 3, "backtracking_wolfe", 10, 1e9, 42, -2.0, 2.0, 0),
+    "stress_edge_m1_bt": ("rosenbrock", 1000, 1, "backtracking", 60, 1e-5, 42, -2.0, 2.0, 0),
+    "stress_edge_m1_interp": ("rosenbrock", 1000, 1, "interpolation", 60, 1e-5, 42, -2.0, 2.0, 0),
+    "stress_edge_qtri_n1_wolfe": ("quad_tridiag", 1, 3, "wolfe", 30, 1e-8, 42, -2.0, 2.0, 0),
+    "stress_edge_m20_n3_bt": ("rosenbrock", 3, 20, "backtracking", 500, 1e-10, 42, -2.0, 2.0, 0),
+    "stress_edge_tol0_n2_bt": ("rosenbrock", 2, 2, "backtracking", 300, 0.0, 5, -2.0, 2.0, 0),
 }
 CASES.update(STRESS)
 
