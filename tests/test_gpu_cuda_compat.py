@@ -45,6 +45,10 @@ CASES = [
     ("quad_tridiag", 100_003, 5, "backtracking", 40, 1e-8, -2.0, 2.0, 3),
     ("quad_sep", 1000, 5, "backtracking", 30, 1e-5, 1 - 1e-7, 1 + 1e-7, 42),
     ("quad_sep", 1000, 5, "interpolation", 30, 1e-5, -2.0, 2.0, 5),
+    # edges: no iteration, x0 at the minimiser (g = 0: the step is taken, then |g| <= tol), n = 1
+    ("rosenbrock", 100, 5, "backtracking", 0, 1e-5, -2.0, 2.0, 42),
+    ("rosenbrock", 50, 5, "wolfe", 10, 1e-5, 1.0, 1.0, 42),
+    ("quad_tridiag", 1, 3, "backtracking_wolfe", 30, 1e-8, -2.0, 2.0, 42),
 ]
 _ids = [f"{c[0]}-n{c[1]}-m{c[2]}-{c[3]}-it{c[4]}" for c in CASES]
 
@@ -83,6 +87,8 @@ VARIANT_CASES = [
     ("quad_tridiag", 4000, 7, "wolfe", 100, 1e-8, 42),
     ("quad_tridiag", 100_003, 5, "backtracking_wolfe", 40, 1e-8, 3),
     ("quad_sep", 1000, 5, "interpolation", 30, 1e-5, 5),
+    ("rosenbrock", 100, 5, "interpolation", 0, 1e-5, 42),
+    ("quad_tridiag", 1, 3, "wolfe", 30, 1e-8, 42),
 ]
 
 
