@@ -422,3 +422,32 @@ def test_cuda_compat_variant_stringless(tmp_path, how):
     lines = r.stdout.splitlines()
     assert lines[-1] == "END 1000" and lines[:-1] == t["messages"].splitlines()
     assert t["messages"] != u["messages"]  # not L-BFGS.cu's semantics
+
+
+_EMPTY_CALLER = r'''
+#include <cstdio>
+#include <stdexcept>
+#include <benchmark.h>
+#include <lbfgs.h>
+int main() {
+    std::vector<double> x0;
+    try { LBFGS(rosenbrock, rosenbrock_grad, x0, "backtracking"); }
+    catch (const std::invalid_argument& e) { std::printf("INVALID %s\n", e.what()); }
+    try { LBFGS_CUDA(rosenbrock, rosenbrock_grad, x0, "wolfe", 10, 5, 1e-5); }
+    catch (const std::invalid_argument& e) { std::printf("INVALID %s\n", e.what()); }
+    return 0;
+}
+'''
+
+
+def test_empty_x0_throws(tmp_path):
+    """An empty x0 throws std::invalid_argument before any device work (runs on CPU); the
+    reference reads out of bounds there (benchmark.cpp:61, size_t wrap; INTEGRATION.md §1)"""
+    src = tmp_path / "e.cpp"
+    src.write_text(_EMPTY_CALLER)
+    exe = tmp_path / "e"
+    subprocess.run(["g++", "-std=c++17", "-O2", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe), "-L", PKG,
+                    "-l:liblbfgs_hip.so", "-Wl,-rpath," + PKG], check=True, capture_output=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.splitlines() == ["INVALID x0 must not be empty"] * 2
