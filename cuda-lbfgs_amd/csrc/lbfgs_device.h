@@ -222,6 +222,13 @@ typedef struct {
     unsigned long long chain_epoch;
 } lbk_spec;
 int lbk_small_spec_ok(const lbk_ctx* c, int h);
+/* small n, single rank: the Wolfe search (lbfgs_driver.c ls_wolfe) continued on the device from
+ * search iteration iter0 in one cooperative launch (k_coop_wolfe); st = {alpha, alpha_lo, alpha_hi,
+ * f_lo, dphi_lo, f_x, g.d, c1, c2, wolfe_interp_min, last step, its f, its g.d, have_last, first
+ * trial step, its f, its g.d, have_first}; d materialised. out = {step, trial passes, last evaluated
+ * step, its f, its g.d}. */
+int lbk_wolfe_dev_ok(const lbk_ctx* c, int obj);
+int lbk_wolfe_dev(lbk_ctx* c, int obj, const double* x, const double* d, const double* st, int iter0, double* out);
 /* *epoch: the launch's id for lbk_small_fetch (0: not a cooperative host-mirrored launch) */
 int lbk_small_iter(lbk_ctx* c, int obj, int h, const double* g, double* q, double* r, const double* const* S,
                    const double* const* Y, const double* rho, double gamma, int p0_ref, double a0, const double* x,

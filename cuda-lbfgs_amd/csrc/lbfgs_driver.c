@@ -867,6 +867,43 @@ static int ls_interpolation(lbfgs_ctx* c, double gd, double* out) {
     return 0;
 }
 
+/* Small n (single rank, a cooperative size, device objective): once the Wolfe search needs a
+ * trial pass, the rest of the search runs on the device in one launch (lbk_wolfe_dev: the same
+ * loop, the same expressions, the same passes) instead of a launch and a host
+ * round trip per trial. The step and every counter come back as the host loop would leave them. */
+static int wolfe_on_device(const lbfgs_ctx* c, double alpha) {
+    if (ext_obj(c) || c->unfused || !c->batch || c->vf || !lbk_wolfe_dev_ok(c->dev, c->obj)) return 0;
+    if (c->spec_valid && alpha == c->a0) return 0; /* the commit's first trial: no pass */
+    if (c->tc_n >= 1 && c->tc_dphi_ok && alpha == c->tc_a[0]) return 0; /* the last pass */
+    return 1;
+}
+
+static int wolfe_device(lbfgs_ctx* c, int iter, double alpha, double alpha_lo, double alpha_hi, double f_lo,
+                        double dphi_lo, double f_x, double gd, double* out) {
+    const lbfgs_constants* K = &c->K;
+    int rc = materialize_d(c);
+    if (rc) return rc;
+    const int last = c->tc_n >= 1 && c->tc_dphi_ok;
+    const double st[18] = {alpha, alpha_lo, alpha_hi, f_lo, dphi_lo, f_x, gd, K->c1, K->c2, K->wolfe_interp_min,
+                           last ? c->tc_a[0] : 0.0, last ? c->tc_f[0] : 0.0, last ? c->tc_dphi : 0.0, last ? 1.0 : 0.0,
+                           c->a0, c->spec_f, c->spec_dphi, c->spec_valid ? 1.0 : 0.0};
+    double o[5];
+    DEVNC(lbk_wolfe_dev(c->dev, c->obj, c->x, c->d, st, iter, o));
+    const int passes = (int)o[1];
+    c->trials_fg += passes;
+    c->trial_passes += passes;
+    c->passes += passes;
+    if (passes > 0) { /* the host's cache of the last trial pass, as the host loop leaves it */
+        c->tc_n = 1;
+        c->tc_a[0] = o[2];
+        c->tc_f[0] = o[3];
+        c->tc_dphi = o[4];
+        c->tc_dphi_ok = 1;
+    }
+    *out = o[0];
+    return 0;
+}
+
 /* line_search.cpp:125-189 */
 static int ls_wolfe(lbfgs_ctx* c, double gd, double* out) {
     const lbfgs_constants* K = &c->K;
@@ -876,6 +913,7 @@ static int ls_wolfe(lbfgs_ctx* c, double gd, double* out) {
     double alpha = K->initial_step;
     double alpha_lo = 0.0, alpha_hi = INFINITY, f_lo = f_x, dphi_lo = gd;
     for (int iter = 0; iter < 20; ++iter) {
+        if (wolfe_on_device(c, alpha)) return wolfe_device(c, iter, alpha, alpha_lo, alpha_hi, f_lo, dphi_lo, f_x, gd, out);
         double f_new, dphi_new;
         /* f first; the gradient only if the sufficient-decrease tests pass (:144-153) */
         int rc = trial(c, alpha, 0, &f_new, NULL);

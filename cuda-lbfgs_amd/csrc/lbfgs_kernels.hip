@@ -128,6 +128,10 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
     // 342 (7e5) deferred leads 5.07k to 4.81k (profiles/r02/small_n/coop_limit_ab.txt)
     c->coop_max = 256;
     if (const char* e = getenv("LBFGS_COOP")) c->coop_max = std::min(atoi(e), LBK_COOP_SEGMAX);  // max segments
+    // small n, Wolfe search: the trials after the commit's first one in one cooperative launch
+    // (k_coop_wolfe) instead of a launch and a host round trip each; LBFGS_DEV_WOLFE=0: host loop
+    c->dev_wolfe = 1;
+    if (const char* e = getenv("LBFGS_DEV_WOLFE")) c->dev_wolfe = atoi(e) != 0;
     c->pend_slot = -1;
     c->xf_slot = -1;
     // folded exchanges over the mailboxes: 1 (default) when every peer has a GPU of
@@ -222,6 +226,14 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
         CK(hipMalloc(&c->coop_ll, llb));
         CK(hipMemset(c->coop_ll, 0, llb));  // tag 0: no pass (sequence numbers start at 1)
     }
+    {
+        const size_t llb = sizeof(unsigned long long) * 2 * LBK_LL_COMPS * LBK_LL_SEGS * 2;
+        CK(hipMalloc(&c->wolfe_ll, llb));
+        CK(hipMemset(c->wolfe_ll, 0, llb));
+    }
+    CK(hipHostMalloc((void**)&c->wolfe_out_h, sizeof(double) * 8, hipHostMallocMapped | hipHostMallocCoherent));
+    memset(c->wolfe_out_h, 0, sizeof(double) * 8);
+    CK(hipHostGetDevicePointer((void**)&c->wolfe_out_d, c->wolfe_out_h, 0));
     {
         const size_t llb = sizeof(unsigned long long) * 2 * LBK_KMAX * LBK_SEGS;  // regular slots only
         CK(hipMalloc(&c->coll_ll, llb));
@@ -375,6 +387,8 @@ void lbk_destroy(lbk_ctx* c) {
     if (c->d_ckslot) (void)hipFree(c->d_ckslot);
     (void)hipFree(c->partials);
     (void)hipFree(c->coop_ll);
+    (void)hipFree(c->wolfe_ll);
+    if (c->wolfe_out_h) (void)hipHostFree(c->wolfe_out_h);
     (void)hipFree(c->coll_ll);
     xfer_pool_free(c);
     (void)hipFree(c->persist_cnt);
@@ -974,6 +988,65 @@ int lbk_small_iter(lbk_ctx* c, int obj, int h, const double* g, double* q, doubl
 
 int lbk_small_spec_ok(const lbk_ctx* c, int h) {
     return lbk_small_ok(c, h) && c->direct && c->coop_max > 0 && c->geo.nseg <= c->coop_max;
+}
+
+int lbk_wolfe_dev_ok(const lbk_ctx* c, int obj) {
+    return c->dev_wolfe && c->geo.world == 1 && !c->comm && c->coop_max > 0 && c->geo.nseg <= c->coop_max &&
+           (obj == LBK_OBJ_ROSENBROCK || obj == LBK_OBJ_QUAD_TRIDIAG || obj == LBK_OBJ_QUAD_SEPARABLE);
+}
+
+int lbk_wolfe_dev(lbk_ctx* c, int obj, const double* x, const double* d, const double* st, int iter0, double* out) {
+    if (!lbk_wolfe_dev_ok(c, obj)) {
+        snprintf(c->err, sizeof c->err, "lbk_wolfe_dev: not a single-rank cooperative size");
+        return -1;
+    }
+    SmallArgs a;
+    memset(&a, 0, sizeof a);
+    a.ll = c->wolfe_ll;
+    a.seq_base = (unsigned)c->wolfe_seq;
+    a.err = c->coop_err_d;
+    a.timeout = (unsigned long long)(2.0 * c->wall_khz * 1e3);  // 2 s per barrier
+    c->wolfe_seq += 20;                                          // at most 20 trial passes
+    WolfeDev w;
+    w.alpha = st[0];
+    w.alpha_lo = st[1];
+    w.alpha_hi = st[2];
+    w.f_lo = st[3];
+    w.dphi_lo = st[4];
+    w.f_x = st[5];
+    w.gd = st[6];
+    w.c1 = st[7];
+    w.c2 = st[8];
+    w.amin = st[9];
+    w.last_a = st[10];
+    w.last_f = st[11];
+    w.last_dphi = st[12];
+    w.have_last = st[13] != 0.0;
+    w.spec_a = st[14];
+    w.spec_f = st[15];
+    w.spec_dphi = st[16];
+    w.have_spec = st[17] != 0.0;
+    w.iter0 = iter0;
+    Geo geo = kgeo(c);
+    geo.rev = 0;
+    const int nb = (int)c->geo.nseg;
+    double* o = c->wolfe_out_d;
+    const int rc = launch(c, LBK_K_TRIAL_FG, 0.0, -1, [&] {
+        switch (obj) {
+            case LBK_OBJ_ROSENBROCK: hipLaunchKernelGGL(k_coop_wolfe<LBK_OBJ_ROSENBROCK>, dim3(nb), dim3(LB_BLOCK), 0, c->stream, a, geo, w, x, d, o); break;
+            case LBK_OBJ_QUAD_TRIDIAG: hipLaunchKernelGGL(k_coop_wolfe<LBK_OBJ_QUAD_TRIDIAG>, dim3(nb), dim3(LB_BLOCK), 0, c->stream, a, geo, w, x, d, o); break;
+            default: hipLaunchKernelGGL(k_coop_wolfe<LBK_OBJ_QUAD_SEPARABLE>, dim3(nb), dim3(LB_BLOCK), 0, c->stream, a, geo, w, x, d, o); break;
+        }
+    });
+    if (rc) return rc;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (*(volatile unsigned*)c->coop_err_h) {
+        snprintf(c->err, sizeof c->err, "device Wolfe search: grid barrier timed out");
+        return -2;
+    }
+    for (int k = 0; k < 5; ++k) out[k] = ((volatile double*)c->wolfe_out_h)[k];
+    c->bytes_total += out[1] * 2.0 * 8.0 * (double)c->geo.n_loc;  // x and d per trial pass
+    return 0;
 }
 
 // spin on the pinned completion word; every 64k polls ask the stream whether it still runs (a

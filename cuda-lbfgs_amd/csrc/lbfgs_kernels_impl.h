@@ -2435,6 +2435,102 @@ __global__ __launch_bounds__(LB_BLOCK) void k_coop_iter(SmallArgs a, Geo geo) {
 #undef SL
 
 // ---------------------------------------------------------------------------------------
+// Device-resident Wolfe search for small n (lbfgs_driver.c ls_wolfe,
+// line_search.cpp:125-189): once the host's search needs a trial pass, the rest of the search runs
+// in ONE cooperative launch - one workgroup per canonical segment, all resident, each trial a
+// grid-wide pass of f(x + a d) and g(x + a d) . d (OpTrials, the k_trials arithmetic) whose fixed-
+// order totals every workgroup forms (coop_pass), and the search's decisions restated on them in
+// every workgroup with the host's expressions (-ffp-contract=off on both sides; IEEE division and
+// square root), so all workgroups take the same branches and the step is the host's bit for bit.
+// A step equal to the last evaluated one, or to the first trial the commit took, is not evaluated
+// again (the host's caches). Its flagged partials have their own buffer and sequence numbers,
+// apart from the cooperative iteration's, whose counter a dropped speculative launch rolls back.
+// out: [step, passes, last evaluated step, its f, its g.d].
+// ---------------------------------------------------------------------------------------
+struct WolfeDev {
+    double alpha, alpha_lo, alpha_hi, f_lo, dphi_lo, f_x, gd, c1, c2, amin;
+    double last_a, last_f, last_dphi;  // the last trial pass of this search (have_last)
+    double spec_a, spec_f, spec_dphi;  // the first trial, taken by the commit (have_spec)
+    int iter0, have_last, have_spec;
+};
+
+__device__ __forceinline__ double wolfe_cubic(double a0, double a1, double p0, double dp0, double p1, double dp1) {
+    const double d1 = dp0 + dp1 - 3 * (p1 - p0) / (a1 - a0);  // line_search.cpp:8-12
+    const double d2 = copysign(sqrt(d1 * d1 - dp0 * dp1), a1 - a0);
+    return a0 + (a1 - a0) * (dp0 + d2 - d1) / (dp0 - dp1 + 2 * d2);
+}
+
+template <int OBJ>
+__global__ __launch_bounds__(LB_BLOCK) void k_coop_wolfe(SmallArgs a, Geo geo, WolfeDev w, const double* x,
+                                                         const double* d, double* out) {
+    __shared__ double lds[4][8];
+    __shared__ double tl[8];
+    DirArgs da = {d, nullptr, nullptr, 0.0, nullptr, nullptr, 0.0, nullptr, geo.g_lo, geo.g_hi};
+    double alpha = w.alpha, lo = w.alpha_lo, hi = w.alpha_hi, f_lo = w.f_lo, dphi_lo = w.dphi_lo;
+    double la = w.last_a, lf = w.last_f, ld = w.last_dphi;
+    int have = w.have_last, pass = 0, iter = w.iter0;
+    double res;
+    for (;;) {
+        if (iter >= 20) {
+            res = alpha;
+            break;
+        }
+        double f_new, dphi_new;
+        if (w.have_spec && alpha == w.spec_a) {
+            f_new = w.spec_f;
+            dphi_new = w.spec_dphi;
+        } else if (have && alpha == la) {
+            f_new = lf;
+            dphi_new = ld;
+        } else {
+            OpTrials<OBJ, LBK_D_BUF, 1, true, false> op{x, da, {alpha}, geo.n, geo.n_loc};
+            double t[2];
+            coop_pass<2>(op, geo, a, pass++, nullptr, nullptr, nullptr, t, lds, tl);
+            f_new = t[0];
+            dphi_new = t[1];
+            la = alpha;
+            lf = f_new;
+            ld = dphi_new;
+            have = 1;
+        }
+        if (f_new > w.f_x + w.c1 * alpha * w.gd || (f_new >= f_lo && iter > 0)) {
+            hi = alpha;
+            alpha = wolfe_cubic(lo, hi, f_lo, dphi_lo, f_new, (f_new - w.f_x - w.gd * alpha) / (alpha * alpha));
+            ++iter;
+            continue;
+        }
+        if (fabs(dphi_new) <= -w.c2 * w.gd) {
+            res = alpha;
+            break;
+        }
+        if (dphi_new >= 0) {
+            hi = alpha;
+            alpha = wolfe_cubic(lo, hi, f_lo, dphi_lo, f_new, dphi_new);
+        } else {
+            lo = alpha;
+            f_lo = f_new;
+            dphi_lo = dphi_new;
+            if (hi == INFINITY)
+                alpha *= 2;
+            else
+                alpha = wolfe_cubic(lo, hi, f_lo, dphi_lo, f_new, dphi_new);
+        }
+        if (alpha < w.amin) {
+            res = w.amin;
+            break;
+        }
+        ++iter;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        out[0] = res;
+        out[1] = (double)pass;
+        out[2] = la;
+        out[3] = lf;
+        out[4] = ld;
+    }
+}
+
+// ---------------------------------------------------------------------------------------
 // Persistent forms for large n (LBFGS_PERSIST=1: the whole iteration, k_persist_iter;
 // LBFGS_PERSIST=2: the two-loop, k_persist_twoloop; VERDICT r02 item 8, the north star's
 // "persistent-block fused two-loop" at configs[2]'s size): one resident grid of G workgroups
@@ -2858,6 +2954,12 @@ struct lbk_ctx {
     unsigned long long coop_ll_bytes;
     unsigned long long* coop_ll;   // flagged partials (SmallArgs::ll)
     unsigned long long coop_base;  // passes tagged so far (the next launch's sequence base)
+    // device-resident Wolfe search (k_coop_wolfe, LBFGS_DEV_WOLFE): flagged partials and sequence
+    // numbers of its own (never rolled back), results in mapped host memory
+    int dev_wolfe;
+    unsigned long long* wolfe_ll;
+    unsigned long long wolfe_seq;
+    double *wolfe_out_h, *wolfe_out_d;
     unsigned* coop_err_h;          // pinned: barrier timeout
     unsigned* coop_err_d;
     double wall_khz;

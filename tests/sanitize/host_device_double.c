@@ -30,6 +30,7 @@ struct lbk_ctx {
      * product uses it for nseg <= its cooperative limit): launches run at once, in stream order */
     int small_on;
     int twoloop_on;
+    int wolfe_on; /* the device-resident Wolfe search (LBFGS_DEV_WOLFE, with the small-n form) */
     unsigned long long epoch, vd[4];
     int rec_went[4];
     double rec_rho[4], rec_gamma[4];
@@ -79,6 +80,8 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
     c->small_on = e && atoi(e) != 0;
     e = getenv("LBFGS_DOUBLE_TWOLOOP");  /* the driver's persistent two-loop branch (LBFGS_PERSIST=2) */
     c->twoloop_on = e && atoi(e) != 0;
+    e = getenv("LBFGS_DEV_WOLFE");
+    c->wolfe_on = !e || atoi(e) != 0;
     *out = c;
     return 0;
 }
@@ -474,6 +477,79 @@ int lbk_vf_ghost_init(lbk_ctx* c, double* x, double* g, int wslot) {
     return 0;
 }
 int lbk_small_ok(const lbk_ctx* c, int h) { return c->small_on && h >= 1 && h <= 16; }
+
+/* k_coop_wolfe's loop on this double's trial evaluation (lbk_trials, D_BUF, f and g.d) */
+int lbk_wolfe_dev_ok(const lbk_ctx* c, int obj) {
+    return c->small_on && c->wolfe_on && obj >= 0 && obj <= LBK_OBJ_QUAD_SEPARABLE;
+}
+static double wolfe_cubic(double a0, double a1, double p0, double dp0, double p1, double dp1) {
+    const double d1 = dp0 + dp1 - 3 * (p1 - p0) / (a1 - a0);
+    const double d2 = copysign(sqrt(d1 * d1 - dp0 * dp1), a1 - a0);
+    return a0 + (a1 - a0) * (dp0 + d2 - d1) / (dp0 - dp1 + 2 * d2);
+}
+int lbk_wolfe_dev(lbk_ctx* c, int obj, const double* x, const double* d, const double* st, int iter0, double* out) {
+    if (!lbk_wolfe_dev_ok(c, obj)) return -1;
+    const int slot = LBK_NSLOTS - 1; /* a slot the driver never names */
+    double alpha = st[0], lo = st[1], hi = st[2], f_lo = st[3], dphi_lo = st[4];
+    const double f_x = st[5], gd = st[6], c1 = st[7], c2 = st[8], amin = st[9];
+    double la = st[10], lf = st[11], ld = st[12], res;
+    int have = st[13] != 0.0, passes = 0, iter = iter0;
+    for (;;) {
+        if (iter >= 20) {
+            res = alpha;
+            break;
+        }
+        double f_new, dphi_new;
+        if (st[17] != 0.0 && alpha == st[14]) {
+            f_new = st[15];
+            dphi_new = st[16];
+        } else if (have && alpha == la) {
+            f_new = lf;
+            dphi_new = ld;
+        } else {
+            double t[2];
+            if (lbk_trials(c, obj, LBK_D_BUF, x, d, NULL, NULL, 0.0, -1, -1, &alpha, 1, 1, slot) != 0) return -1;
+            if (lbk_fetch(c, slot, 2, t) != 0) return -1;
+            passes++;
+            f_new = t[0];
+            dphi_new = t[1];
+            la = alpha;
+            lf = f_new;
+            ld = dphi_new;
+            have = 1;
+        }
+        if (f_new > f_x + c1 * alpha * gd || (f_new >= f_lo && iter > 0)) {
+            hi = alpha;
+            alpha = wolfe_cubic(lo, hi, f_lo, dphi_lo, f_new, (f_new - f_x - gd * alpha) / (alpha * alpha));
+            ++iter;
+            continue;
+        }
+        if (fabs(dphi_new) <= -c2 * gd) {
+            res = alpha;
+            break;
+        }
+        if (dphi_new >= 0) {
+            hi = alpha;
+            alpha = wolfe_cubic(lo, hi, f_lo, dphi_lo, f_new, dphi_new);
+        } else {
+            lo = alpha;
+            f_lo = f_new;
+            dphi_lo = dphi_new;
+            alpha = hi == INFINITY ? alpha * 2 : wolfe_cubic(lo, hi, f_lo, dphi_lo, f_new, dphi_new);
+        }
+        if (alpha < amin) {
+            res = amin;
+            break;
+        }
+        ++iter;
+    }
+    out[0] = res;
+    out[1] = passes;
+    out[2] = la;
+    out[3] = lf;
+    out[4] = ld;
+    return 0;
+}
 int lbk_small_spec_ok(const lbk_ctx* c, int h) { return lbk_small_ok(c, h); }
 
 /* the prologue of a speculative launch (k_coop_iter's spec_ok), on this double's slots */

@@ -25,7 +25,7 @@ pytestmark = pytest.mark.gpu
 KNOBS = ["LBFGS_TICKET", "LBFGS_DEFER", "LBFGS_REV", "LBFGS_NT", "LBFGS_DIRECT", "LBFGS_COOP",
          "LBFGS_PERSIST", "LBFGS_PINGPONG", "LBFGS_SPEC", "LBFGS_BATCH", "LBFGS_SMALL_SEGS",
          "LBFGS_PERSIST_WG", "LBFGS_PERSIST_OWN", "LBFGS_PERSIST_ALT", "LBFGS_PERSIST_LDS", "LBFGS_COLLECT",
-         "LBFGS_COLLECT_TIMEOUT"]
+         "LBFGS_COLLECT_TIMEOUT", "LBFGS_DEV_WOLFE"]
 
 VARIANTS = {
     "ticket1": {"LBFGS_TICKET": "1"},
@@ -56,10 +56,13 @@ VARIANTS = {
     "defer_all_rev0_pingpong1": {"LBFGS_DEFER": "8192", "LBFGS_TICKET": "0", "LBFGS_REV": "0",
                                  "LBFGS_PINGPONG": "1"},
     "coop0_spec0_batch0": {"LBFGS_COOP": "0", "LBFGS_SPEC": "0", "LBFGS_BATCH": "0"},
+    "devwolfe0": {"LBFGS_DEV_WOLFE": "0"},
+    "devwolfe0_spec0": {"LBFGS_DEV_WOLFE": "0", "LBFGS_SPEC": "0"},
 }
 
 CASES = [  # n, m, objective, line search, iterations
     (100_003, 5, "rosenbrock", "backtracking", 25),       # 196 segments: cooperative iteration
+    (60_001, 5, "rosenbrock", "wolfe", 40),               # 118 segments: the device-resident Wolfe search
     (700_001, 7, "quad_tridiag", "wolfe", 12),             # 342 segments of 2048: deferred stage 2
     (3_000_017, 5, "rosenbrock", "interpolation", 14),     # 5860 segments of 512: reduce kernel
     (5_000_000, 10, "rosenbrock", "backtracking", 14),     # 7813 segments of 640, h = m reached
