@@ -2,6 +2,8 @@
 """Full-size parity fixtures (test infrastructure) for the two single-GPU BASELINE configs the
 headline and the time-to-solution are quoted on:
 
+  config1_n1e7  configs[1]: Rosenbrock n = 1e7, m = 10, backtracking, 12 iterations (the GPU test
+                runs it through the unfused per-vector kernels, the CUDA path's launch shape)
   config2_n1e8  configs[2]: Rosenbrock n = 1e8, m = 10, backtracking, 12 iterations
                 (the bench's history fill plus two steps; bench.py's CPU baseline runs the same)
   config3_n1e8  configs[3]: tridiagonal quadratic (benchmark.cpp:16-56) n = 1e8, m = 20, Wolfe,
@@ -33,7 +35,7 @@ iteration at n = 1e8 and the m = 20 runs ~40 GB of host memory, so the cases run
                 whole-run restatement at smaller n before it runs at 1e9; and f(x0), |g(x0)| of
                 the reference itself (maxit = 0: it evaluates f and grad at x0 and stops).
 
-usage: python tests/golden/make_fullsize.py [config2_n1e8] [config3_n1e8] [config4_n1e9]
+usage: python tests/golden/make_fullsize.py [config1_n1e7] [config2_n1e8] [config3_n1e8] [config4_n1e9]
 """
 import json
 import os
@@ -54,6 +56,7 @@ OUT = os.path.join(HERE, "fullsize")
 
 # name: (objective, n, m, method, maxit, tol, seed, lo, hi, baseline config)
 CASES = {
+    "config1_n1e7": ("rosenbrock", 10 ** 7, 10, "backtracking", 12, 1e-5, 42, -2.0, 2.0, "configs[1]"),
     "config2_n1e8": ("rosenbrock", 10 ** 8, 10, "backtracking", 12, 1e-5, 42, -2.0, 2.0, "configs[2]"),
     "config3_n1e8": ("quad_tridiag", 10 ** 8, 20, "wolfe", 1000, 1e-5, 42, -2.0, 2.0, "configs[3]"),
 }
