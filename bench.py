@@ -66,9 +66,10 @@ def parse(argv=None):
     p.add_argument("--no-config4", action="store_true",
                    help="8 ranks: skip the n=1e9 measurement (BASELINE configs[4]) after the headline")
     p.add_argument("--exchange", choices=["auto", "xgmi", "rccl"], default="auto",
-                   help="sharded runs: reductions through the xGMI peer mailboxes (falls back to RCCL "
-                        "when any rank's self-test fails) or RCCL all-gathers; auto: the mailboxes "
-                        "unless RCCL measures >10%% faster per exchange on this node")
+                   help="sharded runs: reductions through the xGMI peer mailboxes (measured again over "
+                        "RCCL when any rank's mailbox self-test fails) or RCCL all-gathers; auto: the "
+                        "mailboxes, with an RCCL communicator created and timed only after the "
+                        "measurement (bounded by LBFGS_RCCL_TIMEOUT, reported as rccl_leg)")
     p.add_argument("--launch-timeout", type=float, default=float(os.environ.get("BENCH_LAUNCH_TIMEOUT", 3000)),
                    help="--gpus N > 1 without a launcher: seconds before the self-launched ranks are stopped")
     p.add_argument("--no-box-probe", action="store_true", help="skip the in-process HBM stream probe")
@@ -382,33 +383,13 @@ def _measure(a, D, ctx, x0, rank, world, uid, unfused, vector_free, box_probe):
             raise failed[0] if failed else L.LbfgsError(f"{stage} failed on another rank")
 
     if world > 1 and a.exchange in ("xgmi", "auto"):
+        # the measurement's exchange path: the peer mailboxes alone (every wait bounded, 60 s); no
+        # RCCL communicator exists yet (rccl_leg below creates one after the measurement)
         ok, msg = ctx.connect_peers(D.allgather_bytes, D.all_ok)  # collective, its own vote
         if msg:
             print(f"rank {rank}: {msg}", file=sys.stderr, flush=True)
         if not ok and uid is None:
             raise L.LbfgsError("xGMI peer exchange unavailable and no RCCL communicator")  # on every rank
-        if ok and a.exchange == "auto" and uid is not None:
-            # collective calls in the same order on every rank; the slowest rank decides
-            # vote after each collective timing, so that no rank enters the RCCL all-gather
-            # unless every rank got through the mailbox timing (RCCL has no timeout)
-            lx = lr = None
-            try:
-                lx = ctx.exchange_latency("xgmi", 8, 100)
-            except L.LbfgsError as e:
-                print(f"rank {rank}: xgmi exchange timing failed: {e}", file=sys.stderr, flush=True)
-            if D.all_ok(lx is not None):
-                try:
-                    lr = ctx.exchange_latency("rccl", 8, 100)
-                except L.LbfgsError as e:
-                    print(f"rank {rank}: rccl exchange timing failed: {e}", file=sys.stderr, flush=True)
-            timed = D.all_ok(lx is not None and lr is not None)
-            tx = D.allreduce(lx if timed else 0.0, "max")
-            tr = D.allreduce(lr if timed else 0.0, "max")
-            if timed and tr < 0.9 * tx:
-                ctx.peer_enable(False)
-            if rank == 0:
-                print(f"exchange auto: xgmi {tx:.2f} us, rccl {tr:.2f} us -> {ctx.backend}", file=sys.stderr,
-                      flush=True)
     backend = ctx.backend + ("+fold" if world > 1 and ctx.backend == "xgmi" and ctx.folded else "")
     # the untimed history fill and warm-up record the trajectory (f, |g|, alpha, x checksums at
     # the top of every iteration) for reference_parity; the timed steps run untraced
@@ -418,7 +399,7 @@ def _measure(a, D, ctx, x0, rank, world, uid, unfused, vector_free, box_probe):
     # history fill (untimed, not counted as warm-up): m iterations store m pairs, so every later
     # step uses h = m whatever --warmup is (B_iter grows with h)
     fill = run(ctx.step, a.history)
-    run(ctx.step, a.warmup)
+    warm = run(ctx.step, a.warmup)
     if trace:
         run(ctx.trace_enable, False)
     run(ctx.sync)
@@ -479,19 +460,69 @@ def _measure(a, D, ctx, x0, rank, world, uid, unfused, vector_free, box_probe):
     lat = None
     if world > 1 and not vector_free and not unfused:
         lat = {}
-        backends = (["xgmi"] if backend.startswith("xgmi") else []) + (["rccl"] if uid is not None else [])
+        if backend.startswith("xgmi") and uid is None and a.exchange == "auto":
+            # only now, with the measurement done: an RCCL communicator for the comparison leg
+            lat["rccl_leg"] = rccl_leg(D, ctx, rank)
+            uid_leg = lat["rccl_leg"]["ok"]
+        else:
+            uid_leg = uid is not None
+        backends = (["xgmi"] if backend.startswith("xgmi") else []) + (["rccl"] if uid_leg else [])
         for b in backends:
             for k in (8, 96):
-                us = run(ctx.exchange_latency, b, k, 200)
+                us = None
+                try:  # an RCCL wait is bounded in the library (LBFGS_RCCL_TIMEOUT): a stall costs this entry
+                    us = ctx.exchange_latency(b, k, 200) if not failed else None
+                except L.LbfgsError as e:
+                    if b != "rccl":
+                        failed.append(e)
+                    lat[f"{b}_{k * 8}doubles_error"] = str(e)
+                    print(f"rank {rank}: {b} exchange timing: {e}", file=sys.stderr, flush=True)
+                if b == "rccl" and not D.all_ok(us is not None):
+                    break  # a rank's RCCL timing failed: no rank enters another RCCL collective
                 if us is not None:
                     lat[f"{b}_{k * 8}doubles"] = round(us, 2)
         vote("exchange latency")
     if trace:
         res["trajectory"] = ctx.trace()
     res["history_fill"] = fill["iterations"]
+    res["warm_counters"] = {k: warm[k] for k in ("trials_f", "trials_fg", "commits", "passes")} if warm else None
     res["box_probe"] = probe
     done_steps = a.steps if res["status"] == "running" else max(res["iterations"] - a.warmup - fill["iterations"], 1)
     return T, res, prof, bytes_all, done_steps, (backend, lat)
+
+
+def rccl_leg(D, ctx, rank):
+    """Sharded, --exchange auto, after the measurement: an RCCL communicator for the comparison
+    timing (lbfgs_rccl_attach: non-blocking init, bootstrap and self-test all-gather bounded by
+    LBFGS_RCCL_TIMEOUT). A failure or stall on any rank is reported here and costs nothing else:
+    the line has been measured on the mailboxes already. BENCH_RCCL_STALL=<rank> makes that rank
+    skip the init (a peer that never joins: the other ranks' init must time out)."""
+    t0 = time.perf_counter()
+    err, mine = None, None
+    if rank == 0:
+        try:
+            mine = L.unique_id()
+        except L.LbfgsError as e:
+            err = f"unique id: {e}"
+    uid = D.broadcast_bytes(mine)  # every rank enters the broadcast (None: no id on rank 0)
+    if uid is None and err is None:
+        err = "rank 0 produced no RCCL unique id"
+    stall = os.environ.get("BENCH_RCCL_STALL")
+    if uid is not None:
+        if stall is not None and int(stall) == rank:
+            err = "BENCH_RCCL_STALL: this rank did not join the RCCL init"
+        else:
+            try:
+                ctx.rccl_attach(uid)
+            except L.LbfgsError as e:
+                err = str(e)
+    if err:
+        print(f"rank {rank}: RCCL leg: {err}", file=sys.stderr, flush=True)
+    ok = D.all_ok(err is None)
+    errs = [e for e in D.allgather_bytes(err or "") if e]
+    return {"ok": ok, "init_s": round(time.perf_counter() - t0, 2),
+            "errors": errs[:4] or None,
+            "note": "RCCL communicator created after the measurement (non-blocking init, bounded wait)"}
 
 
 def shard_check(a, D, n, x0, dev, rank, world, res):
@@ -680,6 +711,27 @@ def reference_parity(traj, live, fixture, fsrc):
     return out
 
 
+def survey_bytes(res, n, a, steps, T):
+    """SURVEY.md 8(d)'s algorithmic bytes per iteration, B_iter = 8 n (8h + 2 T_f + 3 T_g + 9), over
+    the timed steps: h = the pairs in use (m in the steady state), T_f / T_g the line-search
+    evaluations per iteration that read x and d (f only / f and g.d), counted per pass: the first
+    trial, which the commit pass takes (T_g for the Wolfe searches, T_f otherwise), plus the extra
+    trial passes the solver counted over the timed steps (a batched pass evaluating up to 4 halving
+    steps in one read of x and d counts once). Beside it the line keeps the solver's own count
+    (bytes_per_step: 8n per vector pass actually issued)."""
+    w = res.get("warm_counters")
+    if not w or steps < 1 or res.get("h_min", -1) != res.get("h_max", -2):
+        return {}
+    wolfe = a.line_search in ("wolfe", "backtracking_wolfe")
+    tf = (res["trials_f"] - w["trials_f"]) / steps + (0 if wolfe else 1)
+    tg = (res["trials_fg"] - w["trials_fg"]) / steps + (1 if wolfe else 0)
+    h = res["h_max"]
+    b = 8.0 * n * (8 * h + 2 * tf + 3 * tg + 9)
+    return {"bytes_per_step_survey": b, "achieved_hbm_gbps_survey": round(b * steps / T / 1e9, 1),
+            "survey_bytes_terms": {"formula": "8n(8h + 2T_f + 3T_g + 9), SURVEY.md 8(d)", "h": h,
+                                   "T_f": round(tf, 4), "T_g": round(tg, 4)}}
+
+
 def box_fields(probe, value, achieved_gbps, world):
     """This box's HBM rate for the two-loop passes' access pattern (lbfgs_stream_probe: 20 launches
     of a 3 R + 1 W stream over the solver's own q, y, s in the passes' geometry and cache policy,
@@ -735,10 +787,12 @@ def main():
     n = int(a.size)
     D = Dist(a.gpus)
     world, rank = a.gpus, D.rank
-    # BENCH_DEVICE_MOD (several ranks on one GPU) cannot create an RCCL communicator: RCCL
-    # refuses two ranks on one device; those rehearsals run on the peer exchange alone
+    # sharded: no RCCL communicator before the measurement (the mailboxes carry it; --exchange rccl
+    # or a mailbox failure creates one, non-blocking with a bounded wait, inside the library).
+    # BENCH_DEVICE_MOD (several ranks on one GPU) cannot measure over RCCL: RCCL refuses two ranks
+    # on one device (its comparison leg then reports that refusal)
     rehearsal = "BENCH_DEVICE_MOD" in os.environ
-    need_uid = world > 1 and not rehearsal
+    need_uid = world > 1 and a.exchange == "rccl"
     uid = D.broadcast_bytes(L.unique_id() if (need_uid and rank == 0) else None) if need_uid else None
 
     # the reference on host cores, started first and collected after the GPU work (rank 0, N=1)
@@ -762,7 +816,7 @@ def main():
         # a mailbox failure across GPUs: measure() raises on every rank together (its votes), so
         # every rank lands here and the line is measured again over RCCL rather than lost, and
         # says why
-        if not (world > 1 and uid is not None and a.exchange in ("xgmi", "auto")):
+        if not (world > 1 and uid is None and a.exchange in ("xgmi", "auto") and not rehearsal):
             raise
         fallback = f"xgmi: {e}"
         print(f"rank {rank}: {fallback}; measuring again over RCCL", file=sys.stderr, flush=True)
@@ -771,11 +825,12 @@ def main():
         a = copy.copy(a)
         a.exchange = "rccl"
         uid = D.broadcast_bytes(L.unique_id() if rank == 0 else None)
+        need_uid = True
         T, res, prof, bytes_all, done_steps, (backend, xlat) = measure(a, D, n, x0, dev, rank, world, uid,
                                                       unfused=a.unfused, vector_free=a.vector_free, box_probe=True)
     check = shard_check(a, D, n, x0, dev, rank, world, res) if world > 1 else None
     # the opt-in vector-free mode alongside the default (outside the bit-parity contract with
-    # the reference's operation order); sharded runs need a fresh RCCL id
+    # the reference's operation order); sharded runs over RCCL need a fresh id
     vf = None
     if not (a.unfused or a.vector_free or a.no_vector_free) and a.history <= 20:
         # a failure here is deterministic across ranks (same arguments everywhere) and must not
@@ -857,6 +912,8 @@ def main():
                        "exchange": backend},
             "achieved_hbm_gbps": round(bytes_all / T / 1e9, 1),
             "bytes_per_step": bytes_all / max(done_steps, 1),
+            "bytes_per_step_note": "the solver's own count: 8n per vector read or written by the passes it issued",
+            **survey_bytes(res, n, a, done_steps, T),
             "roofline": roof,
             **box_fields(res.get("box_probe"), value, bytes_all / T / 1e9, world),
             "exchange_latency_us": xlat,

@@ -125,6 +125,8 @@ int lbk_device_count(void);
 int lbk_peer_handle(lbk_ctx* c, void* out);
 int lbk_peer_connect(lbk_ctx* c, const void* handles);
 int lbk_peer_enable(lbk_ctx* c, int on);
+/* a sharded context created without an RCCL id takes a communicator (bounded init + self-test) */
+int lbk_rccl_attach(lbk_ctx* c, const void* nccl_id);
 /* 0 none (one rank), 1 RCCL, 2 xGMI peer mailboxes, 3 host group (emulated ranks) */
 int lbk_exchange_backend(const lbk_ctx* c);
 int lbk_exchange_fold(const lbk_ctx* c);
@@ -133,6 +135,8 @@ int lbk_exchange_fold(const lbk_ctx* c);
 int lbk_exchange_bench(lbk_ctx* c, int backend, int ks, int iters, double* us);
 /* LBFGS_CU_PARTITION: CUs of this rank's solver stream (0: not partitioned) */
 int lbk_cu_partition(const lbk_ctx* c);
+/* the cooperative forms' grid caps (segments) and the device searches redone on the host loop */
+int lbk_coop_info(const lbk_ctx* c, int* coop_max, int* wolfe_max, int* fallbacks);
 /* box probe: `launches` back-to-back 3 R + 1 W streams over (q, y, s) in the two-loop passes'
  * geometry and cache policy, q written back unchanged; mean microseconds per launch */
 int lbk_stream_probe(lbk_ctx* c, double* q, const double* y, const double* s, int launches, double* us);
@@ -228,6 +232,8 @@ int lbk_small_spec_ok(const lbk_ctx* c, int h);
  * trial step, its f, its g.d, have_first}; d materialised. out = {step, trial passes, last evaluated
  * step, its f, its g.d}. */
 int lbk_wolfe_dev_ok(const lbk_ctx* c, int obj);
+/* -6: the launch's grid barrier timed out (nothing stored); the device search is then off for the
+ * context and the caller redoes the search on the host loop */
 int lbk_wolfe_dev(lbk_ctx* c, int obj, const double* x, const double* d, const double* st, int iter0, double* out);
 /* *epoch: the launch's id for lbk_small_fetch (0: not a cooperative host-mirrored launch) */
 int lbk_small_iter(lbk_ctx* c, int obj, int h, const double* g, double* q, double* r, const double* const* S,

@@ -430,6 +430,16 @@ int lbfgs_peer_enable(lbfgs_ctx* c, int on) {
     return lbk_peer_enable(c->dev, on) == 0 ? 0 : LBFGS_ERR_STATE;
 }
 
+int lbfgs_rccl_attach(lbfgs_ctx* c, const void* unique_id) {
+    if (!c || !unique_id || c->geo->world <= 1) return LBFGS_ERR_BAD_ARG;
+    const int rc = lbk_rccl_attach(c->dev, unique_id);
+    if (rc != 0) {
+        snprintf(c->err, sizeof c->err, "%s", lbk_last_error(c->dev));
+        return rc == -1 ? LBFGS_ERR_BAD_ARG : rc == -3 ? LBFGS_ERR_RCCL : LBFGS_ERR_HIP;
+    }
+    return 0;
+}
+
 int lbfgs_set_dense_quadratic(lbfgs_ctx* c, const double* A, const double* b) {
     if (!c || !A || !b || c->geo->world != 1) return LBFGS_ERR_BAD_ARG;
     const int rc = lbk_dense_set(c->dev, A, b);
@@ -455,10 +465,19 @@ int lbfgs_exchange_latency(lbfgs_ctx* c, int backend, int components, int iters,
 
 int lbfgs_cu_partition(const lbfgs_ctx* c) { return c ? lbk_cu_partition(c->dev) : LBFGS_ERR_BAD_ARG; }
 
+int lbfgs_coop_info(const lbfgs_ctx* c, int* coop_max, int* search_max, int* fallbacks) {
+    return c ? lbk_coop_info(c->dev, coop_max, search_max, fallbacks) : LBFGS_ERR_BAD_ARG;
+}
+
 int lbfgs_stream_probe(lbfgs_ctx* c, int launches, double* us, double* bytes) {
     if (!c || !us || launches < 1) return LBFGS_ERR_BAD_ARG;
     if (!c->inited) return LBFGS_ERR_STATE;
-    const int rc = lbk_stream_probe(c->dev, c->q, c->Y[0], c->S[0], launches, us);
+    /* the written operand is a scratch vector, not the solver's q: nothing of the solve is touched
+     * (q - 0 * y is q only while y is finite) */
+    double* scratch = lbk_vec_alloc(c->dev);
+    if (!scratch) return dev_err(c, -2);
+    const int rc = lbk_stream_probe(c->dev, scratch, c->Y[0], c->S[0], launches, us);
+    lbk_vec_free(c->dev, scratch);
     if (rc != 0) return dev_err(c, rc);
     if (bytes) *bytes = 32.0 * (double)c->geo->n_loc;
     return 0;
@@ -870,7 +889,9 @@ static int ls_interpolation(lbfgs_ctx* c, double gd, double* out) {
 /* Small n (single rank, a cooperative size, device objective): once the Wolfe search needs a
  * trial pass, the rest of the search runs on the device in one launch (lbk_wolfe_dev: the same
  * loop, the same expressions, the same passes) instead of a launch and a host
- * round trip per trial. The step and every counter come back as the host loop would leave them. */
+ * round trip per trial. The step and every counter come back as the host loop would leave them.
+ * Returns 1 when the launch's grid barrier timed out: it stored nothing, so the host loop takes
+ * the search over from the same state (and the device form is off for the context). */
 static int wolfe_on_device(const lbfgs_ctx* c, double alpha) {
     if (ext_obj(c) || c->unfused || !c->batch || c->vf || !lbk_wolfe_dev_ok(c->dev, c->obj)) return 0;
     if (c->spec_valid && alpha == c->a0) return 0; /* the commit's first trial: no pass */
@@ -888,7 +909,9 @@ static int wolfe_device(lbfgs_ctx* c, int iter, double alpha, double alpha_lo, d
                            last ? c->tc_a[0] : 0.0, last ? c->tc_f[0] : 0.0, last ? c->tc_dphi : 0.0, last ? 1.0 : 0.0,
                            c->a0, c->spec_f, c->spec_dphi, c->spec_valid ? 1.0 : 0.0};
     double o[5];
-    DEVNC(lbk_wolfe_dev(c->dev, c->obj, c->x, c->d, st, iter, o));
+    rc = lbk_wolfe_dev(c->dev, c->obj, c->x, c->d, st, iter, o);
+    if (rc == -6) return 1; /* the launch's grid barrier timed out, nothing stored: the host loop goes on */
+    if (rc) return dev_err(c, rc);
     const int passes = (int)o[1];
     c->trials_fg += passes;
     c->trial_passes += passes;
@@ -913,7 +936,12 @@ static int ls_wolfe(lbfgs_ctx* c, double gd, double* out) {
     double alpha = K->initial_step;
     double alpha_lo = 0.0, alpha_hi = INFINITY, f_lo = f_x, dphi_lo = gd;
     for (int iter = 0; iter < 20; ++iter) {
-        if (wolfe_on_device(c, alpha)) return wolfe_device(c, iter, alpha, alpha_lo, alpha_hi, f_lo, dphi_lo, f_x, gd, out);
+        if (wolfe_on_device(c, alpha)) {
+            const int rc = wolfe_device(c, iter, alpha, alpha_lo, alpha_hi, f_lo, dphi_lo, f_x, gd, out);
+            if (rc <= 0) return rc;
+            /* 1: the device search gave up (a grid barrier timed out) having changed nothing; it is
+             * off for this context now, and this iteration of the host loop runs as it would have */
+        }
         double f_new, dphi_new;
         /* f first; the gradient only if the sufficient-decrease tests pass (:144-153) */
         int rc = trial(c, alpha, 0, &f_new, NULL);

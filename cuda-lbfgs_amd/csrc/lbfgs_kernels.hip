@@ -71,6 +71,8 @@ int lbk_geometry_plan(int64_t n, int rank, int world, lbk_geo* out) {
     return 0;
 }
 
+static int rccl_init(lbk_ctx* c, const void* nccl_id);
+
 int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const void* nccl_id, lbk_group* grp) {
     *out = nullptr;
     lbk_ctx* c = new (std::nothrow) lbk_ctx();
@@ -132,6 +134,12 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
     // (k_coop_wolfe) instead of a launch and a host round trip each; LBFGS_DEV_WOLFE=0: host loop
     c->dev_wolfe = 1;
     if (const char* e = getenv("LBFGS_DEV_WOLFE")) c->dev_wolfe = atoi(e) != 0;
+    // the device search's wait at each grid barrier (2 s; tests set 0 to force its time-out path,
+    // after which the host loop redoes the search)
+    c->search_timeout_s = 2.0;
+    if (const char* e = getenv("LBFGS_SEARCH_TIMEOUT")) c->search_timeout_s = std::max(0.0, atof(e));
+    c->rccl_timeout_s = 60.0;
+    if (const char* e = getenv("LBFGS_RCCL_TIMEOUT")) c->rccl_timeout_s = std::max(0.5, atof(e));
     c->pend_slot = -1;
     c->xf_slot = -1;
     // folded exchanges over the mailboxes: 1 (default) when every peer has a GPU of
@@ -266,6 +274,16 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
         occ = std::min(occ, o);
         if (c->cu_part) cus = c->cu_count;  // the stream sees only its own CUs
         c->coop_max = (int)std::min<int64_t>(c->coop_max, (int64_t)occ * cus);
+        // the device-resident Wolfe search has a grid barrier of its own: its own occupancy caps it
+        // (a register footprint above k_coop_iter's would otherwise over-commit the grid)
+        int wocc = 1 << 30;
+        CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, k_coop_wolfe<LBK_OBJ_ROSENBROCK>, LB_BLOCK, 0));
+        wocc = std::min(wocc, o);
+        CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, k_coop_wolfe<LBK_OBJ_QUAD_TRIDIAG>, LB_BLOCK, 0));
+        wocc = std::min(wocc, o);
+        CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, k_coop_wolfe<LBK_OBJ_QUAD_SEPARABLE>, LB_BLOCK, 0));
+        wocc = std::min(wocc, o);
+        c->wolfe_max = (int)std::min<int64_t>(c->coop_max, (int64_t)wocc * cus);
         // the persistent forms: every workgroup of their grid resident, at most `cap` per CU (the
         // occupancy answer is VGPR-bound here, where the API and the hardware agree;
         // MI355X_MICROARCH.md's one-short case is SGPR-bound, 82-98 SGPRs at 7-8 per CU). A grid that
@@ -357,25 +375,61 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
     if (world == 1 && !grp && nccl_id) {
         c->direct = 0;
         c->coop_max = 0;
+        c->wolfe_max = 0;
         c->small_seg_max = 0;
     }
-    if (!grp && nccl_id) {
-        ncclUniqueId id;
-        memcpy(&id, nccl_id, sizeof id);
-        ncclResult_t r = ncclCommInitRank(&c->comm, world, id, rank);
-        if (r != ncclSuccess) {
-            snprintf(c->err, sizeof c->err, "ncclCommInitRank: %s", ncclGetErrorString(r));
-            return -3;
-        }
-    }
+    if (!grp && nccl_id) return rccl_init(c, nccl_id);
     return 0;
+}
+
+// The RCCL communicator of a sharded context, created non-blocking and waited for with a bound
+// (LBFGS_RCCL_TIMEOUT, 60 s): a rank that never joins, or a bootstrap that stalls, costs this
+// call one timeout and an aborted communicator, not a hang
+static int rccl_init(lbk_ctx* c, const void* nccl_id) {
+    ncclUniqueId id;
+    memcpy(&id, nccl_id, sizeof id);
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    ncclComm_t comm = nullptr;
+    const ncclResult_t r = ncclCommInitRankConfig(&comm, c->geo.world, id, c->geo.rank, &cfg);
+    if (!comm) {
+        snprintf(c->err, sizeof c->err, "ncclCommInitRankConfig: %s", ncclGetErrorString(r));
+        return -3;
+    }
+    c->comm = comm;
+    return rccl_settle(c, r, "ncclCommInitRankConfig");
+}
+
+// A context created without an RCCL id (the mailboxes alone) takes a communicator afterwards
+// (bench.py: after the headline measurement, for the RCCL comparison leg)
+int lbk_rccl_attach(lbk_ctx* c, const void* nccl_id) {
+    if (!c || !nccl_id || c->grp || c->geo.world < 2) return -1;
+    if (c->comm) return 0;
+    if (c->rccl_hung) {
+        snprintf(c->err, sizeof c->err, "an earlier RCCL communicator of this context was aborted");
+        return -3;
+    }
+    HIPCHK(c, hipSetDevice(c->device));
+    int rc = rccl_init(c, nccl_id);
+    if (rc) return rc;
+    // one all-gather through it, waited for with the same bound, before anything relies on it
+    double* buf = nullptr;
+    HIPCHK(c, hipMalloc(&buf, sizeof(double) * LBK_WSLOT));
+    if (hipMemsetAsync(buf, 0, sizeof(double) * LBK_WSLOT, c->stream) != hipSuccess) rc = -2;
+    const int saved = c->xg_on;
+    c->xg_on = 0;
+    if (rc == 0) rc = exchange_buf(c, buf, LBK_KMAX);
+    c->xg_on = saved;
+    if (rc == 0) rc = rccl_stream_wait(c, "RCCL self-test all-gather");
+    if (!c->rccl_hung) (void)hipFree(buf);  // else a collective may still address it
+    return rc;
 }
 
 void lbk_destroy(lbk_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
-    if (c->stream) (void)hipStreamSynchronize(c->stream);
-    prof_flush(c);
+    if (c->stream && !c->rccl_hung) (void)hipStreamSynchronize(c->stream);
+    if (!c->rccl_hung) prof_flush(c);
     for (auto e : c->ev_free) (void)hipEventDestroy(e);
     for (auto e : c->xfer_ev)
         if (e) (void)hipEventDestroy(e);
@@ -991,7 +1045,7 @@ int lbk_small_spec_ok(const lbk_ctx* c, int h) {
 }
 
 int lbk_wolfe_dev_ok(const lbk_ctx* c, int obj) {
-    return c->dev_wolfe && c->geo.world == 1 && !c->comm && c->coop_max > 0 && c->geo.nseg <= c->coop_max &&
+    return c->dev_wolfe && c->geo.world == 1 && !c->comm && c->wolfe_max > 0 && c->geo.nseg <= c->wolfe_max &&
            (obj == LBK_OBJ_ROSENBROCK || obj == LBK_OBJ_QUAD_TRIDIAG || obj == LBK_OBJ_QUAD_SEPARABLE);
 }
 
@@ -1005,8 +1059,8 @@ int lbk_wolfe_dev(lbk_ctx* c, int obj, const double* x, const double* d, const d
     a.ll = c->wolfe_ll;
     a.seq_base = (unsigned)c->wolfe_seq;
     a.err = c->coop_err_d;
-    a.timeout = (unsigned long long)(2.0 * c->wall_khz * 1e3);  // 2 s per barrier
-    c->wolfe_seq += 20;                                          // at most 20 trial passes
+    a.timeout = (unsigned long long)(c->search_timeout_s * c->wall_khz * 1e3);  // 2 s per barrier
+    c->wolfe_seq += 20;                                                        // at most 20 trial passes
     WolfeDev w;
     w.alpha = st[0];
     w.alpha_lo = st[1];
@@ -1041,8 +1095,14 @@ int lbk_wolfe_dev(lbk_ctx* c, int obj, const double* x, const double* d, const d
     if (rc) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (*(volatile unsigned*)c->coop_err_h) {
-        snprintf(c->err, sizeof c->err, "device Wolfe search: grid barrier timed out");
-        return -2;
+        // the grid was not resident together (or a barrier waited past its bound): every workgroup
+        // has left the launch, which stored no vector, so the caller redoes the search on the host
+        // loop from the same state; the device form stays off for this context
+        *(volatile unsigned*)c->coop_err_h = 0;
+        c->dev_wolfe = 0;
+        c->coop_fallbacks++;
+        snprintf(c->err, sizeof c->err, "device Wolfe search: grid barrier timed out (search redone on the host loop)");
+        return -6;
     }
     for (int k = 0; k < 5; ++k) out[k] = ((volatile double*)c->wolfe_out_h)[k];
     c->bytes_total += out[1] * 2.0 * 8.0 * (double)c->geo.n_loc;  // x and d per trial pass
@@ -1220,8 +1280,9 @@ int lbk_checksum(lbk_ctx* c, const double* x, uint64_t* c1, uint64_t* c2) {
             snprintf(c->err, sizeof c->err, "sharded context has no exchange backend");
             return -3;
         }
-        ncclResult_t r = ncclAllReduce(c->d_ck, c->d_ck, 2, ncclUint64, ncclSum, c->comm, c->stream);
-        if (r != ncclSuccess) return -3;
+        const int rrc = rccl_settle(c, ncclAllReduce(c->d_ck, c->d_ck, 2, ncclUint64, ncclSum, c->comm, c->stream),
+                                    "ncclAllReduce");
+        if (rrc) return rrc;
     }
     HIPCHK(c, hipMemcpyAsync(c->h_ck, c->d_ck, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -1328,6 +1389,13 @@ int lbk_peer_enable(lbk_ctx* c, int on) {
 
 int lbk_cu_partition(const lbk_ctx* c) { return c->cu_part ? c->cu_count : 0; }
 
+int lbk_coop_info(const lbk_ctx* c, int* coop_max, int* wolfe_max, int* fallbacks) {
+    if (coop_max) *coop_max = c->coop_max;
+    if (wolfe_max) *wolfe_max = c->dev_wolfe ? c->wolfe_max : 0;
+    if (fallbacks) *fallbacks = c->coop_fallbacks;
+    return 0;
+}
+
 int lbk_stream_probe(lbk_ctx* c, double* q, const double* y, const double* s, int launches, double* us) {
     if (launches < 1 || !us || !q || !y || !s) return -1;
     HIPCHK(c, hipSetDevice(c->device));
@@ -1345,13 +1413,17 @@ int lbk_stream_probe(lbk_ctx* c, double* q, const double* y, const double* s, in
         return -2;
     }
     HIPCHK(c, hipEventRecord(a, c->stream));
+    const int par = c->rev_par;  // the solver's walk parity is left as it was
     for (int i = 0; i < launches; ++i) {
         const Geo g = kgeo(c);  // alternating walk, as the passes
         NT_DISPATCH(c, hipLaunchKernelGGL(k_probe_stream<NT_>, dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, q, y, s,
                                           g, c->partials));
-        HIPCHK(c, hipGetLastError());
         c->rev_par ^= 1;
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) c->rev_par = par;
+        HIPCHK(c, e);
     }
+    c->rev_par = par;
     HIPCHK(c, hipEventRecord(b, c->stream));
     HIPCHK(c, hipEventSynchronize(b));
     float ms = 0.f;
@@ -1376,15 +1448,18 @@ int lbk_exchange_bench(lbk_ctx* c, int backend, int ks, int iters, double* us) {
     double* buf = nullptr;
     HIPCHK(c, hipMalloc(&buf, sizeof(double) * LBK_WSLOT));
     HIPCHK(c, hipMemsetAsync(buf, 0, sizeof(double) * LBK_WSLOT, c->stream));
+    // an RCCL wait is bounded (rccl_stream_wait); the mailbox kernels bound their own waits
+    auto wait = [&]() { return backend == 1 ? rccl_stream_wait(c, "RCCL exchange timing")
+                                            : (hipStreamSynchronize(c->stream) == hipSuccess ? 0 : -2); };
     int rc = exchange_buf(c, buf, ks);  // warm-up, also lines the ranks up
-    if (rc == 0 && hipStreamSynchronize(c->stream) != hipSuccess) rc = -2;
+    if (rc == 0) rc = wait();
     timespec t0, t1;
     clock_gettime(CLOCK_MONOTONIC, &t0);
     for (int i = 0; i < iters && rc == 0; ++i) rc = exchange_buf(c, buf, ks);
-    if (rc == 0 && hipStreamSynchronize(c->stream) != hipSuccess) rc = -2;
+    if (rc == 0) rc = wait();
     clock_gettime(CLOCK_MONOTONIC, &t1);
     c->xg_on = saved;
-    (void)hipFree(buf);
+    if (!c->rccl_hung) (void)hipFree(buf);
     if (rc == 0 && backend == 2 && lbk_xgmi_failed(c->xg)) rc = -3;
     *us = ((double)(t1.tv_sec - t0.tv_sec) * 1e6 + (double)(t1.tv_nsec - t0.tv_nsec) * 1e-3) / iters;
     return rc;

@@ -41,6 +41,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <pthread.h>
+#include <unistd.h>
 #include <cstring>
 #include <ctime>
 #include <new>
@@ -2768,8 +2769,9 @@ __global__ void k_point(double* __restrict__ z, const double* __restrict__ x, co
 //   op 1: out = a + b          (add, :53-63)
 //   op 2: out = -a             (negative, :65-73)
 //   op 3: out = a + alpha * b  (x + (alpha d), the trial point of every line search)
-__global__ void k_elementwise(int op, double* __restrict__ out, const double* __restrict__ a,
-                              const double* __restrict__ b, double alpha, int64_t n_loc) {
+// out may alias a or b (the CUDA-compat loop's in-place axpys, lbfgs_driver.c iterate_cuda): each
+// element is read before it is written, and no __restrict__ promises otherwise
+__global__ void k_elementwise(int op, double* out, const double* a, const double* b, double alpha, int64_t n_loc) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_loc; i += (int64_t)gridDim.x * blockDim.x) {
         double v;
         switch (op) {
@@ -2904,6 +2906,12 @@ struct lbk_ctx {
     unsigned long long* h_ck;
     int64_t vec_doubles;  // allocation per vector
     ncclComm_t comm;
+    // RCCL is driven non-blocking (ncclConfig_t::blocking = 0): its bootstrap, every enqueue and
+    // a host wait on an RCCL collective end after rccl_timeout_s (LBFGS_RCCL_TIMEOUT, 60 s) with
+    // the communicator aborted, never in a hang; rccl_hung: an aborted collective may still sit
+    // on the stream, which destroy then does not wait for
+    double rccl_timeout_s;
+    int rccl_hung;
     char err[256];
     // profiling
     int prof_on;
@@ -2957,6 +2965,9 @@ struct lbk_ctx {
     // device-resident Wolfe search (k_coop_wolfe, LBFGS_DEV_WOLFE): flagged partials and sequence
     // numbers of its own (never rolled back), results in mapped host memory
     int dev_wolfe;
+    int wolfe_max;         // its grid cap: k_coop_wolfe's own occupancy x CUs (and coop_max)
+    int coop_fallbacks;    // device searches redone on the host loop after a barrier time-out
+    double search_timeout_s; // the device search's wait per grid barrier (LBFGS_SEARCH_TIMEOUT, 2 s)
     unsigned long long* wolfe_ll;
     unsigned long long wolfe_seq;
     double *wolfe_out_h, *wolfe_out_d;
@@ -3161,6 +3172,54 @@ int prof_flush(lbk_ctx* c) {
     return 0;
 }
 
+double mono_s() {
+    timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return (double)t.tv_sec + 1e-9 * (double)t.tv_nsec;
+}
+
+// Ends an RCCL call on the non-blocking communicator: ncclInProgress is polled through
+// ncclCommGetAsyncError for at most rccl_timeout_s; a timeout or an error aborts the communicator
+// (ncclCommAbort also stops its kernels) and leaves the context without one (-3, LBFGS_ERR_RCCL).
+int rccl_settle(lbk_ctx* c, ncclResult_t r, const char* what) {
+    const double t_end = mono_s() + c->rccl_timeout_s;
+    while (r == ncclInProgress) {
+        if (mono_s() > t_end) break;
+        usleep(100);
+        if (ncclCommGetAsyncError(c->comm, &r) != ncclSuccess) r = ncclInternalError;
+    }
+    if (r == ncclSuccess) return 0;
+    if (r == ncclInProgress)
+        snprintf(c->err, sizeof c->err, "%s: no progress in %.0f s (RCCL communicator aborted)", what, c->rccl_timeout_s);
+    else
+        snprintf(c->err, sizeof c->err, "%s: %s (RCCL communicator aborted)", what, ncclGetErrorString(r));
+    (void)ncclCommAbort(c->comm);
+    c->comm = nullptr;
+    c->rccl_hung = 1;
+    return -3;
+}
+
+// A host wait on the solver stream while RCCL work is queued on it: bounded like rccl_settle
+int rccl_stream_wait(lbk_ctx* c, const char* what) {
+    const double t_end = mono_s() + c->rccl_timeout_s;
+    for (;;) {
+        const hipError_t e = hipStreamQuery(c->stream);
+        if (e == hipSuccess) return 0;
+        if (e != hipErrorNotReady) {
+            snprintf(c->err, sizeof c->err, "%s: %s", what, hipGetErrorString(e));
+            return -2;
+        }
+        if (mono_s() > t_end) break;
+        usleep(50);
+    }
+    snprintf(c->err, sizeof c->err, "%s: the RCCL collective did not complete in %.0f s (communicator aborted)", what,
+             c->rccl_timeout_s);
+    if (c->comm) (void)ncclCommAbort(c->comm);
+    c->comm = nullptr;
+    c->rccl_hung = 1;
+    return -3;
+}
+
 // Sharded runs: each rank owns groups [g_lo, g_hi) of every result slot; gather them so
 // every rank holds all 8 (one RCCL all-gather of (8/world) x KMAX doubles per reduction, in
 // place, on the solver stream), or through the host group for emulated ranks.
@@ -3192,12 +3251,8 @@ int exchange_buf(lbk_ctx* c, double* base, int ks, double* host_mirror = nullptr
         snprintf(c->err, sizeof c->err, "sharded context has no exchange backend (no RCCL id, peers not enabled)");
         return -3;
     }
-    ncclResult_t r = ncclAllGather(base + c->geo.g_lo * ks, base, (size_t)per, ncclDouble, c->comm, c->stream);
-    if (r != ncclSuccess) {
-        snprintf(c->err, sizeof c->err, "ncclAllGather: %s", ncclGetErrorString(r));
-        return -3;
-    }
-    return 0;
+    return rccl_settle(c, ncclAllGather(base + c->geo.g_lo * ks, base, (size_t)per, ncclDouble, c->comm, c->stream),
+                       "ncclAllGather");
 }
 
 // Over the peer mailboxes the exchange kernel also completes the host mirror of the slots the

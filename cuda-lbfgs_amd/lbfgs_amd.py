@@ -115,11 +115,13 @@ def lib():
     L.lbfgs_peer_handle.argtypes = [vp, C.c_char_p]
     L.lbfgs_peer_connect.argtypes = [vp, C.c_char_p]
     L.lbfgs_peer_enable.argtypes = [vp, C.c_int]
+    L.lbfgs_rccl_attach.argtypes = [vp, C.c_char_p]
     L.lbfgs_exchange_backend.argtypes = [vp]
     L.lbfgs_exchange_fold.argtypes = [vp]
     L.lbfgs_exchange_latency.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_double)]
     L.lbfgs_spec_stats.argtypes = [vp, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
     L.lbfgs_cu_partition.argtypes = [vp]
+    L.lbfgs_coop_info.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]
     L.lbfgs_stream_probe.argtypes = [vp, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double)]
     L.lbfgs_prof_enable.argtypes = [vp, C.c_int]
     L.lbfgs_prof_enable.restype = None
@@ -140,9 +142,9 @@ EXPORTED_SYMBOLS = [
     "lbfgs_trace_enable",
     "lbfgs_dev_dot", "lbfgs_dev_norm", "lbfgs_dev_objective", "lbfgs_dev_trial",
     "lbfgs_dev_twoloop", "lbfgs_dev_elementwise", "lbfgs_line_search", "lbfgs_prof_enable",
-    "lbfgs_prof_reset", "lbfgs_prof_get", "lbfgs_peer_handle", "lbfgs_peer_connect", "lbfgs_peer_enable",
+    "lbfgs_prof_reset", "lbfgs_prof_get", "lbfgs_peer_handle", "lbfgs_peer_connect", "lbfgs_peer_enable", "lbfgs_rccl_attach",
     "lbfgs_exchange_backend", "lbfgs_exchange_fold", "lbfgs_exchange_latency", "lbfgs_device_count", "lbfgs_set_dense_quadratic", "lbfgs_build_info",
-    "lbfgs_spec_stats", "lbfgs_cu_partition", "lbfgs_stream_probe",
+    "lbfgs_spec_stats", "lbfgs_cu_partition", "lbfgs_stream_probe", "lbfgs_coop_info",
 ]
 PEER_HANDLE_BYTES = 64
 BACKENDS = {0: "single", 1: "rccl", 2: "xgmi", 3: "host-group"}
@@ -332,6 +334,14 @@ class Context:
         if rc != 0:
             self._err("lbfgs_peer_enable", rc)
 
+    def rccl_attach(self, uid):
+        """Give this sharded context (created without an RCCL id) a communicator: collective over
+        every rank, bounded by LBFGS_RCCL_TIMEOUT (60 s); raises LbfgsError on a failed or stalled
+        init, leaving the context on its mailboxes."""
+        rc = lib().lbfgs_rccl_attach(self.h, uid)
+        if rc != 0:
+            self._err("lbfgs_rccl_attach", rc)
+
     def exchange_latency(self, backend, components=8, iters=200):
         """Collective: microseconds per exchange through 'rccl' or 'xgmi' (every rank calls)."""
         us = C.c_double()
@@ -344,6 +354,13 @@ class Context:
     @property
     def backend(self):
         return BACKENDS.get(lib().lbfgs_exchange_backend(self.h), "unknown")
+
+    def coop_info(self):
+        """dict(coop_max, search_max, fallbacks): the cooperative forms' grid caps (segments) and
+        the device line searches redone on the host loop after a grid-barrier time-out"""
+        a, b, f = C.c_int(), C.c_int(), C.c_int()
+        lib().lbfgs_coop_info(self.h, C.byref(a), C.byref(b), C.byref(f))
+        return dict(coop_max=a.value, search_max=b.value, fallbacks=f.value)
 
     @property
     def cu_partition(self):
@@ -398,7 +415,8 @@ class Context:
                 (FLAG_VECTOR_FREE if vector_free else 0) | (FLAG_REFERENCE_CALLS if reference_calls else 0) | \
                 (FLAG_CUDA_COMPAT if cuda_compat else 0) | (FLAG_CUDA_VARIANT if cuda_variant else 0)
         cb = self._host_fn(f, grad) if objective == "host" else None
-        k = consts if consts is not None else constants()
+        # the CUDA path reads parallel-implementation/constants.h (C2 = 0.7), not config.h
+        k = consts if consts is not None else constants("cuda" if cuda_compat else "config")
         rc = lib().lbfgs_minimize(self.h, OBJECTIVES[objective], C.byref(cb) if cb else None,
                                   LINE_SEARCHES[line_search], C.byref(k), x0, x,
                                   int(max_iterations), float(tolerance), flags, C.byref(res))

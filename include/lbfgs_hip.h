@@ -105,7 +105,9 @@ enum {
  * every vector stays on the device, scalars round-trip per dot as the cuBLAS host-pointer calls do.
  * Bit-exact with the oracle's restatement of that path (ORC_CANON); parity with the CUDA program
  * itself is unpinned (no CUDA toolchain here), its line searches are pinned against
- * line_search.cpp compiled here. Trace entry k = the state iteration k prints after its step. */
+ * line_search.cpp compiled here. Trace entry k = the state iteration k prints after its step.
+ * The caller passes the CUDA path's constants with it (lbfgs_constants_cuda: parallel-
+ * implementation/constants.h, C2 = 0.7); the flag does not change the constants it is given. */
 #define LBFGS_FLAG_CUDA_COMPAT 64u
 /* with LBFGS_FLAG_CUDA_COMPAT: the string-less LBFGS_CUDA of the four variant files instead, each
  * with its own inline line search (the line_search argument names the file): backtracking =
@@ -204,9 +206,16 @@ int lbfgs_device_count(void);
 int lbfgs_peer_handle(lbfgs_ctx* ctx, void* out /* LBFGS_PEER_HANDLE_BYTES */);
 int lbfgs_peer_connect(lbfgs_ctx* ctx, const void* handles /* world x LBFGS_PEER_HANDLE_BYTES */);
 /* on = 1: exchanges through the mailboxes (after a successful connect on every rank); on = 0: back
- * to the RCCL communicator (LBFGS_ERR_STATE without one). Every rank must make the same choice;
- * bench.py --exchange auto keeps the mailboxes unless RCCL measures >10 % faster. */
+ * to the RCCL communicator (LBFGS_ERR_STATE without one). Every rank must make the same choice. */
 int lbfgs_peer_enable(lbfgs_ctx* ctx, int on);
+/* A sharded context created without a unique_id takes an RCCL communicator afterwards (every rank
+ * calls it with the same id). Every RCCL communicator of the library is created non-blocking and
+ * waited for with a bound (LBFGS_RCCL_TIMEOUT seconds, default 60), and so are the host's waits on
+ * its collectives: a rank that never joins, a stalled bootstrap or a collective that does not
+ * complete returns LBFGS_ERR_RCCL with the communicator aborted, never a hang. This call also runs
+ * one all-gather through the new communicator under the same bound. Exchanges stay on the
+ * mailboxes until lbfgs_peer_enable(ctx, 0). */
+int lbfgs_rccl_attach(lbfgs_ctx* ctx, const void* unique_id /* 128 bytes, lbfgs_unique_id */);
 /* 0: one rank, 1: RCCL all-gathers, 2: xGMI peer mailboxes, 3: host group (emulated ranks) */
 int lbfgs_exchange_backend(const lbfgs_ctx* ctx);
 /* 1 when the mailbox exchanges of the two-loop are folded into the passes (the producing pass
@@ -224,9 +233,14 @@ int lbfgs_exchange_latency(lbfgs_ctx* ctx, int backend, int components, int iter
  * folded exchanges run ungated, as across GPUs. Returns the rank's CU count, 0 when not
  * partitioned. */
 int lbfgs_cu_partition(const lbfgs_ctx* ctx);
+/* Diagnostic: the cooperative forms' grid caps in canonical segments, from each kernel's own
+ * occupancy x the stream's CUs: *coop_max for the one-launch iteration (k_coop_iter), *search_max
+ * for the device-resident line search (k_coop_wolfe; 0 when off); *fallbacks = device searches
+ * whose grid barrier timed out (LBFGS_SEARCH_TIMEOUT, 2 s) and that the host loop redid. */
+int lbfgs_coop_info(const lbfgs_ctx* ctx, int* coop_max, int* search_max, int* fallbacks);
 /* Diagnostic (no reference counterpart): `launches` back-to-back streams of 3 reads + 1 write
- * over the context's own work and history vectors (q, y, s of the pair pool) in the two-loop
- * passes' geometry and cache policy, q written back unchanged. *us = mean microseconds per
+ * over a scratch work vector and the context's history vectors (y, s of the pair pool) in the
+ * two-loop passes' geometry and cache policy; the solve's own vectors and state are untouched. *us = mean microseconds per
  * launch, *bytes = this rank's bytes per launch (32 n_loc). bench.py reports this box's rate for
  * the passes' access pattern beside the solver's. Call between lbfgs_solver_step calls of an
  * initialised solve. */

@@ -123,6 +123,11 @@ int lbk_peer_enable(lbk_ctx* c, int on) {
     (void)on;
     return -5;
 }
+int lbk_rccl_attach(lbk_ctx* c, const void* id) {
+    (void)c;
+    (void)id;
+    return -1;
+}
 int lbk_exchange_backend(const lbk_ctx* c) {
     (void)c;
     return 0;
@@ -138,6 +143,13 @@ int lbk_exchange_bench(lbk_ctx* c, int b, int ks, int it, double* us) {
 }
 int lbk_cu_partition(const lbk_ctx* c) {
     (void)c;
+    return 0;
+}
+int lbk_coop_info(const lbk_ctx* c, int* a, int* b, int* f) {
+    (void)c;
+    if (a) *a = 0;
+    if (b) *b = 0;
+    if (f) *f = 0;
     return 0;
 }
 int lbk_stream_probe(lbk_ctx* c, double* q, const double* y, const double* s, int launches, double* us) {
