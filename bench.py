@@ -137,10 +137,17 @@ def self_launch(argv, world, timeout, script=None):
     old = signal.signal(signal.SIGTERM, on_term)
     rc = 0
     fwd = None
+    # BENCH_RANK_WRAPPER (profiling): a command each rank is started under, e.g. "rocprofv3
+    # --kernel-trace --stats -d DIR -o %pid% --": the profiler then starts the rank itself (this
+    # launcher stays outside it and never touches a GPU)
+    import shlex
+
+    wrap = shlex.split(os.environ.get("BENCH_RANK_WRAPPER", ""))
     try:
         for r in range(world):
             env = dict(base, RANK=str(r), LOCAL_RANK=str(r), GROUP_RANK="0")
-            procs.append(subprocess.Popen([sys.executable, script, *argv], env=env, start_new_session=True,
+            env.pop("BENCH_RANK_WRAPPER", None)
+            procs.append(subprocess.Popen([*wrap, sys.executable, script, *argv], env=env, start_new_session=True,
                                           stdout=subprocess.PIPE if r == 0 else sys.stderr.fileno()))
             if r == 0:
                 fwd = threading.Thread(target=forward, args=(procs[0].stdout,), daemon=True)
@@ -491,6 +498,9 @@ def _measure(a, D, ctx, x0, rank, world, uid, unfused, vector_free, box_probe):
     return T, res, prof, bytes_all, done_steps, (backend, lat)
 
 
+RCCL_ABANDONED = False
+
+
 def rccl_leg(D, ctx, rank):
     """Sharded, --exchange auto, after the measurement: an RCCL communicator for the comparison
     timing (lbfgs_rccl_attach: non-blocking init, bootstrap and self-test all-gather bounded by
@@ -518,6 +528,9 @@ def rccl_leg(D, ctx, rank):
                 err = str(e)
     if err:
         print(f"rank {rank}: RCCL leg: {err}", file=sys.stderr, flush=True)
+        if "abandoned" in err:  # an RCCL thread still waits in its bootstrap: main() ends with os._exit
+            global RCCL_ABANDONED
+            RCCL_ABANDONED = True
     ok = D.all_ok(err is None)
     errs = [e for e in D.allgather_bytes(err or "") if e]
     return {"ok": ok, "init_s": round(time.perf_counter() - t0, 2),
@@ -932,6 +945,12 @@ def main():
         }
         print(json.dumps(out), flush=True)
     D.close()
+    if RCCL_ABANDONED:
+        # an abandoned RCCL bootstrap thread could hold the interpreter's teardown: every context is
+        # closed and the line printed, so the process ends here
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0)
 
 
 if __name__ == "__main__":

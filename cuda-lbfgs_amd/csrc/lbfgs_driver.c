@@ -68,9 +68,7 @@ struct lbfgs_ctx {
     int m;
     /* device vectors */
     double *x, *g, *xn, *gn, *d, *q, *r, *gt;
-    double *q2, *r2;    /* ping-pong partners of q and r (two-loop passes write out of place) */
     const double* rc;   /* the r the last two-loop pass wrote */
-    int pingpong;
     double* S[MMAX + 1];
     double* Y[MMAX + 1];
     /* history: ring[0] oldest .. ring[h-1] newest, indices into the m+1 pair pool */
@@ -277,7 +275,7 @@ int lbfgs_unique_id(void* out128) { return lbk_unique_id(out128) == 0 ? 0 : LBFG
 int lbfgs_device_count(void) { return lbk_device_count(); }
 
 static void free_vectors(lbfgs_ctx* c) {
-    double** v[] = {&c->x, &c->g, &c->xn, &c->gn, &c->d, &c->q, &c->r, &c->gt, &c->q2, &c->r2, &c->g0c};
+    double** v[] = {&c->x, &c->g, &c->xn, &c->gn, &c->d, &c->q, &c->r, &c->gt, &c->g0c};
     for (size_t i = 0; i < sizeof v / sizeof v[0]; ++i) {
         lbk_vec_free(c->dev, *v[i]);
         *v[i] = NULL;
@@ -1361,33 +1359,23 @@ static int iterate(lbfgs_ctx* c) {
                     DEV(lbk_dot(c->dev, c->S[top], c->g, SLOT_P0));
                     refA[h - 1] = REF(SLOT_P0, 0);
                 }
-                /* q and r ping-pong between two buffers when c->pingpong: every pass writes a
-                 * different vector than it reads (same values; measured faster) */
+                /* q and r are updated in place (the passes' q/r stay in the Infinity Cache; a
+                 * ping-pong between two buffers measured neutral at 1e8 and -8 % at 1e7) */
                 const double* qsrc = c->g;
-                double* qb[2] = {c->q, c->pingpong ? c->q2 : c->q};
-                int qi = 0;
                 for (int i = h - 2; i >= 0; --i) {
-                    double* qout = qb[qi];
-                    qi ^= 1;
-                    DEV(lbk_axpy_dot(c->dev, qout, qsrc, c->Y[c->ring[i + 1]], c->S[c->ring[i]], rho[i + 1],
+                    DEV(lbk_axpy_dot(c->dev, c->q, qsrc, c->Y[c->ring[i + 1]], c->S[c->ring[i]], rho[i + 1],
                                      refA[i + 1], SLOT_A0 + i));
                     refA[i] = REF(SLOT_A0 + i, 0);
-                    qsrc = qout;
+                    qsrc = c->q;
                 }
                 DEV(lbk_mid(c->dev, c->r, qsrc, c->Y[c->ring[0]], rho[0], gamma, refA[0], SLOT_B0(m)));
                 refB[0] = REF(SLOT_B0(m), 0);
-                double* rb[2] = {c->r, c->pingpong ? c->r2 : c->r};
-                int ri = 1;
-                const double* rcur = c->r;
                 for (int i = 0; i + 1 < h; ++i) {
-                    double* rout = rb[ri];
-                    ri ^= 1;
-                    DEV(lbk_axpy2_dot(c->dev, rout, rcur, c->S[c->ring[i]], c->Y[c->ring[i + 1]], rho[i], refB[i],
+                    DEV(lbk_axpy2_dot(c->dev, c->r, c->r, c->S[c->ring[i]], c->Y[c->ring[i + 1]], rho[i], refB[i],
                                       refA[i], SLOT_B0(m) + i + 1));
                     refB[i + 1] = REF(SLOT_B0(m) + i + 1, 0);
-                    rcur = rout;
                 }
-                c->rc = rcur;
+                c->rc = c->r;
                 c->rho_last = rho[h - 1];
                 c->ref_b_last = refB[h - 1];
                 c->ref_a_last = refA[h - 1];
@@ -2255,18 +2243,6 @@ int lbfgs_solver_init(lbfgs_ctx* c, int objective, const lbfgs_host_fn* cb, int 
         if (e) c->batch = atoi(e) != 0;
     }
     if (c->unfused && (objective >= LBFGS_OBJ_HOST || c->geo->world != 1)) return LBFGS_ERR_BAD_ARG;
-    /* ping-pong q/r (LBFGS_PINGPONG=1): measured neutral at n=1e8 and -8 % at n=1e7 (the
-     * in-place passes keep q/r in the Infinity Cache), so in-place is the default */
-    c->pingpong = 0;
-    {
-        const char* e = getenv("LBFGS_PINGPONG");
-        if (e) c->pingpong = atoi(e) != 0;
-    }
-    if (c->pingpong && !c->q2) {
-        c->q2 = lbk_vec_alloc(c->dev);
-        c->r2 = lbk_vec_alloc(c->dev);
-        if (!c->q2 || !c->r2) return LBFGS_ERR_NOMEM;
-    }
     c->vf = (flags & LBFGS_FLAG_VECTOR_FREE) != 0;
     if (c->vf) {
         if (c->unfused || objective >= LBFGS_OBJ_HOST || c->m > LBK_VF_HMAX) return LBFGS_ERR_BAD_ARG;

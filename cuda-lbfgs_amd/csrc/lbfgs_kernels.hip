@@ -2,6 +2,7 @@
 // results, exchange, profiling (kernels and helpers: lbfgs_kernels_impl.h).
 #include "lbfgs_kernels_impl.h"
 
+#include <atomic>
 #include <thread>
 
 extern "C" {
@@ -116,8 +117,12 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
     // enables it for nseg <= N). Measured 1.8x slower at n=1e4 and 5x at 3e4 than the launch
     // sequence (profiles/r01/small_persistent.txt): one workgroup pays an L2 round trip per
     // segment step, more than the kernel boundaries it removes. Off by default.
+    // (variant builds only: -DLBK_SMALL_SEGS=<segments>, tools/build_variant.sh)
+#ifdef LBK_SMALL_SEGS
+    c->small_seg_max = LBK_SMALL_SEGS;
+#else
     c->small_seg_max = 0;
-    if (const char* e = getenv("LBFGS_SMALL_SEGS")) c->small_seg_max = atoi(e);
+#endif
     // measured (profiles/r01/coop_ab.txt): +48 % at n = 1e4 (14-15k -> 22k it/s), +41 % at 3e4,
     // +22 % at 1e5 (196 segments); -22 % at 391 segments and -38 % at 508, where the barrier's
     // fan-in and every workgroup's read of all partials outweigh the saved launches. Bit-identical
@@ -169,9 +174,13 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
     c->direct = world == 1 ? 1 : 0;
     if (const char* e = getenv("LBFGS_DIRECT")) c->direct = world == 1 && atoi(e) != 0;
     // measured neutral in 4-rank rehearsals on one GPU (profiles/r01/xgmi_mirror_ab.txt), where
-    // the ranks share the card; the saved copy is ~1 % of an 8-GPU iteration at best: opt-in
+    // the ranks share the card; the saved copy is ~1 % of an 8-GPU iteration at best: variant
+    // builds only (-DLBK_XGMI_MIRROR=1)
+#ifdef LBK_XGMI_MIRROR
+    c->xg_mirror = LBK_XGMI_MIRROR;
+#else
     c->xg_mirror = 0;
-    if (const char* e = getenv("LBFGS_XGMI_MIRROR")) c->xg_mirror = atoi(e) != 0;
+#endif
     *out = c;
 #define CK(expr)                                                                             \
     do {                                                                                     \
@@ -189,16 +198,26 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
     // take across GPUs.
     c->cu_part = 0;
     if (const char* e = getenv("LBFGS_CU_PARTITION")) c->cu_part = world > 1 && !grp && atoi(e) != 0;
+    int pworld = world, prank = rank;
+#ifdef LBK_DEBUG_CU_WORLD  // timing experiments only (variant builds): a one-rank context confined to
+    // rank LBFGS_DEBUG_CU_RANK's (default 0) CU share of a LBK_DEBUG_CU_WORLD-rank partition
+    if (world == 1 && !grp) {
+        c->cu_part = 1;
+        pworld = LBK_DEBUG_CU_WORLD;
+        prank = 0;
+        if (const char* e = getenv("LBFGS_DEBUG_CU_RANK")) prank = atoi(e) % LBK_DEBUG_CU_WORLD;
+    }
+#endif
     if (c->cu_part) {
         int cus = 0;
         CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
-        const int per = cus / world;
+        const int per = cus / pworld;
         if (per < 1) {
-            snprintf(c->err, sizeof c->err, "LBFGS_CU_PARTITION: %d CUs cannot be split over %d ranks", cus, world);
+            snprintf(c->err, sizeof c->err, "LBFGS_CU_PARTITION: %d CUs cannot be split over %d ranks", cus, pworld);
             return -1;
         }
         std::vector<uint32_t> mask((size_t)(cus + 31) / 32, 0u);
-        for (int i = rank * per; i < (rank + 1) * per; ++i) mask[(size_t)i >> 5] |= 1u << (i & 31);
+        for (int i = prank * per; i < (prank + 1) * per; ++i) mask[(size_t)i >> 5] |= 1u << (i & 31);
         CK(hipExtStreamCreateWithCUMask(&c->stream, (uint32_t)mask.size(), mask.data()));
         std::vector<uint32_t> got(mask.size(), 0u);
         CK(hipExtStreamGetCUMask(c->stream, (uint32_t)got.size(), got.data()));
@@ -294,8 +313,12 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
         // queries use the same figure
         int lds_cu = 0;
         CK(hipDeviceGetAttribute(&lds_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, device));
-        int lds_on = 1;
-        if (const char* e = getenv("LBFGS_PERSIST_LDS")) lds_on = atoi(e) != 0;
+        // (an A/B without the reservation changed nothing: -DLBK_PERSIST_LDS=0 in variant builds)
+#ifdef LBK_PERSIST_LDS
+        const int lds_on = LBK_PERSIST_LDS;
+#else
+        const int lds_on = 1;
+#endif
         c->persist_lds = lds_on && lds_cu > 0 ? lds_cu / (cap + 1) + 1024 : 0;
         c->persist_gmax = 0;
 #if LBK_PERSIST_ITER
@@ -343,10 +366,18 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
     }
     c->persist_on = 0;
     if (const char* e = getenv("LBFGS_PERSIST")) c->persist_on = atoi(e);  // 1: whole iteration, 2: two-loop
+    // strided segment ownership and walks without the alternation measured slower:
+    // variant builds only (-DLBK_PERSIST_STRIDE=1, -DLBK_PERSIST_ALT=0)
+#ifdef LBK_PERSIST_STRIDE
+    c->persist_stride = LBK_PERSIST_STRIDE;
+#else
     c->persist_stride = 0;
-    if (const char* e = getenv("LBFGS_PERSIST_OWN")) c->persist_stride = strcmp(e, "stride") == 0;
+#endif
+#ifdef LBK_PERSIST_ALT
+    c->persist_alt = LBK_PERSIST_ALT;
+#else
     c->persist_alt = 1;
-    if (const char* e = getenv("LBFGS_PERSIST_ALT")) c->persist_alt = atoi(e) != 0;
+#endif
     CK(hipMalloc(&c->fold_wait, sizeof(unsigned long long)));
     CK(hipMemset(c->fold_wait, 0, sizeof(unsigned long long)));
     CK(hipMalloc(&c->persist_cnt, sizeof(unsigned long long) * LBK_GROUPS));
@@ -382,22 +413,68 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
     return 0;
 }
 
-// The RCCL communicator of a sharded context, created non-blocking and waited for with a bound
-// (LBFGS_RCCL_TIMEOUT, 60 s): a rank that never joins, or a bootstrap that stalls, costs this
-// call one timeout and an aborted communicator, not a hang
-static int rccl_init(lbk_ctx* c, const void* nccl_id) {
+// The RCCL communicator of a sharded context, created on a helper thread and waited for with a
+// bound (LBFGS_RCCL_TIMEOUT, 60 s): a rank that never joins, or a bootstrap that stalls, costs this
+// call one timeout, not a hang. (A non-blocking ncclCommInitRankConfig alone is not enough: on this
+// RCCL the call itself blocked in its bootstrap when a peer never joined, profiles/r05/rccl_leg/.)
+// On a timeout the thread is abandoned, still waiting inside RCCL, and ends with the process.
+namespace {
+struct RcclInitJob {
     ncclUniqueId id;
-    memcpy(&id, nccl_id, sizeof id);
-    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
-    cfg.blocking = 0;
+    int device, world, rank;
     ncclComm_t comm = nullptr;
-    const ncclResult_t r = ncclCommInitRankConfig(&comm, c->geo.world, id, c->geo.rank, &cfg);
-    if (!comm) {
+    ncclResult_t r = ncclInProgress;
+    std::atomic<int> done{0};
+    std::atomic<int> abandoned{0};
+};
+}  // namespace
+
+static int rccl_init(lbk_ctx* c, const void* nccl_id) {
+    RcclInitJob* job = new (std::nothrow) RcclInitJob();
+    if (!job) return -4;
+    memcpy(&job->id, nccl_id, sizeof job->id);
+    job->device = c->device;
+    job->world = c->geo.world;
+    job->rank = c->geo.rank;
+    try {
+        std::thread([job] {
+            (void)hipSetDevice(job->device);
+            ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+            cfg.blocking = 1;
+            ncclComm_t comm = nullptr;
+            const ncclResult_t r = ncclCommInitRankConfig(&comm, job->world, job->id, job->rank, &cfg);
+            job->comm = comm;
+            job->r = r;
+            job->done.store(1, std::memory_order_release);
+            if (job->abandoned.load(std::memory_order_acquire)) {  // the caller gave up: nobody owns it
+                if (comm) (void)ncclCommAbort(comm);
+            }
+        }).detach();
+    } catch (...) {
+        delete job;
+        snprintf(c->err, sizeof c->err, "RCCL init: cannot start its thread");
+        return -3;
+    }
+    const double t_end = mono_s() + c->rccl_timeout_s;
+    while (!job->done.load(std::memory_order_acquire) && mono_s() < t_end) usleep(200);
+    if (!job->done.load(std::memory_order_acquire)) {
+        job->abandoned.store(1, std::memory_order_release);
+        snprintf(c->err, sizeof c->err, "ncclCommInitRankConfig: no progress in %.0f s (RCCL communicator abandoned)",
+                 c->rccl_timeout_s);
+        fprintf(stderr, "lbfgs rank %d: %s\n", c->geo.rank, c->err);
+        c->rccl_hung = 1;
+        return -3;  // job stays with the thread (a race with a late completion costs one leaked job)
+    }
+    const ncclResult_t r = job->r;
+    ncclComm_t comm = job->comm;
+    delete job;
+    if (r != ncclSuccess) {
         snprintf(c->err, sizeof c->err, "ncclCommInitRankConfig: %s", ncclGetErrorString(r));
+        if (comm) (void)ncclCommAbort(comm);
         return -3;
     }
     c->comm = comm;
-    return rccl_settle(c, r, "ncclCommInitRankConfig");
+    return 0;
 }
 
 // A context created without an RCCL id (the mailboxes alone) takes a communicator afterwards

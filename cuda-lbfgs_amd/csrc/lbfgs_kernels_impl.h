@@ -2906,10 +2906,10 @@ struct lbk_ctx {
     unsigned long long* h_ck;
     int64_t vec_doubles;  // allocation per vector
     ncclComm_t comm;
-    // RCCL is driven non-blocking (ncclConfig_t::blocking = 0): its bootstrap, every enqueue and
-    // a host wait on an RCCL collective end after rccl_timeout_s (LBFGS_RCCL_TIMEOUT, 60 s) with
-    // the communicator aborted, never in a hang; rccl_hung: an aborted collective may still sit
-    // on the stream, which destroy then does not wait for
+    // RCCL waits are bounded: the communicator's init (on a helper thread), every enqueue and a
+    // host wait on an RCCL collective end after rccl_timeout_s (LBFGS_RCCL_TIMEOUT, 60 s) with the
+    // communicator abandoned or aborted, never in a hang; rccl_hung: an aborted collective may
+    // still sit on the stream, which destroy then does not wait for
     double rccl_timeout_s;
     int rccl_hung;
     char err[256];

@@ -209,10 +209,11 @@ int lbfgs_peer_connect(lbfgs_ctx* ctx, const void* handles /* world x LBFGS_PEER
  * to the RCCL communicator (LBFGS_ERR_STATE without one). Every rank must make the same choice. */
 int lbfgs_peer_enable(lbfgs_ctx* ctx, int on);
 /* A sharded context created without a unique_id takes an RCCL communicator afterwards (every rank
- * calls it with the same id). Every RCCL communicator of the library is created non-blocking and
- * waited for with a bound (LBFGS_RCCL_TIMEOUT seconds, default 60), and so are the host's waits on
- * its collectives: a rank that never joins, a stalled bootstrap or a collective that does not
- * complete returns LBFGS_ERR_RCCL with the communicator aborted, never a hang. This call also runs
+ * calls it with the same id). Every RCCL communicator of the library is created on a helper thread
+ * and waited for with a bound (LBFGS_RCCL_TIMEOUT seconds, default 60), and so are the host's waits
+ * on its collectives: a rank that never joins, a stalled bootstrap or a collective that does not
+ * complete returns LBFGS_ERR_RCCL (the stalled init thread abandoned, a stalled collective's
+ * communicator aborted), never a hang. This call also runs
  * one all-gather through the new communicator under the same bound. Exchanges stay on the
  * mailboxes until lbfgs_peer_enable(ctx, 0). */
 int lbfgs_rccl_attach(lbfgs_ctx* ctx, const void* unique_id /* 128 bytes, lbfgs_unique_id */);

@@ -143,7 +143,7 @@ def test_config4_n1e9_8_processes_cu_partitioned(tmp_path):
     iters = 13  # the history fill (h reaches m = 10) and 3 steps with the ring full
     outs = run_ranks(tmp_path, 8, N9, 10, "rosenbrock", "backtracking", iters, "steps",
                      env={"LBFGS_CU_PARTITION": "1"},
-                     unset=("LBFGS_TICKET", "LBFGS_XGMI_MIRROR", "LBFGS_XGMI_FOLD"), timeout=900)
+                     unset=("LBFGS_TICKET", "LBFGS_XGMI_FOLD"), timeout=900)
     x0 = L.x0_uniform(N9, 42, -2.0, 2.0)
     with L.Context(N9, 10) as c:
         c.init("rosenbrock", x0, "backtracking", tolerance=1e-5, trace=True)
@@ -195,7 +195,7 @@ def test_config4_mailboxes_8_processes(tmp_path, ls, mode, fold):
     # the library's own stage-2 and mirror choices, as bench.py runs it
     outs = run_ranks(tmp_path, 8, N4, 10, "rosenbrock", ls, iters, mode,
                      env={"LBFGS_XGMI_FOLD": "2"} if fold == "2" else None,
-                     unset=("LBFGS_TICKET", "LBFGS_XGMI_MIRROR", "LBFGS_XGMI_FOLD"))
+                     unset=("LBFGS_TICKET", "LBFGS_XGMI_FOLD"))
     assert all(bool(o["folded"]) == (fold == "2") for o in outs)
     x = np.zeros(N4)
     for r, o in enumerate(outs):

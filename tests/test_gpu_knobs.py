@@ -22,10 +22,15 @@ import lbfgs_amd as L  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 
+# every switch of the shipped library that changes how a one-rank solve runs;
+# the sharded ones (LBFGS_XGMI_FOLD, LBFGS_CU_PARTITION, the time-outs of the exchanges) are
+# covered by tests/test_gpu_xgmi.py and tests/test_gpu_rccl.py, the transfer paths (LBFGS_XFER)
+# by tests/test_gpu_xfer.py. A/B forms measured slower are compiled into variant builds only
+# (tools/build_variant.sh: LBK_PERSIST_ITER, LBK_SMALL_SEGS, LBK_XGMI_MIRROR, LBK_PERSIST_STRIDE,
+# LBK_PERSIST_ALT, LBK_PERSIST_LDS; the q/r ping-pong was removed).
 KNOBS = ["LBFGS_TICKET", "LBFGS_DEFER", "LBFGS_REV", "LBFGS_NT", "LBFGS_DIRECT", "LBFGS_COOP",
-         "LBFGS_PERSIST", "LBFGS_PINGPONG", "LBFGS_SPEC", "LBFGS_BATCH", "LBFGS_SMALL_SEGS",
-         "LBFGS_PERSIST_WG", "LBFGS_PERSIST_OWN", "LBFGS_PERSIST_ALT", "LBFGS_PERSIST_LDS", "LBFGS_COLLECT",
-         "LBFGS_COLLECT_TIMEOUT", "LBFGS_DEV_WOLFE"]
+         "LBFGS_PERSIST", "LBFGS_SPEC", "LBFGS_BATCH", "LBFGS_PERSIST_WG", "LBFGS_COLLECT",
+         "LBFGS_COLLECT_TIMEOUT", "LBFGS_DEV_WOLFE", "LBFGS_SEARCH_TIMEOUT"]
 
 VARIANTS = {
     "ticket1": {"LBFGS_TICKET": "1"},
@@ -39,10 +44,8 @@ VARIANTS = {
     "coop0": {"LBFGS_COOP": "0"},
     "persist1_not_shipped": {"LBFGS_PERSIST": "1"},  # compiled out of the library: the default path runs
     "persist2": {"LBFGS_PERSIST": "2"},
-    "persist2_wg1_stride": {"LBFGS_PERSIST": "2", "LBFGS_PERSIST_WG": "1", "LBFGS_PERSIST_OWN": "stride"},
-    "persist2_alt0_lds0_nt1": {"LBFGS_PERSIST": "2", "LBFGS_PERSIST_ALT": "0", "LBFGS_PERSIST_LDS": "0",
-                               "LBFGS_NT": "1"},
-    "pingpong1": {"LBFGS_PINGPONG": "1"},
+    "persist2_wg1": {"LBFGS_PERSIST": "2", "LBFGS_PERSIST_WG": "1"},
+    "persist2_nt1": {"LBFGS_PERSIST": "2", "LBFGS_NT": "1"},
     "collect1": {"LBFGS_COLLECT": "1"},
     "collect1_rev0_nt1": {"LBFGS_COLLECT": "1", "LBFGS_REV": "0", "LBFGS_NT": "1"},
     "collect1_defer0_batch0": {"LBFGS_COLLECT": "1", "LBFGS_DEFER": "0", "LBFGS_BATCH": "0"},
@@ -50,14 +53,13 @@ VARIANTS = {
     "batch0": {"LBFGS_BATCH": "0"},
     "ticket1_direct0": {"LBFGS_TICKET": "1", "LBFGS_DIRECT": "0"},
     "ticket1_rev0_nt0": {"LBFGS_TICKET": "1", "LBFGS_REV": "0", "LBFGS_NT": "0"},
-    "ticket1_pingpong1": {"LBFGS_TICKET": "1", "LBFGS_PINGPONG": "1"},
     "persist2_coop0_nt1": {"LBFGS_PERSIST": "2", "LBFGS_COOP": "0", "LBFGS_NT": "1"},
     "collect_timeout": {"LBFGS_COLLECT": "1", "LBFGS_COLLECT_TIMEOUT": "30"},
-    "defer_all_rev0_pingpong1": {"LBFGS_DEFER": "8192", "LBFGS_TICKET": "0", "LBFGS_REV": "0",
-                                 "LBFGS_PINGPONG": "1"},
+    "defer_all_rev0": {"LBFGS_DEFER": "8192", "LBFGS_TICKET": "0", "LBFGS_REV": "0"},
     "coop0_spec0_batch0": {"LBFGS_COOP": "0", "LBFGS_SPEC": "0", "LBFGS_BATCH": "0"},
     "devwolfe0": {"LBFGS_DEV_WOLFE": "0"},
     "devwolfe0_spec0": {"LBFGS_DEV_WOLFE": "0", "LBFGS_SPEC": "0"},
+    "search_timeout0": {"LBFGS_SEARCH_TIMEOUT": "0"},  # the device search gives up, the host loop redoes it
 }
 
 CASES = [  # n, m, objective, line search, iterations

@@ -319,28 +319,6 @@ def test_sharded_emulated_bit_exact(world, obj, ls, ticket, monkeypatch):
 
 
 @pytest.mark.parametrize("n,m,ls", [(10_000, 5, "backtracking"), (30_001, 16, "wolfe"), (4097, 7, "interpolation"),
-                                    (20_000, 10, "backtracking_wolfe")])
-def test_small_persistent_iteration_bit_exact(monkeypatch, n, m, ls):
-    """The single-workgroup persistent iteration (small n: the whole two-loop and the commit at
-    a0 in one launch) against the multi-launch sequence (LBFGS_SMALL_SEGS=0) and the oracle:
-    identical bits, including every rejected-step recommit that reads its slots."""
-    x0 = L.x0_uniform(n, 3, -2.0, 2.0)
-    out = []
-    monkeypatch.setenv("LBFGS_COOP", "0")  # the single-workgroup form, not the cooperative one
-    for segs in ("0", "256"):
-        monkeypatch.setenv("LBFGS_SMALL_SEGS", segs)
-        with L.Context(n, m) as c:
-            out.append(c.minimize("rosenbrock", x0, ls, 60, trace=True))
-    a, b = out
-    assert b["passes"] < a["passes"]  # the persistent path really ran
-    for key in ("tr_f", "tr_gnorm", "x"):
-        assert np.array_equal(bits(a[key]), bits(b[key])), key
-    assert np.array_equal(a["tr_c1"], b["tr_c1"]) and a["messages"] == b["messages"]
-    o = O.lbfgs("rosenbrock", x0, ls, m, 60, 1e-5, mode=O.CANON)
-    assert np.array_equal(bits(b["tr_f"]), bits(o["f"]))
-
-
-@pytest.mark.parametrize("n,m,ls", [(10_000, 5, "backtracking"), (30_001, 16, "wolfe"), (4097, 7, "interpolation"),
                                     (20_000, 10, "backtracking_wolfe"), (32_768, 1, "backtracking"),
                                     (100_000, 10, "backtracking"), (200_001, 6, "wolfe")])
 def test_cooperative_iteration_bit_exact(monkeypatch, n, m, ls):

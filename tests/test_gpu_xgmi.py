@@ -55,14 +55,14 @@ def run_ranks(tmp_path, world, n, m, obj, ls, iters, mode, env=None, unset=(), t
     (8, "rosenbrock", "backtracking", "default", "1"),
     (8, "quad_tridiag", "wolfe", "vf", "0"),
 ])
-def test_xgmi_sharded_bit_exact(tmp_path, world, obj, ls, mode, ticket, mirror="0"):
+def test_xgmi_sharded_bit_exact(tmp_path, world, obj, ls, mode, ticket):
     n = 4_000_003  # every one of up to 8 ranks owns segments
     m, iters = 5, 12
     x0 = L.x0_uniform(n, 42, -2.0, 2.0)
     with L.Context(n, m) as c:
         ref = c.minimize(obj, x0, ls, iters, trace=True, vector_free=(mode == "vf"))
     outs = run_ranks(tmp_path, world, n, m, obj, ls, iters, mode,
-                     env={"LBFGS_TICKET": ticket, "LBFGS_XGMI_MIRROR": mirror})
+                     env={"LBFGS_TICKET": ticket})
     x = np.zeros(n)
     for r, o in enumerate(outs):
         for key in ("tr_f", "tr_gnorm", "tr_alpha"):
@@ -143,13 +143,6 @@ def test_xgmi_fold_off_on_a_shared_gpu(tmp_path):
     the peer's producing kernel waits for); the exchange kernel carries their reductions."""
     outs = run_ranks(tmp_path, 2, 4_000_003, 5, "rosenbrock", "backtracking", 3, "default", unset=("LBFGS_XGMI_FOLD",))
     assert not any(bool(o["folded"]) for o in outs)
-
-
-@pytest.mark.parametrize("mode,ls,ticket", [("default", "wolfe", "1"), ("vf", "interpolation", "0")])
-def test_xgmi_host_mirror_bit_exact(tmp_path, mode, ls, ticket):
-    """LBFGS_XGMI_MIRROR=1: the exchange kernel also fills the host mirror of the slots the host
-    reads (commit, trials, vector-free Gram rows), which the host then reads with no copy."""
-    test_xgmi_sharded_bit_exact(tmp_path, 4, "rosenbrock", ls, mode, ticket, mirror="1")
 
 
 def test_xgmi_soak_8_ranks_bit_exact(tmp_path):

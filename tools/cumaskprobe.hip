@@ -70,6 +70,14 @@ int main() {
         printf("world %d (%d CUs per rank):", world, per);
         for (int r = 0; r < world; ++r) printf(" rank%d=%zu", r, used[r].size());
         printf("  distinct over ranks %zu, CUs shared by two ranks %d\n", all.size(), overlap);
+        // which XCDs each rank's CUs sit on (CUs per XCC id): one XCD per rank, or spread over all 8
+        for (int r = 0; r < world; ++r) {
+            int per_xcc[16] = {0};
+            for (unsigned v : used[r]) per_xcc[(v >> 8) & 0xf]++;
+            printf("  rank%d CUs per XCC:", r);
+            for (int x = 0; x < 8; ++x) printf(" %d", per_xcc[x]);
+            printf("\n");
+        }
         if (overlap) bad = 1;
         for (int r = 0; r < world; ++r) {
             CK(hipFree(d[r]));
