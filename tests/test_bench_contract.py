@@ -164,3 +164,18 @@ def test_reference_parity_live_and_fixture(bench):
     assert p["first_divergent_k"] == m + 2 and p["within_tolerance_iterations"]["gnorm"] == m + 2 and p["ok"]
     p = bench.reference_parity(far, live, dict(fx2, horizons={"ref": [m + 3, m + 3]}), "fixture.json")
     assert not p["ok"]
+
+
+def test_fullsize_fixture_lookup(bench):
+    """the committed full-size fixture of a workload, or (None, None) at sizes without one; files
+    of other shapes (the CUDA-mode cases, with no single method) are passed over, not a KeyError
+    (bench.py --size 1.25e8 failed there in round 5)"""
+    import types
+
+    a = types.SimpleNamespace(objective="rosenbrock", history=10, line_search="backtracking")
+    d, src = bench.fullsize_fixture(a, 10 ** 8)
+    assert d is not None and src.endswith("config2_n1e8.json")
+    d, src = bench.fullsize_fixture(a, 10 ** 7)
+    assert d is not None and src.endswith("config1_n1e7.json")
+    assert bench.fullsize_fixture(a, 125_000_000) == (None, None)
+    assert bench.fullsize_fixture(a, 50_000_000) == (None, None)

@@ -5,8 +5,6 @@ set -o pipefail
 cd /root/repo && mkdir -p gpurun_out/r05b
 LIB=$PWD/cuda-lbfgs_amd
 B="python -u bench.py --size 1.25e8 --no-cpu-baseline --no-vector-free"
-timeout -k 10 60 tools/cumaskprobe > gpurun_out/r05b/cumaskprobe.txt 2>&1 &&
-timeout -k 10 120 tools/vfilprobe > gpurun_out/r05b/vfilprobe_n1e8.txt 2>&1 &&
 LBFGS_LIB=$LIB/liblbfgs_hip_seg122k.so LBFGS_TICKET=1 timeout -k 10 300 $B --steps 50 --warmup 3 > gpurun_out/r05b/rank_geo_fullgpu_ticket.json 2> gpurun_out/r05b/rank_geo_fullgpu_ticket.err &&
 LBFGS_LIB=$LIB/liblbfgs_hip_seg122k.so LBFGS_TICKET=0 timeout -k 10 300 $B --steps 50 --warmup 3 > gpurun_out/r05b/rank_geo_fullgpu_collect.json 2> gpurun_out/r05b/rank_geo_fullgpu_collect.err &&
 LBFGS_LIB=$LIB/liblbfgs_hip_seg122k_cuw8.so LBFGS_TICKET=1 timeout -k 10 300 $B --steps 50 --warmup 3 > gpurun_out/r05b/rank_geo_cu32_ticket.json 2> gpurun_out/r05b/rank_geo_cu32_ticket.err &&
