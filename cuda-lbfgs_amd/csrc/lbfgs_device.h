@@ -136,7 +136,7 @@ int lbk_exchange_bench(lbk_ctx* c, int backend, int ks, int iters, double* us);
 /* LBFGS_CU_PARTITION: CUs of this rank's solver stream (0: not partitioned) */
 int lbk_cu_partition(const lbk_ctx* c);
 /* the cooperative forms' grid caps (segments) and the device searches redone on the host loop */
-int lbk_coop_info(const lbk_ctx* c, int* coop_max, int* wolfe_max, int* fallbacks);
+int lbk_coop_info(const lbk_ctx* c, int* coop_max, int* search_max, int* fallbacks);
 /* box probe: `launches` back-to-back 3 R + 1 W streams over (q, y, s) in the two-loop passes'
  * geometry and cache policy, q written back unchanged; mean microseconds per launch */
 int lbk_stream_probe(lbk_ctx* c, double* q, const double* y, const double* s, int launches, double* us);
@@ -226,15 +226,37 @@ typedef struct {
     unsigned long long chain_epoch;
 } lbk_spec;
 int lbk_small_spec_ok(const lbk_ctx* c, int h);
-/* small n, single rank: the Wolfe search (lbfgs_driver.c ls_wolfe) continued on the device from
- * search iteration iter0 in one cooperative launch (k_coop_wolfe); st = {alpha, alpha_lo, alpha_hi,
- * f_lo, dphi_lo, f_x, g.d, c1, c2, wolfe_interp_min, last step, its f, its g.d, have_last, first
- * trial step, its f, its g.d, have_first}; d materialised. out = {step, trial passes, last evaluated
- * step, its f, its g.d}. */
-int lbk_wolfe_dev_ok(const lbk_ctx* c, int obj);
-/* -6: the launch's grid barrier timed out (nothing stored); the device search is then off for the
- * context and the caller redoes the search on the host loop */
-int lbk_wolfe_dev(lbk_ctx* c, int obj, const double* x, const double* d, const double* st, int iter0, double* out);
+/* small n, single rank: a line search (lbfgs_driver.c ls_*, LBFGS_LS_* numbering) continued on
+ * the device from the top of one of its iterations, in one cooperative launch (k_coop_search),
+ * d materialised. The state is the host loop's: its constants, the values the host already holds
+ * (the commit's first trial, the backtracking commit's f at its next step, the last trial pass),
+ * and the loop variables; the launch evaluates at most LBK_SEARCH_PASSES trial passes and returns
+ * the state as the host loop would have left it - done with the step, or (pass budget spent) at
+ * the top of an iteration, for the host to continue. With a commit request and the search done at
+ * another step than the commit's first trial, the launch also commits at that step (the D_BUF
+ * commit of lbk_commit, cand 0, into cm->slot) and sets `committed`. */
+#define LBK_SEARCH_PASSES 20
+typedef struct {
+    double f_x, gd, c1, c2, amin, init, beta, tol; /* constants */
+    double spec_a, spec_f, spec_dphi;               /* the commit's first trial (have_spec) */
+    double cand_a, cand_f;                          /* backtracking: f at the next step (have_cand) */
+    double tc_a[LBK_TRIALS_NC], tc_f[LBK_TRIALS_NC], tc_dphi; /* the last trial pass: tc_n steps */
+    int have_spec, have_cand, tc_n, tc_dphi_ok;
+    double alpha, alpha_lo, alpha_hi, f_lo, dphi_lo, alpha_prev, f_prev; /* loop variables */
+    int iter;
+    int done, committed, passes_f, passes_fg; /* results */
+    double step;
+} lbk_search;
+typedef struct {
+    const double* g;
+    double *xn, *gn, *so, *yo;
+    int slot; /* < 0: no commit */
+} lbk_search_commit;
+int lbk_search_dev_ok(const lbk_ctx* c, int obj);
+/* -6: the launch's grid barrier timed out (nothing stored, st unchanged); the device search is then
+ * off for the context and the caller goes on with the host loop */
+int lbk_search_dev(lbk_ctx* c, int obj, int ls, const double* x, const double* d, lbk_search* st,
+                   const lbk_search_commit* cm);
 /* *epoch: the launch's id for lbk_small_fetch (0: not a cooperative host-mirrored launch) */
 int lbk_small_iter(lbk_ctx* c, int obj, int h, const double* g, double* q, double* r, const double* const* S,
                    const double* const* Y, const double* rho, double gamma, int p0_ref, double a0, const double* x,

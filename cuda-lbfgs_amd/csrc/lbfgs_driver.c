@@ -114,6 +114,12 @@ struct lbfgs_ctx {
     int tc_n, tc_dphi_ok;
     double tc_a[LBK_TRIALS_NC], tc_f[LBK_TRIALS_NC], tc_dphi;
     int trial_passes;
+    /* small n: the device-resident line search (lbk_search_dev) commits at the step it finds into
+     * this slot (-1: no commit requested); committed: it did, this iteration; recommit_a0: a
+     * launch that timed out may have left the first commit's outputs partly rewritten, so the
+     * commit is repeated even at the first trial's step */
+    int search_cslot, search_committed, recommit_a0;
+    int64_t search_launches, search_commits; /* since solver init (lbfgs_search_stats) */
     /* vector-free mode (LBFGS_FLAG_VECTOR_FREE): Gram matrix over the pair pool, indexed by
      * pool slot (P = m + 1): Gss[p][q] = s_p.s_q, Gsy[p][q] = s_p.y_q, Gyy[p][q] = y_p.y_q,
      * Gsg[p] = s_p.g, Gyg[p] = y_p.g (g = current gradient; |g|^2 is gg) */
@@ -260,6 +266,13 @@ int lbfgs_spec_stats(const lbfgs_ctx* c, int64_t* adopted, int64_t* dropped) {
     if (!c) return LBFGS_ERR_BAD_ARG;
     if (adopted) *adopted = c->sp_adopted;
     if (dropped) *dropped = c->sp_dropped;
+    return 0;
+}
+
+int lbfgs_search_stats(const lbfgs_ctx* c, int64_t* launches, int64_t* commits) {
+    if (!c) return LBFGS_ERR_BAD_ARG;
+    if (launches) *launches = c->search_launches;
+    if (commits) *commits = c->search_commits;
     return 0;
 }
 
@@ -804,11 +817,25 @@ static double quad_interp(double a0, double p0, double dp0, double p1) { /* :14-
     return a0 - 0.5 * dp0 * a0 * a0 / (p1 - p0 - dp0 * a0);
 }
 
+static int search_here(const lbfgs_ctx* c, double alpha, int need_g);
+static int search_device(lbfgs_ctx* c, double gd, lbk_search* st);
+
 /* line_search.cpp:19-30 (f(x) == f_current, g.d == gd: identical values, evaluated once) */
 static int ls_backtracking(lbfgs_ctx* c, double gd, double* out) {
     const lbfgs_constants* K = &c->K;
     double alpha = K->initial_step;
     for (;;) {
+        if (search_here(c, alpha, 0)) {
+            lbk_search st = {0};
+            st.alpha = alpha;
+            const int rc = search_device(c, gd, &st);
+            if (rc < 0) return rc;
+            if (rc == 0 && st.done) {
+                *out = st.step;
+                return 0;
+            }
+            if (rc == 0) alpha = st.alpha; /* its pass budget spent: on from there */
+        }
         double fx, ft;
         int rc = ls_fx(c, alpha, &fx); /* f(x) - f(x + alpha d), left operand first */
         if (!rc) rc = trial(c, alpha, 0, &ft, NULL);
@@ -826,6 +853,17 @@ static int ls_backtracking_wolfe(lbfgs_ctx* c, double gd, double* out) {
     const lbfgs_constants* K = &c->K;
     double alpha = K->initial_step;
     for (;;) {
+        if (search_here(c, alpha, 1)) {
+            lbk_search st = {0};
+            st.alpha = alpha;
+            const int rd = search_device(c, gd, &st);
+            if (rd < 0) return rd;
+            if (rd == 0 && st.done) {
+                *out = st.step;
+                return 0;
+            }
+            if (rd == 0) alpha = st.alpha;
+        }
         double fn, dphi, fx;
         int rc = trial(c, alpha, 1, &fn, &dphi);
         if (!rc) rc = ls_fx(c, 0.0, &fx);
@@ -851,7 +889,27 @@ static int ls_interpolation(lbfgs_ctx* c, double gd, double* out) {
     if (rc0) return rc0;
     double alpha = K->initial_step, alpha_prev = 0.0, f_prev = f_x;
     int it = 0;
-    while (it++ < 20) {
+    for (;;) {
+        if (search_here(c, alpha, 0)) { /* it: the counter before the loop's `it++ < 20` test */
+            lbk_search st = {0};
+            st.alpha = alpha;
+            st.alpha_prev = alpha_prev;
+            st.f_prev = f_prev;
+            st.iter = it;
+            const int rd = search_device(c, gd, &st);
+            if (rd < 0) return rd;
+            if (rd == 0 && st.done) {
+                *out = st.step;
+                return 0;
+            }
+            if (rd == 0) {
+                alpha = st.alpha;
+                alpha_prev = st.alpha_prev;
+                f_prev = st.f_prev;
+                it = st.iter;
+            }
+        }
+        if (!(it++ < 20)) break;
         double f_new;
         int rc = trial(c, alpha, 0, &f_new, NULL);
         if (rc) return rc;
@@ -884,44 +942,76 @@ static int ls_interpolation(lbfgs_ctx* c, double gd, double* out) {
     return 0;
 }
 
-/* Small n (single rank, a cooperative size, device objective): once the Wolfe search needs a
- * trial pass, the rest of the search runs on the device in one launch (lbk_wolfe_dev: the same
- * loop, the same expressions, the same passes) instead of a launch and a host
- * round trip per trial. The step and every counter come back as the host loop would leave them.
- * Returns 1 when the launch's grid barrier timed out: it stored nothing, so the host loop takes
- * the search over from the same state (and the device form is off for the context). */
-static int wolfe_on_device(const lbfgs_ctx* c, double alpha) {
-    if (ext_obj(c) || c->unfused || !c->batch || c->vf || !lbk_wolfe_dev_ok(c->dev, c->obj)) return 0;
+/* Small n (single rank, a cooperative size, device objective): once a line search needs a trial
+ * pass, the rest of the search runs on the device in one launch (lbk_search_dev: the same loop,
+ * the same expressions, the same passes and caches) instead of a launch and a host
+ * round trip per trial pass, and the commit at the step it finds follows in the same launch.
+ * search_here: trial(alpha, need_g) would launch a pass, and the device form applies. */
+static int search_here(const lbfgs_ctx* c, double alpha, int need_g) {
+    if (ext_obj(c) || c->unfused || !c->batch || c->vf || !lbk_search_dev_ok(c->dev, c->obj)) return 0;
     if (c->spec_valid && alpha == c->a0) return 0; /* the commit's first trial: no pass */
-    if (c->tc_n >= 1 && c->tc_dphi_ok && alpha == c->tc_a[0]) return 0; /* the last pass */
+    if (!need_g && c->cand_valid && alpha == c->cand_alpha) return 0;
+    for (int j = 0; j < c->tc_n; ++j) /* the last trial pass */
+        if (alpha == c->tc_a[j] && (!need_g || (j == 0 && c->tc_dphi_ok))) return 0;
     return 1;
 }
 
-static int wolfe_device(lbfgs_ctx* c, int iter, double alpha, double alpha_lo, double alpha_hi, double f_lo,
-                        double dphi_lo, double f_x, double gd, double* out) {
+/* st: the caller's loop variables at the top of an iteration (alpha, and the search's own); the
+ * constants and the host's caches are filled in here, and the caches come back as the host loop
+ * would leave them. Returns 0 (st->done: the step; else the loop variables to go on from), 1 when
+ * the launch's grid barrier timed out (nothing usable came back: the host loop goes on from the
+ * same state, and the device form is off for the context), or < 0. */
+static int search_device(lbfgs_ctx* c, double gd, lbk_search* st) {
     const lbfgs_constants* K = &c->K;
     int rc = materialize_d(c);
     if (rc) return rc;
-    const int last = c->tc_n >= 1 && c->tc_dphi_ok;
-    const double st[18] = {alpha, alpha_lo, alpha_hi, f_lo, dphi_lo, f_x, gd, K->c1, K->c2, K->wolfe_interp_min,
-                           last ? c->tc_a[0] : 0.0, last ? c->tc_f[0] : 0.0, last ? c->tc_dphi : 0.0, last ? 1.0 : 0.0,
-                           c->a0, c->spec_f, c->spec_dphi, c->spec_valid ? 1.0 : 0.0};
-    double o[5];
-    rc = lbk_wolfe_dev(c->dev, c->obj, c->x, c->d, st, iter, o);
-    if (rc == -6) return 1; /* the launch's grid barrier timed out, nothing stored: the host loop goes on */
+    st->f_x = c->f_cur; /* ls_fx for a device objective */
+    st->gd = gd;
+    st->c1 = K->c1;
+    st->c2 = K->c2;
+    st->amin = K->wolfe_interp_min;
+    st->init = K->initial_step;
+    st->beta = K->backtracking_alpha;
+    st->tol = K->backtracking_tol;
+    st->have_spec = c->spec_valid;
+    st->spec_a = c->a0;
+    st->spec_f = c->spec_f;
+    st->spec_dphi = c->spec_dphi;
+    st->have_cand = c->cand_valid;
+    st->cand_a = c->cand_alpha;
+    st->cand_f = c->cand_f;
+    st->tc_n = c->tc_n;
+    st->tc_dphi_ok = c->tc_dphi_ok;
+    st->tc_dphi = c->tc_dphi;
+    for (int j = 0; j < LBK_TRIALS_NC; ++j) {
+        st->tc_a[j] = c->tc_a[j];
+        st->tc_f[j] = c->tc_f[j];
+    }
+    lbk_search_commit cm = {c->g, c->xn, c->gn, c->S[c->free_pair], c->Y[c->free_pair], c->search_cslot};
+    rc = lbk_search_dev(c->dev, c->obj, c->ls, c->x, c->d, st, &cm);
+    if (rc == -6) { /* barrier time-out: the host loop takes over */
+        if (cm.slot >= 0) c->recommit_a0 = 1;
+        return 1;
+    }
     if (rc) return dev_err(c, rc);
-    const int passes = (int)o[1];
-    c->trials_fg += passes;
+    const int passes = st->passes_f + st->passes_fg;
+    c->trials_f += st->passes_f;
+    c->trials_fg += st->passes_fg;
     c->trial_passes += passes;
     c->passes += passes;
-    if (passes > 0) { /* the host's cache of the last trial pass, as the host loop leaves it */
-        c->tc_n = 1;
-        c->tc_a[0] = o[2];
-        c->tc_f[0] = o[3];
-        c->tc_dphi = o[4];
-        c->tc_dphi_ok = 1;
+    c->tc_n = st->tc_n;
+    c->tc_dphi_ok = st->tc_dphi_ok;
+    c->tc_dphi = st->tc_dphi;
+    for (int j = 0; j < LBK_TRIALS_NC; ++j) {
+        c->tc_a[j] = st->tc_a[j];
+        c->tc_f[j] = st->tc_f[j];
     }
-    *out = o[0];
+    c->search_launches++;
+    if (st->committed) {
+        c->search_committed = 1;
+        c->search_commits++;
+        c->passes++;
+    }
     return 0;
 }
 
@@ -934,11 +1024,32 @@ static int ls_wolfe(lbfgs_ctx* c, double gd, double* out) {
     double alpha = K->initial_step;
     double alpha_lo = 0.0, alpha_hi = INFINITY, f_lo = f_x, dphi_lo = gd;
     for (int iter = 0; iter < 20; ++iter) {
-        if (wolfe_on_device(c, alpha)) {
-            const int rc = wolfe_device(c, iter, alpha, alpha_lo, alpha_hi, f_lo, dphi_lo, f_x, gd, out);
-            if (rc <= 0) return rc;
-            /* 1: the device search gave up (a grid barrier timed out) having changed nothing; it is
-             * off for this context now, and this iteration of the host loop runs as it would have */
+        if (search_here(c, alpha, 0)) {
+            lbk_search st = {0};
+            st.alpha = alpha;
+            st.alpha_lo = alpha_lo;
+            st.alpha_hi = alpha_hi;
+            st.f_lo = f_lo;
+            st.dphi_lo = dphi_lo;
+            st.iter = iter;
+            const int rd = search_device(c, gd, &st);
+            if (rd < 0) return rd;
+            if (rd == 0 && st.done) {
+                *out = st.step;
+                return 0;
+            }
+            /* rd == 1: the device search gave up (a grid barrier timed out) having changed nothing;
+             * it is off for this context now, and this iteration of the host loop runs as it
+             * would have. rd == 0, not done (its pass budget spent; 20 passes cover the 20
+             * iterations, so not expected): on from its state */
+            if (rd == 0) {
+                alpha = st.alpha;
+                alpha_lo = st.alpha_lo;
+                alpha_hi = st.alpha_hi;
+                f_lo = st.f_lo;
+                dphi_lo = st.dphi_lo;
+                iter = st.iter;
+            }
         }
         double f_new, dphi_new;
         /* f first; the gradient only if the sufficient-decrease tests pass (:144-153) */
@@ -1455,12 +1566,29 @@ static int iterate(lbfgs_ctx* c) {
     }
 
     double alpha = 0.0;
+    c->search_cslot = (!ext_obj(c) && !c->unfused) ? cslot : -1; /* a device search may commit */
+    c->search_committed = 0;
+    c->recommit_a0 = 0;
     rc = run_line_search(c, gd, &alpha);
+    c->search_cslot = -1;
     if (rc) return rc;
     if (c->flags & LBFGS_FLAG_TRACE) c->tr_a[c->tr_len - 1] = alpha;
 
     /* ---- commit (:159-198) ---- */
-    if (!(c->spec_valid && alpha == c->a0)) {
+    if (c->search_committed) {
+        /* the device search's launch committed at its step already (the commit below, D_BUF):
+         * its totals, then iteration k + 1 queued behind it as commit_queued would */
+        if (small_done && c->spec_on) {
+            rc = spec_drop(c);
+            if (rc) return rc;
+        }
+        DEVNC(lbk_fetch(c->dev, cslot, 7, tot));
+        c->commits++;
+        if (small_done && c->spec_on && alpha >= 1e-10) {
+            rc = spec_next(c, alpha);
+            if (rc) return rc;
+        }
+    } else if (!(c->spec_valid && alpha == c->a0) || c->recommit_a0) {
         /* batched: d may still be unmaterialised (formed on the fly again, same bits) */
         if (!(c->batch && !c->unfused && !ext_obj(c) && !c->d_ready &&
               (c->dmode == LBK_D_TWOLOOP || (c->dmode == LBK_D_NEG_G && c->geo->world == 1)))) {
@@ -2236,6 +2364,7 @@ int lbfgs_solver_init(lbfgs_ctx* c, int objective, const lbfgs_host_fn* cb, int 
     c->cur_epoch = 0;
     c->cur_spec = 0;
     c->sp_adopted = c->sp_dropped = 0;
+    c->search_launches = c->search_commits = 0;
     c->unfused = (flags & LBFGS_FLAG_UNFUSED) != 0;
     c->batch = 1;
     {
@@ -2580,6 +2709,7 @@ int lbfgs_line_search(lbfgs_ctx* c, int objective, const lbfgs_host_fn* cb, int 
     c->dmode = LBK_D_BUF;
     c->d_ready = 1;
     c->spec_valid = 0;
+    c->search_cslot = -1;
     host_invalidate(c);
     c->hxx_valid = 0;
     double alpha = 0.0;

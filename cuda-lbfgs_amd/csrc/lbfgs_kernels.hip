@@ -135,10 +135,12 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
     // 342 (7e5) deferred leads 5.07k to 4.81k (profiles/r02/small_n/coop_limit_ab.txt)
     c->coop_max = 256;
     if (const char* e = getenv("LBFGS_COOP")) c->coop_max = std::min(atoi(e), LBK_COOP_SEGMAX);  // max segments
-    // small n, Wolfe search: the trials after the commit's first one in one cooperative launch
-    // (k_coop_wolfe) instead of a launch and a host round trip each; LBFGS_DEV_WOLFE=0: host loop
+    // small n, every line search: the trials after the commit's first one, and the recommit at the
+    // step found, in one cooperative launch (k_coop_search) instead of a launch and a host round
+    // trip each; LBFGS_DEV_SEARCH=0: the host loop (LBFGS_DEV_WOLFE, its round-4 name, is read too)
     c->dev_wolfe = 1;
     if (const char* e = getenv("LBFGS_DEV_WOLFE")) c->dev_wolfe = atoi(e) != 0;
+    if (const char* e = getenv("LBFGS_DEV_SEARCH")) c->dev_wolfe = atoi(e) != 0;
     // the device search's wait at each grid barrier (2 s; tests set 0 to force its time-out path,
     // after which the host loop redoes the search)
     c->search_timeout_s = 2.0;
@@ -258,8 +260,8 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
         CK(hipMalloc(&c->wolfe_ll, llb));
         CK(hipMemset(c->wolfe_ll, 0, llb));
     }
-    CK(hipHostMalloc((void**)&c->wolfe_out_h, sizeof(double) * 8, hipHostMallocMapped | hipHostMallocCoherent));
-    memset(c->wolfe_out_h, 0, sizeof(double) * 8);
+    CK(hipHostMalloc((void**)&c->wolfe_out_h, sizeof(lbk_search), hipHostMallocMapped | hipHostMallocCoherent));
+    memset(c->wolfe_out_h, 0, sizeof(lbk_search));
     CK(hipHostGetDevicePointer((void**)&c->wolfe_out_d, c->wolfe_out_h, 0));
     {
         const size_t llb = sizeof(unsigned long long) * 2 * LBK_KMAX * LBK_SEGS;  // regular slots only
@@ -293,15 +295,23 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
         occ = std::min(occ, o);
         if (c->cu_part) cus = c->cu_count;  // the stream sees only its own CUs
         c->coop_max = (int)std::min<int64_t>(c->coop_max, (int64_t)occ * cus);
-        // the device-resident Wolfe search has a grid barrier of its own: its own occupancy caps it
-        // (a register footprint above k_coop_iter's would otherwise over-commit the grid)
+        // the device-resident line searches have grid barriers of their own: their own occupancy caps
+        // them (a register footprint above k_coop_iter's would otherwise over-commit the
+        // grid)
         int wocc = 1 << 30;
-        CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, k_coop_wolfe<LBK_OBJ_ROSENBROCK>, LB_BLOCK, 0));
-        wocc = std::min(wocc, o);
-        CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, k_coop_wolfe<LBK_OBJ_QUAD_TRIDIAG>, LB_BLOCK, 0));
-        wocc = std::min(wocc, o);
-        CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, k_coop_wolfe<LBK_OBJ_QUAD_SEPARABLE>, LB_BLOCK, 0));
-        wocc = std::min(wocc, o);
+#define SEARCH_OCC(O)                                                                                   \
+    CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, (k_coop_search<O, 0>), LB_BLOCK, 0));           \
+    wocc = std::min(wocc, o);                                                                           \
+    CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, (k_coop_search<O, 1>), LB_BLOCK, 0));           \
+    wocc = std::min(wocc, o);                                                                           \
+    CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, (k_coop_search<O, 2>), LB_BLOCK, 0));           \
+    wocc = std::min(wocc, o);                                                                           \
+    CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, (k_coop_search<O, 3>), LB_BLOCK, 0));           \
+    wocc = std::min(wocc, o);
+        SEARCH_OCC(LBK_OBJ_ROSENBROCK)
+        SEARCH_OCC(LBK_OBJ_QUAD_TRIDIAG)
+        SEARCH_OCC(LBK_OBJ_QUAD_SEPARABLE)
+#undef SEARCH_OCC
         c->wolfe_max = (int)std::min<int64_t>(c->coop_max, (int64_t)wocc * cus);
         // the persistent forms: every workgroup of their grid resident, at most `cap` per CU (the
         // occupancy answer is VGPR-bound here, where the API and the hardware agree;
@@ -1121,14 +1131,15 @@ int lbk_small_spec_ok(const lbk_ctx* c, int h) {
     return lbk_small_ok(c, h) && c->direct && c->coop_max > 0 && c->geo.nseg <= c->coop_max;
 }
 
-int lbk_wolfe_dev_ok(const lbk_ctx* c, int obj) {
+int lbk_search_dev_ok(const lbk_ctx* c, int obj) {
     return c->dev_wolfe && c->geo.world == 1 && !c->comm && c->wolfe_max > 0 && c->geo.nseg <= c->wolfe_max &&
            (obj == LBK_OBJ_ROSENBROCK || obj == LBK_OBJ_QUAD_TRIDIAG || obj == LBK_OBJ_QUAD_SEPARABLE);
 }
 
-int lbk_wolfe_dev(lbk_ctx* c, int obj, const double* x, const double* d, const double* st, int iter0, double* out) {
-    if (!lbk_wolfe_dev_ok(c, obj)) {
-        snprintf(c->err, sizeof c->err, "lbk_wolfe_dev: not a single-rank cooperative size");
+int lbk_search_dev(lbk_ctx* c, int obj, int ls, const double* x, const double* d, lbk_search* st,
+                   const lbk_search_commit* cm) {
+    if (!lbk_search_dev_ok(c, obj) || ls < 0 || ls > 3 || (cm && cm->slot >= 0 && (cm->slot >= LBK_NSLOTS || !cm->g))) {
+        snprintf(c->err, sizeof c->err, "lbk_search_dev: not a single-rank cooperative size (or bad arguments)");
         return -1;
     }
     SmallArgs a;
@@ -1137,52 +1148,63 @@ int lbk_wolfe_dev(lbk_ctx* c, int obj, const double* x, const double* d, const d
     a.seq_base = (unsigned)c->wolfe_seq;
     a.err = c->coop_err_d;
     a.timeout = (unsigned long long)(c->search_timeout_s * c->wall_khz * 1e3);  // 2 s per barrier
-    c->wolfe_seq += 20;                                                        // at most 20 trial passes
-    WolfeDev w;
-    w.alpha = st[0];
-    w.alpha_lo = st[1];
-    w.alpha_hi = st[2];
-    w.f_lo = st[3];
-    w.dphi_lo = st[4];
-    w.f_x = st[5];
-    w.gd = st[6];
-    w.c1 = st[7];
-    w.c2 = st[8];
-    w.amin = st[9];
-    w.last_a = st[10];
-    w.last_f = st[11];
-    w.last_dphi = st[12];
-    w.have_last = st[13] != 0.0;
-    w.spec_a = st[14];
-    w.spec_f = st[15];
-    w.spec_dphi = st[16];
-    w.have_spec = st[17] != 0.0;
-    w.iter0 = iter0;
+    c->wolfe_seq += LBK_SEARCH_PASSES + 1;                                     // trial passes + the commit
+    SearchCommit k;
+    memset(&k, 0, sizeof k);
+    const bool commit = cm && cm->slot >= 0;
+    if (commit) {
+        k.g = cm->g;
+        k.xn = cm->xn;
+        k.gn = cm->gn;
+        k.so = cm->so;
+        k.yo = cm->yo;
+        k.slot = c->slots + (int64_t)cm->slot * LBK_SLOT;
+        k.hslot = c->direct ? c->dh_slots + (int64_t)cm->slot * LBK_SLOT : nullptr;
+    }
+    lbk_search s = *st;
+    s.done = s.committed = s.passes_f = s.passes_fg = 0;
     Geo geo = kgeo(c);
     geo.rev = 0;
     const int nb = (int)c->geo.nseg;
-    double* o = c->wolfe_out_d;
+    lbk_search* o = c->wolfe_out_d;
     const int rc = launch(c, LBK_K_TRIAL_FG, 0.0, -1, [&] {
+#define SEARCH_LAUNCH(O)                                                                                                   \
+    switch (ls) {                                                                                                          \
+        case 0: hipLaunchKernelGGL((k_coop_search<O, 0>), dim3(nb), dim3(LB_BLOCK), 0, c->stream, a, geo, s, x, d, k, o); break; \
+        case 1: hipLaunchKernelGGL((k_coop_search<O, 1>), dim3(nb), dim3(LB_BLOCK), 0, c->stream, a, geo, s, x, d, k, o); break; \
+        case 2: hipLaunchKernelGGL((k_coop_search<O, 2>), dim3(nb), dim3(LB_BLOCK), 0, c->stream, a, geo, s, x, d, k, o); break; \
+        default: hipLaunchKernelGGL((k_coop_search<O, 3>), dim3(nb), dim3(LB_BLOCK), 0, c->stream, a, geo, s, x, d, k, o); break; \
+    }
         switch (obj) {
-            case LBK_OBJ_ROSENBROCK: hipLaunchKernelGGL(k_coop_wolfe<LBK_OBJ_ROSENBROCK>, dim3(nb), dim3(LB_BLOCK), 0, c->stream, a, geo, w, x, d, o); break;
-            case LBK_OBJ_QUAD_TRIDIAG: hipLaunchKernelGGL(k_coop_wolfe<LBK_OBJ_QUAD_TRIDIAG>, dim3(nb), dim3(LB_BLOCK), 0, c->stream, a, geo, w, x, d, o); break;
-            default: hipLaunchKernelGGL(k_coop_wolfe<LBK_OBJ_QUAD_SEPARABLE>, dim3(nb), dim3(LB_BLOCK), 0, c->stream, a, geo, w, x, d, o); break;
+            case LBK_OBJ_ROSENBROCK: SEARCH_LAUNCH(LBK_OBJ_ROSENBROCK) break;
+            case LBK_OBJ_QUAD_TRIDIAG: SEARCH_LAUNCH(LBK_OBJ_QUAD_TRIDIAG) break;
+            default: SEARCH_LAUNCH(LBK_OBJ_QUAD_SEPARABLE) break;
         }
+#undef SEARCH_LAUNCH
     });
     if (rc) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (*(volatile unsigned*)c->coop_err_h) {
         // the grid was not resident together (or a barrier waited past its bound): every workgroup
-        // has left the launch, which stored no vector, so the caller redoes the search on the host
-        // loop from the same state; the device form stays off for this context
+        // has left the launch, which stored no vector (the commit pass comes after every trial
+        // pass's barrier), so the caller goes on with the host loop from the same state; the device
+        // form stays off for this context
         *(volatile unsigned*)c->coop_err_h = 0;
         c->dev_wolfe = 0;
         c->coop_fallbacks++;
-        snprintf(c->err, sizeof c->err, "device Wolfe search: grid barrier timed out (search redone on the host loop)");
+        snprintf(c->err, sizeof c->err, "device line search: grid barrier timed out (search redone on the host loop)");
         return -6;
     }
-    for (int k = 0; k < 5; ++k) out[k] = ((volatile double*)c->wolfe_out_h)[k];
-    c->bytes_total += out[1] * 2.0 * 8.0 * (double)c->geo.n_loc;  // x and d per trial pass
+    lbk_search r;
+    memcpy(&r, (const void*)c->wolfe_out_h, sizeof r);
+    *st = r;
+    // x and d per trial pass; the commit's x, g, d in and x', g', s, y out
+    c->bytes_total += (double)(r.passes_f + r.passes_fg) * 2.0 * 8.0 * (double)c->geo.n_loc;
+    if (r.committed) {
+        c->bytes_total += 7.0 * 8.0 * (double)c->geo.n_loc;
+        c->slot_mirror[cm->slot] = c->direct ? 1 : 0;
+        c->slot_s2[cm->slot] = 0;
+    }
     return 0;
 }
 
@@ -1466,9 +1488,9 @@ int lbk_peer_enable(lbk_ctx* c, int on) {
 
 int lbk_cu_partition(const lbk_ctx* c) { return c->cu_part ? c->cu_count : 0; }
 
-int lbk_coop_info(const lbk_ctx* c, int* coop_max, int* wolfe_max, int* fallbacks) {
+int lbk_coop_info(const lbk_ctx* c, int* coop_max, int* search_max, int* fallbacks) {
     if (coop_max) *coop_max = c->coop_max;
-    if (wolfe_max) *wolfe_max = c->dev_wolfe ? c->wolfe_max : 0;
+    if (search_max) *search_max = c->dev_wolfe ? c->wolfe_max : 0;
     if (fallbacks) *fallbacks = c->coop_fallbacks;
     return 0;
 }

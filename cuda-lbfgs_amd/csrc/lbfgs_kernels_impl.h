@@ -2436,23 +2436,28 @@ __global__ __launch_bounds__(LB_BLOCK) void k_coop_iter(SmallArgs a, Geo geo) {
 #undef SL
 
 // ---------------------------------------------------------------------------------------
-// Device-resident Wolfe search for small n (lbfgs_driver.c ls_wolfe,
-// line_search.cpp:125-189): once the host's search needs a trial pass, the rest of the search runs
-// in ONE cooperative launch - one workgroup per canonical segment, all resident, each trial a
-// grid-wide pass of f(x + a d) and g(x + a d) . d (OpTrials, the k_trials arithmetic) whose fixed-
-// order totals every workgroup forms (coop_pass), and the search's decisions restated on them in
-// every workgroup with the host's expressions (-ffp-contract=off on both sides; IEEE division and
-// square root), so all workgroups take the same branches and the step is the host's bit for bit.
-// A step equal to the last evaluated one, or to the first trial the commit took, is not evaluated
-// again (the host's caches). Its flagged partials have their own buffer and sequence numbers,
-// apart from the cooperative iteration's, whose counter a dropped speculative launch rolls back.
-// out: [step, passes, last evaluated step, its f, its g.d].
+// Device-resident line searches for small n (lbfgs_driver.c ls_backtracking,
+// ls_interpolation, ls_wolfe, ls_backtracking_wolfe = line_search.cpp:19-30, 57-121, 125-189,
+// 33-55): once the host's search needs a trial pass, the rest of the search runs in ONE cooperative
+// launch - one workgroup per canonical segment, all resident, each trial a grid-wide pass of the
+// k_trials arithmetic (the f-only searches: f at the host's batched halving chain of
+// LBK_TRIALS_NC steps; the Wolfe searches: f and g(x + a d) . d at one step) whose fixed-order
+// totals every workgroup forms (coop_pass), and the search's decisions restated on them in every
+// workgroup with the host's expressions (-ffp-contract=off on both sides; IEEE division and square
+// root), so all workgroups take the same branches and the step is the host's bit for bit. The
+// host's caches are restated too (the commit's first trial, the backtracking commit's f at the
+// next step, the last trial pass), so the launch evaluates exactly the passes the host loop would
+// and leaves the same cache behind. A search that ends at another step than the commit's first
+// trial is followed, in the same launch, by the commit at that step (the D_BUF commit of k_commit,
+// into the host-read commit slot): no second launch and no host round trip for the recommit.
+// Its flagged partials have their own buffer and sequence numbers, apart from the cooperative
+// iteration's, whose counter a dropped speculative launch rolls back.
 // ---------------------------------------------------------------------------------------
-struct WolfeDev {
-    double alpha, alpha_lo, alpha_hi, f_lo, dphi_lo, f_x, gd, c1, c2, amin;
-    double last_a, last_f, last_dphi;  // the last trial pass of this search (have_last)
-    double spec_a, spec_f, spec_dphi;  // the first trial, taken by the commit (have_spec)
-    int iter0, have_last, have_spec;
+struct SearchCommit {
+    const double* g;
+    double *xn, *gn, *so, *yo;
+    double* slot;   // device slot, or nullptr: no commit
+    double* hslot;  // its host mirror (direct fetch), or nullptr
 };
 
 __device__ __forceinline__ double wolfe_cubic(double a0, double a1, double p0, double dp0, double p1, double dp1) {
@@ -2460,75 +2465,204 @@ __device__ __forceinline__ double wolfe_cubic(double a0, double a1, double p0, d
     const double d2 = copysign(sqrt(d1 * d1 - dp0 * dp1), a1 - a0);
     return a0 + (a1 - a0) * (dp0 + d2 - d1) / (dp0 - dp1 + 2 * d2);
 }
+__device__ __forceinline__ double search_quad(double a0, double p0, double dp0, double p1) {  // :14-16
+    return a0 - 0.5 * dp0 * a0 * a0 / (p1 - p0 - dp0 * a0);
+}
 
-template <int OBJ>
-__global__ __launch_bounds__(LB_BLOCK) void k_coop_wolfe(SmallArgs a, Geo geo, WolfeDev w, const double* x,
-                                                         const double* d, double* out) {
+template <int OBJ, int LS>
+__global__ __launch_bounds__(LB_BLOCK) void k_coop_search(SmallArgs a, Geo geo, lbk_search s, const double* x,
+                                                          const double* d, SearchCommit cm, lbk_search* out) {
     __shared__ double lds[4][8];
     __shared__ double tl[8];
+    constexpr bool FG = LS == 2 || LS == 3;  // Wolfe searches: f and g.d per pass (want_dphi)
+    constexpr int NC = LBK_TRIALS_NC;
     DirArgs da = {d, nullptr, nullptr, 0.0, nullptr, nullptr, 0.0, nullptr, geo.g_lo, geo.g_hi};
-    double alpha = w.alpha, lo = w.alpha_lo, hi = w.alpha_hi, f_lo = w.f_lo, dphi_lo = w.dphi_lo;
-    double la = w.last_a, lf = w.last_f, ld = w.last_dphi;
-    int have = w.have_last, pass = 0, iter = w.iter0;
-    double res;
-    for (;;) {
-        if (iter >= 20) {
-            res = alpha;
-            break;
+    int pass = 0;
+    // lbfgs_driver.c trial() / trial_batched() for a device objective: the caches, else one pass;
+    // false: the launch's pass budget is spent (the state stays at the top of this iteration)
+    auto trial = [&](double alpha, bool need_g, double& f, double& dphi) -> bool {
+        if (s.have_spec && alpha == s.spec_a) {
+            f = s.spec_f;
+            dphi = s.spec_dphi;
+            return true;
         }
-        double f_new, dphi_new;
-        if (w.have_spec && alpha == w.spec_a) {
-            f_new = w.spec_f;
-            dphi_new = w.spec_dphi;
-        } else if (have && alpha == la) {
-            f_new = lf;
-            dphi_new = ld;
-        } else {
+        if (!need_g && s.have_cand && alpha == s.cand_a) {
+            f = s.cand_f;
+            return true;
+        }
+        for (int j = 0; j < s.tc_n; ++j)
+            if (alpha == s.tc_a[j] && (!need_g || (j == 0 && s.tc_dphi_ok))) {
+                f = s.tc_f[j];
+                dphi = s.tc_dphi;
+                return true;
+            }
+        if (pass >= LBK_SEARCH_PASSES) return false;
+        if (FG) {
             OpTrials<OBJ, LBK_D_BUF, 1, true, false> op{x, da, {alpha}, geo.n, geo.n_loc};
             double t[2];
             coop_pass<2>(op, geo, a, pass++, nullptr, nullptr, nullptr, t, lds, tl);
-            f_new = t[0];
-            dphi_new = t[1];
-            la = alpha;
-            lf = f_new;
-            ld = dphi_new;
-            have = 1;
-        }
-        if (f_new > w.f_x + w.c1 * alpha * w.gd || (f_new >= f_lo && iter > 0)) {
-            hi = alpha;
-            alpha = wolfe_cubic(lo, hi, f_lo, dphi_lo, f_new, (f_new - w.f_x - w.gd * alpha) / (alpha * alpha));
-            ++iter;
-            continue;
-        }
-        if (fabs(dphi_new) <= -w.c2 * w.gd) {
-            res = alpha;
-            break;
-        }
-        if (dphi_new >= 0) {
-            hi = alpha;
-            alpha = wolfe_cubic(lo, hi, f_lo, dphi_lo, f_new, dphi_new);
+            s.tc_n = 1;
+            s.tc_a[0] = alpha;
+            s.tc_f[0] = t[0];
+            s.tc_dphi = t[1];
+            s.tc_dphi_ok = 1;
+            s.passes_fg++;
+            f = t[0];
+            dphi = t[1];
         } else {
-            lo = alpha;
-            f_lo = f_new;
-            dphi_lo = dphi_new;
-            if (hi == INFINITY)
-                alpha *= 2;
-            else
+            const double ratio = LS == 0 ? s.beta : 0.5;  // the search's halving chain
+            OpTrials<OBJ, LBK_D_BUF, NC, false, false> op{x, da, {}, geo.n, geo.n_loc};
+            op.a[0] = alpha;
+#pragma unroll
+            for (int j = 1; j < NC; ++j) op.a[j] = op.a[j - 1] * ratio;
+            double t[NC];
+            coop_pass<NC>(op, geo, a, pass++, nullptr, nullptr, nullptr, t, lds, tl);
+            s.tc_n = NC;
+#pragma unroll
+            for (int j = 0; j < NC; ++j) {
+                s.tc_a[j] = op.a[j];
+                s.tc_f[j] = t[j];
+            }
+            s.tc_dphi = 0.0;
+            s.tc_dphi_ok = 0;
+            s.passes_f++;
+            f = t[0];
+        }
+        return true;
+    };
+    auto finish = [&](double step) {
+        s.done = 1;
+        s.step = step;
+    };
+    double alpha = s.alpha;
+    if (LS == 0) {  // ls_backtracking
+        for (;;) {
+            double ft, dd;
+            if (!trial(alpha, false, ft, dd)) break;
+            if (!(s.f_x - ft < s.c1 * alpha * s.gd)) {
+                finish(alpha);
+                break;
+            }
+            alpha *= s.beta;
+            if (alpha < s.tol) {
+                finish(alpha);
+                break;
+            }
+        }
+    } else if (LS == 1) {  // ls_interpolation (iter: the loop counter before its `it++ < 20` test)
+        double alpha_prev = s.alpha_prev, f_prev = s.f_prev;
+        int it = s.iter;
+        for (;;) {
+            if (!(it++ < 20)) {
+                finish(alpha);
+                break;
+            }
+            double f_new, dd;
+            if (!trial(alpha, false, f_new, dd)) {
+                --it;
+                break;
+            }
+            if (f_new <= s.f_x + s.c1 * alpha * s.gd) {
+                finish(alpha);
+                break;
+            }
+            if (alpha < s.amin) {
+                finish(s.amin);
+                break;
+            }
+            if (alpha_prev > 0) {
+                const double delta = alpha - alpha_prev;
+                if (fabs(delta) < 1e-10) {
+                    alpha *= 0.5;
+                } else {
+                    const double ga = (f_new - s.f_x - s.gd * alpha) / (alpha * alpha);
+                    alpha = wolfe_cubic(alpha_prev, alpha, f_prev, s.gd, f_new, ga);
+                    if (alpha < 0.1 * alpha_prev || alpha > 0.9 * alpha_prev) alpha = alpha_prev * 0.5;
+                }
+            } else {
+                alpha = search_quad(alpha, f_new, s.gd, s.f_x);
+                if (alpha < 0.1 * s.init || alpha > 0.9 * s.init) alpha = s.init * 0.5;
+            }
+            alpha_prev = alpha;
+            f_prev = f_new;
+        }
+        s.alpha_prev = alpha_prev;
+        s.f_prev = f_prev;
+        s.iter = it;
+    } else if (LS == 2) {  // ls_wolfe
+        double lo = s.alpha_lo, hi = s.alpha_hi, f_lo = s.f_lo, dphi_lo = s.dphi_lo;
+        int iter = s.iter;
+        for (;;) {
+            if (iter >= 20) {
+                finish(alpha);
+                break;
+            }
+            double f_new, dphi_new;
+            if (!trial(alpha, false, f_new, dphi_new)) break;
+            if (f_new > s.f_x + s.c1 * alpha * s.gd || (f_new >= f_lo && iter > 0)) {
+                hi = alpha;
+                alpha = wolfe_cubic(lo, hi, f_lo, dphi_lo, f_new, (f_new - s.f_x - s.gd * alpha) / (alpha * alpha));
+                ++iter;
+                continue;
+            }
+            trial(alpha, true, f_new, dphi_new);  // the same pass's g.d (cached: want_dphi)
+            if (fabs(dphi_new) <= -s.c2 * s.gd) {
+                finish(alpha);
+                break;
+            }
+            if (dphi_new >= 0) {
+                hi = alpha;
                 alpha = wolfe_cubic(lo, hi, f_lo, dphi_lo, f_new, dphi_new);
+            } else {
+                lo = alpha;
+                f_lo = f_new;
+                dphi_lo = dphi_new;
+                if (hi == INFINITY)
+                    alpha *= 2;
+                else
+                    alpha = wolfe_cubic(lo, hi, f_lo, dphi_lo, f_new, dphi_new);
+            }
+            if (alpha < s.amin) {
+                finish(s.amin);
+                break;
+            }
+            ++iter;
         }
-        if (alpha < w.amin) {
-            res = w.amin;
-            break;
+        s.alpha_lo = lo;
+        s.alpha_hi = hi;
+        s.f_lo = f_lo;
+        s.dphi_lo = dphi_lo;
+        s.iter = iter;
+    } else {  // ls_backtracking_wolfe
+        for (;;) {
+            double fn, dphi;
+            if (!trial(alpha, true, fn, dphi)) break;
+            if (fn > s.f_x + s.c1 * alpha * s.gd) {
+                alpha *= s.beta;
+            } else if (dphi < s.c2 * s.gd) {
+                alpha *= 1.1;
+            } else {
+                finish(alpha);
+                break;
+            }
+            if (alpha < s.tol) {
+                finish(alpha);
+                break;
+            }
         }
-        ++iter;
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        out[0] = res;
-        out[1] = (double)pass;
-        out[2] = la;
-        out[3] = lf;
-        out[4] = ld;
+    s.alpha = alpha;
+    // the commit at the decided step (lbfgs_driver.c commit(), D_BUF, cand 0), unless the commit
+    // already taken was at that step
+    if (s.done && cm.slot && !(s.have_spec && s.step == s.spec_a)) {
+        DirArgs dc = {d, nullptr, cm.g, 0.0, nullptr, nullptr, 0.0, nullptr, geo.g_lo, geo.g_hi};
+        double t7[7];
+        coop_pass<7>(OpCommit<OBJ, LBK_D_BUF, false>{x, dc, s.step, cm.xn, cm.gn, cm.so, cm.yo, geo.n, geo.n_loc,
+                                                      0.0},
+                     geo, a, pass++, cm.slot, cm.hslot, nullptr, t7, lds, tl);
+        s.committed = 1;
     }
+    if (blockIdx.x == 0 && threadIdx.x == 0) *out = s;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -2962,15 +3096,15 @@ struct lbk_ctx {
     unsigned long long coop_ll_bytes;
     unsigned long long* coop_ll;   // flagged partials (SmallArgs::ll)
     unsigned long long coop_base;  // passes tagged so far (the next launch's sequence base)
-    // device-resident Wolfe search (k_coop_wolfe, LBFGS_DEV_WOLFE): flagged partials and sequence
-    // numbers of its own (never rolled back), results in mapped host memory
+    // device-resident line searches (k_coop_search, LBFGS_DEV_SEARCH): flagged partials and sequence
+    // numbers of their own (never rolled back), the state in mapped host memory
     int dev_wolfe;
-    int wolfe_max;         // its grid cap: k_coop_wolfe's own occupancy x CUs (and coop_max)
+    int wolfe_max;         // their grid cap: k_coop_search's own occupancy x CUs (and coop_max)
     int coop_fallbacks;    // device searches redone on the host loop after a barrier time-out
     double search_timeout_s; // the device search's wait per grid barrier (LBFGS_SEARCH_TIMEOUT, 2 s)
     unsigned long long* wolfe_ll;
     unsigned long long wolfe_seq;
-    double *wolfe_out_h, *wolfe_out_d;
+    lbk_search *wolfe_out_h, *wolfe_out_d;
     unsigned* coop_err_h;          // pinned: barrier timeout
     unsigned* coop_err_d;
     double wall_khz;

@@ -120,6 +120,7 @@ def lib():
     L.lbfgs_exchange_fold.argtypes = [vp]
     L.lbfgs_exchange_latency.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_double)]
     L.lbfgs_spec_stats.argtypes = [vp, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
+    L.lbfgs_search_stats.argtypes = [vp, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
     L.lbfgs_cu_partition.argtypes = [vp]
     L.lbfgs_coop_info.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]
     L.lbfgs_stream_probe.argtypes = [vp, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double)]
@@ -144,7 +145,7 @@ EXPORTED_SYMBOLS = [
     "lbfgs_dev_twoloop", "lbfgs_dev_elementwise", "lbfgs_line_search", "lbfgs_prof_enable",
     "lbfgs_prof_reset", "lbfgs_prof_get", "lbfgs_peer_handle", "lbfgs_peer_connect", "lbfgs_peer_enable", "lbfgs_rccl_attach",
     "lbfgs_exchange_backend", "lbfgs_exchange_fold", "lbfgs_exchange_latency", "lbfgs_device_count", "lbfgs_set_dense_quadratic", "lbfgs_build_info",
-    "lbfgs_spec_stats", "lbfgs_cu_partition", "lbfgs_stream_probe", "lbfgs_coop_info",
+    "lbfgs_spec_stats", "lbfgs_cu_partition", "lbfgs_stream_probe", "lbfgs_coop_info", "lbfgs_search_stats",
 ]
 PEER_HANDLE_BYTES = 64
 BACKENDS = {0: "single", 1: "rccl", 2: "xgmi", 3: "host-group"}
@@ -281,6 +282,13 @@ class Context:
         since solver init (small n, cooperative iteration; LBFGS_SPEC=0: none)."""
         a, d = C.c_int64(), C.c_int64()
         lib().lbfgs_spec_stats(self.h, C.byref(a), C.byref(d))
+        return a.value, d.value
+
+    def search_stats(self):
+        """(launches, commits): line searches continued on the device since solver init, and the
+        commits those launches took at the step they found (small n; LBFGS_DEV_SEARCH=0: none)."""
+        a, d = C.c_int64(), C.c_int64()
+        lib().lbfgs_search_stats(self.h, C.byref(a), C.byref(d))
         return a.value, d.value
 
     def set_dense_quadratic(self, A, b):
@@ -508,6 +516,19 @@ class Context:
         if rc != 0:
             self._err("lbfgs_dev_trial", rc)
         return f.value, g, dphi.value
+
+    def line_search(self, objective, line_search, x, d, g, consts=None):
+        """lbfgs_line_search: the reference's free line-search functions (line_search.cpp) at x along
+        d with gradient g, device objective; returns the step"""
+        a = C.c_double()
+        k = consts if consts is not None else constants()
+        dp = lambda v: np.ascontiguousarray(v, np.float64).ctypes.data_as(C.POINTER(C.c_double))  # noqa: E731
+        xs, ds, gs = (np.ascontiguousarray(v, np.float64) for v in (x, d, g))
+        rc = lib().lbfgs_line_search(self.h, OBJECTIVES[objective], None, LINE_SEARCHES[line_search], C.byref(k),
+                                     dp(xs), dp(ds), dp(gs), C.byref(a))
+        if rc != 0:
+            self._err("lbfgs_line_search", rc)
+        return a.value
 
     def twoloop(self, g, S, Y):
         h = len(S)

@@ -177,6 +177,13 @@ const char* lbfgs_build_info(void);
  * LBFGS_SPEC=0 turns it off (bit-identical iterates either way). */
 int lbfgs_spec_stats(const lbfgs_ctx* c, int64_t* adopted, int64_t* dropped);
 
+/* Small n (one rank, a cooperative size, device objective): once a line search needs a trial pass
+ * beyond the commit's first one, the rest of the search - and the commit at the step it finds -
+ * runs in one cooperative launch instead of a launch and a host round trip per trial pass
+ * (DESIGN.md §4.3). Launches and commits taken that way since solver init. LBFGS_DEV_SEARCH=0
+ * turns it off (bit-identical iterates and counters either way). */
+int lbfgs_search_stats(const lbfgs_ctx* c, int64_t* launches, int64_t* commits);
+
 /* ---- context ---------------------------------------------------------------------------- */
 /* n: global problem size; m: history length (1..64); device: HIP device ordinal. */
 int lbfgs_ctx_create(lbfgs_ctx** out, int64_t n, int m, int device);
@@ -236,7 +243,7 @@ int lbfgs_exchange_latency(lbfgs_ctx* ctx, int backend, int components, int iter
 int lbfgs_cu_partition(const lbfgs_ctx* ctx);
 /* Diagnostic: the cooperative forms' grid caps in canonical segments, from each kernel's own
  * occupancy x the stream's CUs: *coop_max for the one-launch iteration (k_coop_iter), *search_max
- * for the device-resident line search (k_coop_wolfe; 0 when off); *fallbacks = device searches
+ * for the device-resident line searches (k_coop_search; 0 when off); *fallbacks = device searches
  * whose grid barrier timed out (LBFGS_SEARCH_TIMEOUT, 2 s) and that the host loop redid. */
 int lbfgs_coop_info(const lbfgs_ctx* ctx, int* coop_max, int* search_max, int* fallbacks);
 /* Diagnostic (no reference counterpart): `launches` back-to-back streams of 3 reads + 1 write

@@ -30,7 +30,7 @@ struct lbk_ctx {
      * product uses it for nseg <= its cooperative limit): launches run at once, in stream order */
     int small_on;
     int twoloop_on;
-    int wolfe_on; /* the device-resident Wolfe search (LBFGS_DEV_WOLFE, with the small-n form) */
+    int wolfe_on; /* the device-resident line searches (LBFGS_DEV_SEARCH, with the small-n form) */
     unsigned long long epoch, vd[4];
     int rec_went[4];
     double rec_rho[4], rec_gamma[4];
@@ -82,6 +82,8 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
     c->twoloop_on = e && atoi(e) != 0;
     e = getenv("LBFGS_DEV_WOLFE");
     c->wolfe_on = !e || atoi(e) != 0;
+    e = getenv("LBFGS_DEV_SEARCH");
+    if (e) c->wolfe_on = atoi(e) != 0;
     *out = c;
     return 0;
 }
@@ -490,8 +492,9 @@ int lbk_vf_ghost_init(lbk_ctx* c, double* x, double* g, int wslot) {
 }
 int lbk_small_ok(const lbk_ctx* c, int h) { return c->small_on && h >= 1 && h <= 16; }
 
-/* k_coop_wolfe's loop on this double's trial evaluation (lbk_trials, D_BUF, f and g.d) */
-int lbk_wolfe_dev_ok(const lbk_ctx* c, int obj) {
+/* k_coop_search's loops on this double's trial evaluation (lbk_trials, D_BUF: f at the halving
+ * chain, or f and g.d) and its commit (lbk_commit, D_BUF) */
+int lbk_search_dev_ok(const lbk_ctx* c, int obj) {
     return c->small_on && c->wolfe_on && obj >= 0 && obj <= LBK_OBJ_QUAD_SEPARABLE;
 }
 static double wolfe_cubic(double a0, double a1, double p0, double dp0, double p1, double dp1) {
@@ -499,69 +502,186 @@ static double wolfe_cubic(double a0, double a1, double p0, double dp0, double p1
     const double d2 = copysign(sqrt(d1 * d1 - dp0 * dp1), a1 - a0);
     return a0 + (a1 - a0) * (dp0 + d2 - d1) / (dp0 - dp1 + 2 * d2);
 }
-int lbk_wolfe_dev(lbk_ctx* c, int obj, const double* x, const double* d, const double* st, int iter0, double* out) {
-    if (!lbk_wolfe_dev_ok(c, obj)) return -1;
+/* 1: a value, 0: the pass budget is spent, -1: error */
+static int dbl_trial(lbk_ctx* c, int obj, int ls, const double* x, const double* d, lbk_search* s, int* pass,
+                     double alpha, int need_g, double* f, double* dphi) {
     const int slot = LBK_NSLOTS - 1; /* a slot the driver never names */
-    double alpha = st[0], lo = st[1], hi = st[2], f_lo = st[3], dphi_lo = st[4];
-    const double f_x = st[5], gd = st[6], c1 = st[7], c2 = st[8], amin = st[9];
-    double la = st[10], lf = st[11], ld = st[12], res;
-    int have = st[13] != 0.0, passes = 0, iter = iter0;
-    for (;;) {
-        if (iter >= 20) {
-            res = alpha;
-            break;
-        }
-        double f_new, dphi_new;
-        if (st[17] != 0.0 && alpha == st[14]) {
-            f_new = st[15];
-            dphi_new = st[16];
-        } else if (have && alpha == la) {
-            f_new = lf;
-            dphi_new = ld;
-        } else {
-            double t[2];
-            if (lbk_trials(c, obj, LBK_D_BUF, x, d, NULL, NULL, 0.0, -1, -1, &alpha, 1, 1, slot) != 0) return -1;
-            if (lbk_fetch(c, slot, 2, t) != 0) return -1;
-            passes++;
-            f_new = t[0];
-            dphi_new = t[1];
-            la = alpha;
-            lf = f_new;
-            ld = dphi_new;
-            have = 1;
-        }
-        if (f_new > f_x + c1 * alpha * gd || (f_new >= f_lo && iter > 0)) {
-            hi = alpha;
-            alpha = wolfe_cubic(lo, hi, f_lo, dphi_lo, f_new, (f_new - f_x - gd * alpha) / (alpha * alpha));
-            ++iter;
-            continue;
-        }
-        if (fabs(dphi_new) <= -c2 * gd) {
-            res = alpha;
-            break;
-        }
-        if (dphi_new >= 0) {
-            hi = alpha;
-            alpha = wolfe_cubic(lo, hi, f_lo, dphi_lo, f_new, dphi_new);
-        } else {
-            lo = alpha;
-            f_lo = f_new;
-            dphi_lo = dphi_new;
-            alpha = hi == INFINITY ? alpha * 2 : wolfe_cubic(lo, hi, f_lo, dphi_lo, f_new, dphi_new);
-        }
-        if (alpha < amin) {
-            res = amin;
-            break;
-        }
-        ++iter;
+    if (s->have_spec && alpha == s->spec_a) {
+        *f = s->spec_f;
+        *dphi = s->spec_dphi;
+        return 1;
     }
-    out[0] = res;
-    out[1] = passes;
-    out[2] = la;
-    out[3] = lf;
-    out[4] = ld;
+    if (!need_g && s->have_cand && alpha == s->cand_a) {
+        *f = s->cand_f;
+        return 1;
+    }
+    for (int j = 0; j < s->tc_n; ++j)
+        if (alpha == s->tc_a[j] && (!need_g || (j == 0 && s->tc_dphi_ok))) {
+            *f = s->tc_f[j];
+            *dphi = s->tc_dphi;
+            return 1;
+        }
+    if (*pass >= LBK_SEARCH_PASSES) return 0;
+    (*pass)++;
+    if (ls == 2 || ls == 3) {
+        double t[2];
+        if (lbk_trials(c, obj, LBK_D_BUF, x, d, NULL, NULL, 0.0, -1, -1, &alpha, 1, 1, slot) != 0) return -1;
+        if (lbk_fetch(c, slot, 2, t) != 0) return -1;
+        s->tc_n = 1;
+        s->tc_a[0] = alpha;
+        s->tc_f[0] = t[0];
+        s->tc_dphi = t[1];
+        s->tc_dphi_ok = 1;
+        s->passes_fg++;
+        *f = t[0];
+        *dphi = t[1];
+    } else {
+        double a[LBK_TRIALS_NC], t[LBK_TRIALS_NC];
+        a[0] = alpha;
+        for (int j = 1; j < LBK_TRIALS_NC; ++j) a[j] = a[j - 1] * (ls == 0 ? s->beta : 0.5);
+        if (lbk_trials(c, obj, LBK_D_BUF, x, d, NULL, NULL, 0.0, -1, -1, a, LBK_TRIALS_NC, 0, slot) != 0) return -1;
+        if (lbk_fetch(c, slot, LBK_TRIALS_NC, t) != 0) return -1;
+        s->tc_n = LBK_TRIALS_NC;
+        for (int j = 0; j < LBK_TRIALS_NC; ++j) {
+            s->tc_a[j] = a[j];
+            s->tc_f[j] = t[j];
+        }
+        s->tc_dphi = 0.0;
+        s->tc_dphi_ok = 0;
+        s->passes_f++;
+        *f = t[0];
+    }
+    return 1;
+}
+#define TRIAL(al, ng, f, dp)                                                          \
+    do {                                                                              \
+        const int r_ = dbl_trial(c, obj, ls, x, d, &s, &pass, (al), (ng), (f), (dp)); \
+        if (r_ < 0) return -1;                                                        \
+        if (r_ == 0) goto out;                                                        \
+    } while (0)
+int lbk_search_dev(lbk_ctx* c, int obj, int ls, const double* x, const double* d, lbk_search* st,
+                   const lbk_search_commit* cm) {
+    if (!lbk_search_dev_ok(c, obj)) return -1;
+    lbk_search s = *st;
+    s.done = s.committed = s.passes_f = s.passes_fg = 0;
+    int pass = 0;
+    double alpha = s.alpha, dd = 0.0;
+    if (ls == 0) {
+        for (;;) {
+            double ft;
+            TRIAL(alpha, 0, &ft, &dd);
+            if (!(s.f_x - ft < s.c1 * alpha * s.gd)) break;
+            alpha *= s.beta;
+            if (alpha < s.tol) break;
+        }
+        s.done = 1;
+        s.step = alpha;
+    } else if (ls == 1) {
+        for (;;) {
+            if (!(s.iter++ < 20)) {
+                s.done = 1;
+                s.step = alpha;
+                break;
+            }
+            double f_new;
+            const int r = dbl_trial(c, obj, ls, x, d, &s, &pass, alpha, 0, &f_new, &dd);
+            if (r < 0) return -1;
+            if (r == 0) {
+                s.iter--;
+                break;
+            }
+            if (f_new <= s.f_x + s.c1 * alpha * s.gd) {
+                s.done = 1;
+                s.step = alpha;
+                break;
+            }
+            if (alpha < s.amin) {
+                s.done = 1;
+                s.step = s.amin;
+                break;
+            }
+            if (s.alpha_prev > 0) {
+                if (fabs(alpha - s.alpha_prev) < 1e-10) {
+                    alpha *= 0.5;
+                } else {
+                    const double ga = (f_new - s.f_x - s.gd * alpha) / (alpha * alpha);
+                    alpha = wolfe_cubic(s.alpha_prev, alpha, s.f_prev, s.gd, f_new, ga);
+                    if (alpha < 0.1 * s.alpha_prev || alpha > 0.9 * s.alpha_prev) alpha = s.alpha_prev * 0.5;
+                }
+            } else {
+                alpha = alpha - 0.5 * s.gd * alpha * alpha / (s.f_x - f_new - s.gd * alpha);
+                if (alpha < 0.1 * s.init || alpha > 0.9 * s.init) alpha = s.init * 0.5;
+            }
+            s.alpha_prev = alpha;
+            s.f_prev = f_new;
+        }
+    } else if (ls == 2) {
+        for (;;) {
+            if (s.iter >= 20) {
+                s.done = 1;
+                s.step = alpha;
+                break;
+            }
+            double f_new, dphi_new;
+            TRIAL(alpha, 0, &f_new, &dphi_new);
+            if (f_new > s.f_x + s.c1 * alpha * s.gd || (f_new >= s.f_lo && s.iter > 0)) {
+                s.alpha_hi = alpha;
+                alpha = wolfe_cubic(s.alpha_lo, s.alpha_hi, s.f_lo, s.dphi_lo, f_new,
+                                    (f_new - s.f_x - s.gd * alpha) / (alpha * alpha));
+                ++s.iter;
+                continue;
+            }
+            TRIAL(alpha, 1, &f_new, &dphi_new);
+            if (fabs(dphi_new) <= -s.c2 * s.gd) {
+                s.done = 1;
+                s.step = alpha;
+                break;
+            }
+            if (dphi_new >= 0) {
+                s.alpha_hi = alpha;
+                alpha = wolfe_cubic(s.alpha_lo, s.alpha_hi, s.f_lo, s.dphi_lo, f_new, dphi_new);
+            } else {
+                s.alpha_lo = alpha;
+                s.f_lo = f_new;
+                s.dphi_lo = dphi_new;
+                alpha = s.alpha_hi == INFINITY ? alpha * 2
+                                               : wolfe_cubic(s.alpha_lo, s.alpha_hi, s.f_lo, s.dphi_lo, f_new, dphi_new);
+            }
+            if (alpha < s.amin) {
+                s.done = 1;
+                s.step = s.amin;
+                break;
+            }
+            ++s.iter;
+        }
+    } else {
+        for (;;) {
+            double fn, dphi;
+            TRIAL(alpha, 1, &fn, &dphi);
+            if (fn > s.f_x + s.c1 * alpha * s.gd) {
+                alpha *= s.beta;
+            } else if (dphi < s.c2 * s.gd) {
+                alpha *= 1.1;
+            } else {
+                break;
+            }
+            if (alpha < s.tol) break;
+        }
+        s.done = 1;
+        s.step = alpha;
+    }
+out:
+    s.alpha = alpha;
+    if (s.done && cm && cm->slot >= 0 && !(s.have_spec && s.step == s.spec_a)) {
+        if (lbk_commit(c, obj, LBK_D_BUF, x, d, NULL, cm->g, 0.0, -1, -1, s.step, cm->xn, cm->gn, cm->so, cm->yo,
+                       cm->slot, 0.0) != 0)
+            return -1;
+        s.committed = 1;
+    }
+    *st = s;
     return 0;
 }
+#undef TRIAL
 int lbk_small_spec_ok(const lbk_ctx* c, int h) { return lbk_small_ok(c, h); }
 
 /* the prologue of a speculative launch (k_coop_iter's spec_ok), on this double's slots */

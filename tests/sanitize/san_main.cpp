@@ -120,7 +120,7 @@ static std::vector<double> x0_for(int64_t n, uint32_t seed) {
 static void device_objectives() {
     const int64_t sizes[] = {1, 2, 3, 1000, 4097, 70001};
     const int objs[] = {LBFGS_OBJ_ROSENBROCK, LBFGS_OBJ_QUAD_TRIDIAG, LBFGS_OBJ_QUAD_SEPARABLE};
-    int64_t adopted = 0, dropped = 0;
+    int64_t adopted = 0, dropped = 0, searches[4] = {0, 0, 0, 0}, search_commits = 0;
     for (int64_t n : sizes)
         for (int obj : objs)
             for (int ls = 0; ls < 4; ++ls)
@@ -150,12 +150,24 @@ static void device_objectives() {
                     EXPECT(mode == 3 || a + d == 0, "%s: speculative launches outside the speculative mode", tag);
                     adopted += a;
                     dropped += d;
+                    int64_t sl = 0, sc = 0;  // the device-resident line search (the double's restatement)
+                    lbfgs_search_stats(c, &sl, &sc);
+                    EXPECT(mode == 3 || mode == 4 || sl == 0, "%s: device searches outside the small-n forms", tag);
+                    EXPECT(sc <= sl, "%s: %lld device-search commits of %lld launches", tag, (long long)sc,
+                           (long long)sl);
+                    searches[ls] += sl;
+                    search_commits += sc;
                     lbfgs_ctx_destroy(c);
                 }
     EXPECT(adopted > 100 && dropped > 10, "speculative launches: %lld taken, %lld dropped", (long long)adopted,
            (long long)dropped);
     std::printf("speculative next iteration: %lld launches taken, %lld dropped\n", (long long)adopted,
                 (long long)dropped);
+    for (int ls = 0; ls < 4; ++ls) EXPECT(searches[ls] > 0, "line search %d never continued on the device", ls);
+    EXPECT(search_commits > 0, "no device-search commit");
+    std::printf("device line searches: %lld / %lld / %lld / %lld launches (backtracking / interpolation / Wolfe / "
+                "backtracking-Wolfe), %lld commits in them\n", (long long)searches[0], (long long)searches[1],
+                (long long)searches[2], (long long)searches[3], (long long)search_commits);
     setenv("LBFGS_BATCH", "1", 1);
     setenv("LBFGS_DOUBLE_SMALL", "0", 1);
     setenv("LBFGS_SPEC", "1", 1);

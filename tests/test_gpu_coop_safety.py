@@ -1,12 +1,14 @@
 """The cooperative forms are safe by construction.
 
-* Each grid-barrier kernel is capped by its OWN occupancy: the device-resident line search
-  (k_coop_wolfe) has a cap of its own (search_max), never above the cooperative iteration's, and
+* Each grid-barrier kernel is capped by its OWN occupancy: the device-resident line searches
+  (k_coop_search) have a cap of their own (search_max), never above the cooperative iteration's, and
   a context whose cap is below the grid (LBFGS_COOP forcing it) runs the host loop instead.
 * A device search whose grid barrier times out (forced here with LBFGS_SEARCH_TIMEOUT=0: every
   barrier gives up at its first miss) stored nothing, so the host loop redoes the search from the
   same state: the solve continues, bit-identical to the host loop and to the canonical oracle,
-  instead of failing with "grid barrier timed out"."""
+  instead of failing with "grid barrier timed out". The launch may have reached its commit pass
+  (the recommit at the step it found), so the host then also repeats the first commit when its
+  search ends at the first trial's step."""
 import os
 import sys
 
@@ -26,7 +28,7 @@ def bits(a):
 
 
 def solve(monkeypatch, env, n, m, obj, ls, iters, seed=3):
-    for k in ("LBFGS_SEARCH_TIMEOUT", "LBFGS_DEV_WOLFE", "LBFGS_COOP"):
+    for k in ("LBFGS_SEARCH_TIMEOUT", "LBFGS_DEV_WOLFE", "LBFGS_DEV_SEARCH", "LBFGS_COOP"):
         monkeypatch.delenv(k, raising=False)
     for k, v in env.items():
         monkeypatch.setenv(k, v)
@@ -53,20 +55,23 @@ def test_grid_caps_from_each_kernels_occupancy(monkeypatch):
     assert r["coop"]["fallbacks"] == 0
 
 
-@pytest.mark.parametrize("n,m,obj", [(10_000, 5, "rosenbrock"), (100_000, 10, "rosenbrock"),
-                                     (30_001, 7, "rosenbrock")])
-def test_search_barrier_timeout_falls_back_bit_identical(monkeypatch, n, m, obj):
+@pytest.mark.parametrize("n,m,obj,ls", [(10_000, 5, "rosenbrock", "wolfe"), (100_000, 10, "rosenbrock", "wolfe"),
+                                        (30_001, 7, "rosenbrock", "wolfe"),
+                                        (10_000, 5, "rosenbrock", "interpolation"),
+                                        (30_001, 7, "quad_tridiag", "backtracking_wolfe"),
+                                        (20_001, 3, "rosenbrock", "backtracking")])
+def test_search_barrier_timeout_falls_back_bit_identical(monkeypatch, n, m, obj, ls):
     iters = 150
-    x0, host = solve(monkeypatch, {"LBFGS_DEV_WOLFE": "0"}, n, m, obj, "wolfe", iters)
-    _, dev = solve(monkeypatch, {}, n, m, obj, "wolfe", iters)
-    _, forced = solve(monkeypatch, {"LBFGS_SEARCH_TIMEOUT": "0"}, n, m, obj, "wolfe", iters)
+    x0, host = solve(monkeypatch, {"LBFGS_DEV_SEARCH": "0"}, n, m, obj, ls, iters)
+    _, dev = solve(monkeypatch, {}, n, m, obj, ls, iters)
+    _, forced = solve(monkeypatch, {"LBFGS_SEARCH_TIMEOUT": "0"}, n, m, obj, ls, iters)
     assert host["coop0"]["search_max"] == 0 and dev["coop0"]["search_max"] > 0
     # the forced run took the device path, timed out once, and then stayed on the host loop
     assert forced["coop"]["fallbacks"] == 1 and forced["coop"]["search_max"] == 0, forced["coop"]
     assert dev["coop"]["fallbacks"] == 0
     same(forced, host)
     same(dev, host)
-    o = O.lbfgs(obj, x0, "wolfe", m, iters, 1e-5, mode=O.CANON)
+    o = O.lbfgs(obj, x0, ls, m, iters, 1e-5, mode=O.CANON)
     assert np.array_equal(bits(forced["tr_f"]), bits(o["f"])) and np.array_equal(bits(forced["x"]), bits(o["x"]))
 
 

@@ -30,7 +30,7 @@ pytestmark = pytest.mark.gpu
 # LBK_PERSIST_ALT, LBK_PERSIST_LDS; the q/r ping-pong was removed).
 KNOBS = ["LBFGS_TICKET", "LBFGS_DEFER", "LBFGS_REV", "LBFGS_NT", "LBFGS_DIRECT", "LBFGS_COOP",
          "LBFGS_PERSIST", "LBFGS_SPEC", "LBFGS_BATCH", "LBFGS_PERSIST_WG", "LBFGS_COLLECT",
-         "LBFGS_COLLECT_TIMEOUT", "LBFGS_DEV_WOLFE", "LBFGS_SEARCH_TIMEOUT"]
+         "LBFGS_COLLECT_TIMEOUT", "LBFGS_DEV_SEARCH", "LBFGS_DEV_WOLFE", "LBFGS_SEARCH_TIMEOUT"]
 
 VARIANTS = {
     "ticket1": {"LBFGS_TICKET": "1"},
@@ -57,14 +57,17 @@ VARIANTS = {
     "collect_timeout": {"LBFGS_COLLECT": "1", "LBFGS_COLLECT_TIMEOUT": "30"},
     "defer_all_rev0": {"LBFGS_DEFER": "8192", "LBFGS_TICKET": "0", "LBFGS_REV": "0"},
     "coop0_spec0_batch0": {"LBFGS_COOP": "0", "LBFGS_SPEC": "0", "LBFGS_BATCH": "0"},
-    "devwolfe0": {"LBFGS_DEV_WOLFE": "0"},
-    "devwolfe0_spec0": {"LBFGS_DEV_WOLFE": "0", "LBFGS_SPEC": "0"},
+    "devsearch0": {"LBFGS_DEV_SEARCH": "0"},
+    "devsearch0_spec0": {"LBFGS_DEV_SEARCH": "0", "LBFGS_SPEC": "0"},
+    "devwolfe0_round4_name": {"LBFGS_DEV_WOLFE": "0"},
     "search_timeout0": {"LBFGS_SEARCH_TIMEOUT": "0"},  # the device search gives up, the host loop redoes it
 }
 
 CASES = [  # n, m, objective, line search, iterations
     (100_003, 5, "rosenbrock", "backtracking", 25),       # 196 segments: cooperative iteration
-    (60_001, 5, "rosenbrock", "wolfe", 40),               # 118 segments: the device-resident Wolfe search
+    (60_001, 5, "rosenbrock", "wolfe", 40),               # 118 segments: the device-resident line searches
+    (30_001, 6, "quad_tridiag", "interpolation", 40),      # 59 segments: ... the interpolation search
+    (20_001, 4, "rosenbrock", "backtracking_wolfe", 60),   # 40 segments: ... backtracking-Wolfe
     (700_001, 7, "quad_tridiag", "wolfe", 12),             # 342 segments of 2048: deferred stage 2
     (3_000_017, 5, "rosenbrock", "interpolation", 14),     # 5860 segments of 512: reduce kernel
     (5_000_000, 10, "rosenbrock", "backtracking", 14),     # 7813 segments of 640, h = m reached

@@ -1,11 +1,11 @@
 #!/usr/bin/env python3
-"""Soak of the device-resident Wolfe search: seeded random cooperative sizes
-(n up to 131 072, <= 256 segments), histories 1..20, every objective, random tolerances and caps,
-the Wolfe search in the default mode; each solve compared bit for bit with the oracle's canonical
-restatement (trace f / |g| / step / x checksums, final x, messages, status, iterations), and the
-host loop (LBFGS_DEV_WOLFE=0) on every tenth draw. Prints progress and one JSON summary line.
+"""Soak of the device-resident line searches: seeded random cooperative sizes
+(n up to 131 072, <= 256 segments), histories 1..20, every objective, every line search, random
+tolerances and caps, in the default mode; each solve compared bit for bit with the oracle's
+canonical restatement (trace f / |g| / step / x checksums, final x, messages, status, iterations),
+and the host loop (LBFGS_DEV_SEARCH=0) on every tenth draw. Prints progress and one JSON summary.
 
-usage: python tools/wolfe_soak.py [cases] [out.json]
+usage: python tools/search_soak.py [cases] [out.json]
 """
 import json
 import os
@@ -34,34 +34,44 @@ def same(r, o):
             and np.array_equal(bits(r["x"]), bits(o["x"])) and r["messages"] == o["messages"])
 
 
-def solve(n, m, obj, x0, maxit, tol, dev):
-    os.environ["LBFGS_DEV_WOLFE"] = "1" if dev else "0"
+def solve(n, m, obj, ls, x0, maxit, tol, dev):
+    os.environ["LBFGS_DEV_SEARCH"] = "1" if dev else "0"
     with L.Context(n, m) as c:
-        return c.minimize(obj, x0, "wolfe", maxit, tolerance=tol, trace=True)
+        r = c.minimize(obj, x0, ls, maxit, tolerance=tol, trace=True)
+        r["search"] = c.search_stats()
+        return r
 
 
 def main():
     cases = int(sys.argv[1]) if len(sys.argv) > 1 else 300
     rs = np.random.RandomState(9090)
-    objs = ["rosenbrock", "quad_tridiag"]  # the separable quadratic diverges under Wolfe (reference too)
-    bad, trials, t0 = [], 0, time.time()
+    objs = ["rosenbrock", "quad_tridiag", "quad_sep"]
+    searches = ["backtracking", "interpolation", "wolfe", "backtracking_wolfe"]
+    bad, trials, launches, commits, t0 = [], 0, 0, 0, time.time()
     for i in range(cases):
         n = int(rs.choice([rs.randint(1, 600), rs.randint(600, 20001), rs.randint(20001, 131073)]))
-        m, obj, seed = int(rs.randint(1, 21)), objs[rs.randint(2)], int(rs.randint(1, 1 << 30))
+        m, obj, seed = int(rs.randint(1, 21)), objs[rs.randint(3)], int(rs.randint(1, 1 << 30))
+        ls = searches[rs.randint(4)]
+        if obj == "quad_sep" and ls == "wolfe":  # diverges to NaN (the reference too)
+            obj = "rosenbrock"
         maxit, tol = int(rs.choice([20, 100, 400])), float(10.0 ** rs.uniform(-10, -3))
         x0 = O.x0_uniform(n, seed, -2.0, 2.0)
         with np.errstate(all="ignore"):
-            o = O.lbfgs(obj, x0, "wolfe", m, maxit, tol, mode=O.CANON)
-            r = solve(n, m, obj, x0, maxit, tol, True)
+            o = O.lbfgs(obj, x0, ls, m, maxit, tol, mode=O.CANON)
+            r = solve(n, m, obj, ls, x0, maxit, tol, True)
             ok = same(r, o)
             if ok and i % 10 == 0:
-                ok = same(solve(n, m, obj, x0, maxit, tol, False), o)
-        trials += int(r["trials_fg"])
+                h = solve(n, m, obj, ls, x0, maxit, tol, False)
+                ok = same(h, o) and all(h[k] == r[k] for k in ("trials_f", "trials_fg", "commits", "passes"))
+        trials += int(r["trials_fg"]) + int(r["trials_f"])
+        launches += r["search"][0]
+        commits += r["search"][1]
         if not ok:
-            bad.append(dict(n=n, m=m, obj=obj, seed=seed, maxit=maxit, tol=tol))
+            bad.append(dict(n=n, m=m, obj=obj, ls=ls, seed=seed, maxit=maxit, tol=tol))
         if (i + 1) % 50 == 0:
             print(f"{i + 1}/{cases} solves, {len(bad)} mismatches, {time.time() - t0:.0f} s", flush=True)
-    out = dict(tool="tools/wolfe_soak.py", cases=cases, mismatches=len(bad), bad=bad[:20], trial_passes=trials,
+    out = dict(tool="tools/search_soak.py", cases=cases, mismatches=len(bad), bad=bad[:20], trial_passes=trials,
+               device_searches=launches, device_commits=commits,
                seconds=round(time.time() - t0, 1), build=L.build_info()[0])
     line = json.dumps(out)
     print(line)
