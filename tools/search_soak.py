@@ -62,7 +62,8 @@ def main():
             ok = same(r, o)
             if ok and i % 10 == 0:
                 h = solve(n, m, obj, ls, x0, maxit, tol, False)
-                ok = same(h, o) and all(h[k] == r[k] for k in ("trials_f", "trials_fg", "commits", "passes"))
+                ok = (same(h, o) and all(h[k] == r[k] for k in ("trials_f", "trials_fg", "commits"))
+                      and 0 <= r["passes"] - h["passes"] <= r["search"][0])
         trials += int(r["trials_fg"]) + int(r["trials_f"])
         launches += r["search"][0]
         commits += r["search"][1]
