@@ -1350,7 +1350,7 @@ static int commit_queued(lbfgs_ctx* c, int dmode, double alpha, int cslot, doubl
     const double* s_last = dmode == LBK_D_TWOLOOP ? c->S[c->s_last_pair] : NULL;
     DEV(lbk_commit(c->dev, c->obj, dmode, c->x, dsrc, s_last, c->g, c->rho_last, c->ref_b_last, c->ref_a_last, alpha,
                    c->xn, c->gn, c->S[pair], c->Y[pair], cslot, 0.0));
-    DEV(lbk_mark(c->dev));
+    DEVNC(lbk_mark(c->dev)); /* an event, not a pass */
     int rc = alpha >= 1e-10 ? spec_next(c, alpha) : 0;
     if (rc) return rc;
     DEVNC(lbk_fetch_marked(c->dev, cslot, 7, tot));
