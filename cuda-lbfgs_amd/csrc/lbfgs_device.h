@@ -138,8 +138,11 @@ int lbk_cu_partition(const lbk_ctx* c);
 /* the cooperative forms' grid caps (segments) and the device searches redone on the host loop */
 int lbk_coop_info(const lbk_ctx* c, int* coop_max, int* search_max, int* fallbacks);
 /* box probe: `launches` back-to-back 3 R + 1 W streams over (q, y, s) in the two-loop passes'
- * geometry and cache policy, q written back unchanged; mean microseconds per launch */
-int lbk_stream_probe(lbk_ctx* c, double* q, const double* y, const double* s, int launches, double* us);
+ * geometry and cache policy, q written back unchanged; launch i reads the pair pool's
+ * y[(i + 1) % npairs] and s[i % npairs] (another pair every launch, as the passes: only q's tail
+ * is left in the Infinity Cache by the launch before); mean microseconds per launch */
+int lbk_stream_probe(lbk_ctx* c, double* q, const double* const* ys, const double* const* ss, int npairs,
+                     int launches, double* us);
 
 /* memory */
 double* lbk_vec_alloc(lbk_ctx* c);

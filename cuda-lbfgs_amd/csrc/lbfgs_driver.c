@@ -505,7 +505,10 @@ int lbfgs_stream_probe(lbfgs_ctx* c, int launches, double* us, double* bytes) {
      * (q - 0 * y is q only while y is finite) */
     double* scratch = lbk_vec_alloc(c->dev);
     if (!scratch) return dev_err(c, -2);
-    const int rc = lbk_stream_probe(c->dev, scratch, c->Y[0], c->S[0], launches, us);
+    pair_views(c, 0); /* (a vector-free solve's paired rows are read as plain vectors here) */
+    const int rc = lbk_stream_probe(c->dev, scratch, (const double* const*)c->Y, (const double* const*)c->S, c->m + 1,
+                                    launches, us);
+    pair_views(c, c->vf);
     lbk_vec_free(c->dev, scratch);
     if (rc != 0) return dev_err(c, rc);
     if (bytes) *bytes = 32.0 * (double)c->geo->n_loc;

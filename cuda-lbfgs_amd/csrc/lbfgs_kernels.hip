@@ -1538,8 +1538,11 @@ int lbk_coop_info(const lbk_ctx* c, int* coop_max, int* search_max, int* fallbac
     return 0;
 }
 
-int lbk_stream_probe(lbk_ctx* c, double* q, const double* y, const double* s, int launches, double* us) {
-    if (launches < 1 || !us || !q || !y || !s) return -1;
+int lbk_stream_probe(lbk_ctx* c, double* q, const double* const* ys, const double* const* ss, int npairs,
+                     int launches, double* us) {
+    if (launches < 1 || !us || !q || !ys || !ss || npairs < 1) return -1;
+    for (int k = 0; k < npairs; ++k)
+        if (!ys[k] || !ss[k]) return -1;
     HIPCHK(c, hipSetDevice(c->device));
     {
         const int rc = flush_pending(c);
@@ -1558,6 +1561,8 @@ int lbk_stream_probe(lbk_ctx* c, double* q, const double* y, const double* s, in
     const int par = c->rev_par;  // the solver's walk parity is left as it was
     for (int i = 0; i < launches; ++i) {
         const Geo g = kgeo(c);  // alternating walk, as the passes
+        const double* y = ys[(i + 1) % npairs];
+        const double* s = ss[i % npairs];
         NT_DISPATCH(c, hipLaunchKernelGGL(k_probe_stream<NT_>, dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, q, y, s,
                                           g, c->partials));
         c->rev_par ^= 1;

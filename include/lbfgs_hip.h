@@ -247,8 +247,9 @@ int lbfgs_cu_partition(const lbfgs_ctx* ctx);
  * whose grid barrier timed out (LBFGS_SEARCH_TIMEOUT, 2 s) and that the host loop redid. */
 int lbfgs_coop_info(const lbfgs_ctx* ctx, int* coop_max, int* search_max, int* fallbacks);
 /* Diagnostic (no reference counterpart): `launches` back-to-back streams of 3 reads + 1 write
- * over a scratch work vector and the context's history vectors (y, s of the pair pool) in the
- * two-loop passes' geometry and cache policy; the solve's own vectors and state are untouched. *us = mean microseconds per
+ * over a scratch work vector and the context's history vectors (y, s of the pair pool, another
+ * pair every launch as the two-loop passes read them) in the passes' geometry and cache policy;
+ * the solve's own vectors and state are untouched. *us = mean microseconds per
  * launch, *bytes = this rank's bytes per launch (32 n_loc). bench.py reports this box's rate for
  * the passes' access pattern beside the solver's. Call between lbfgs_solver_step calls of an
  * initialised solve. */

@@ -154,8 +154,9 @@ int lbk_coop_info(const lbk_ctx* c, int* a, int* b, int* f) {
     if (f) *f = 0;
     return 0;
 }
-int lbk_stream_probe(lbk_ctx* c, double* q, const double* y, const double* s, int launches, double* us) {
-    (void)c, (void)q, (void)y, (void)s, (void)launches;
+int lbk_stream_probe(lbk_ctx* c, double* q, const double* const* ys, const double* const* ss, int npairs,
+                     int launches, double* us) {
+    (void)c, (void)q, (void)ys, (void)ss, (void)npairs, (void)launches;
     *us = 0.0;  /* no device: nothing to time */
     return 0;
 }
