@@ -1141,7 +1141,7 @@ __device__ __forceinline__ void run_pass(const Op& op, const Geo& geo, const Red
 #ifndef LBK_FOLD_PREFETCH
 #define LBK_FOLD_PREFETCH 1  // A/B: 0 polls before any load, as round 3's first folded consumers
 #endif
-template <class Op, int K, class Coef>
+template <class Op, int K, class Coef, bool FOLD = true>
 __device__ __forceinline__ void run_pass_prefetch(Op op, const Geo& geo, const Red& red, Coef coef) {
     const Seg s = seg_setup(geo);
     double acc[K];
@@ -1158,9 +1158,16 @@ __device__ __forceinline__ void run_pass_prefetch(Op op, const Geo& geo, const R
         op.set_coef(coef());
         stream(op, s, geo, acc);
     }
-    if (red.fp.peers && geo.edge_slot) fold_push_edges(geo, s, red.fp);
-    reduce_publish<K, true>(acc, geo, red);
+    if (FOLD && red.fp.peers && geo.edge_slot) fold_push_edges(geo, s, red.fp);
+    reduce_publish<K, FOLD>(acc, geo, red);
 }
+
+// A/B (variant builds): one GPU, the two-loop passes issue their first row group's loads before
+// they read the previous pass's total (the slot read's latency under those loads, as the folded
+// consumers do)
+#ifndef LBK_PREFETCH_COEF
+#define LBK_PREFETCH_COEF 0
+#endif
 
 template <class Op, int K>
 __device__ __forceinline__ void run_pass_halo(const Op& op, const Geo& geo, const Red& red) {
@@ -1193,6 +1200,11 @@ __global__ __launch_bounds__(LB_BLOCK) void k_axpy_dot(double* qout, const doubl
             return;
         }
     }
+    if (LBK_PREFETCH_COEF) {
+        auto coef = [&] { return rho * src_total(prev, geo); };
+        run_pass_prefetch<OpAxpyDot<NT>, 1, decltype(coef), FOLD>(OpAxpyDot<NT>{qout, qin, y, sv, 0.0}, geo, red, coef);
+        return;
+    }
     const double alpha = rho * src_total(prev, geo);
     run_pass<OpAxpyDot<NT>, 1, FOLD>(OpAxpyDot<NT>{qout, qin, y, sv, alpha}, geo, red);
 }
@@ -1208,6 +1220,12 @@ __global__ __launch_bounds__(LB_BLOCK) void k_mid(double* __restrict__ rout, con
                                             geo, red, [&] { return rho0 * src_total_mailbox(prev, geo, fs); });
             return;
         }
+    }
+    if (LBK_PREFETCH_COEF) {
+        auto coef = [&] { return rho0 * src_total(prev, geo); };
+        run_pass_prefetch<OpMid<NT>, 1, decltype(coef), FOLD>(
+            OpMid<NT>{rout, qin, y0, 0.0, gamma, geo.edge_slot, geo.n_loc, geo.g_lo, geo.g_hi}, geo, red, coef);
+        return;
     }
     const double alpha = rho0 * src_total(prev, geo);
     run_pass<OpMid<NT>, 1, FOLD>(OpMid<NT>{rout, qin, y0, alpha, gamma, geo.edge_slot, geo.n_loc, geo.g_lo, geo.g_hi},
@@ -1230,6 +1248,16 @@ __global__ __launch_bounds__(LB_BLOCK) void k_axpy2_dot(double* r, const double*
                 });
             return;
         }
+    }
+    if (LBK_PREFETCH_COEF) {
+        auto coef = [&] {
+            const double beta = rho * src_total(pb, geo);
+            const double alpha = rho * slot_total(pa);
+            return alpha - beta;
+        };
+        run_pass_prefetch<OpAxpy2Dot<NT>, 1, decltype(coef), FOLD>(
+            OpAxpy2Dot<NT>{r, rin, sv, yn, 0.0, geo.edge_slot, geo.n_loc, geo.g_lo, geo.g_hi}, geo, red, coef);
+        return;
     }
     const double beta = rho * src_total(pb, geo);
     const double alpha = rho * slot_total(pa);
