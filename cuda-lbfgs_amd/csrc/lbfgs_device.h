@@ -147,14 +147,6 @@ int lbk_stream_probe(lbk_ctx* c, double* q, const double* const* ys, const doubl
 /* memory */
 double* lbk_vec_alloc(lbk_ctx* c);
 void lbk_vec_free(lbk_ctx* c, double* v);
-/* a history pair's storage (s and y): one allocation of two vectors' room. View 0: two vectors of
- * lbk_vec_alloc's layout, each at the offset a separate allocation would have (a whole number of
- * 2-MiB pages apart); view 1 (the vector-free kernels' paired rows, lbk_vf_paired): s and y
- * alternate by 128-element rows, element i at s[2i - (i mod 128)], y = s + 128 */
-int lbk_vf_paired(const lbk_ctx* c);
-double* lbk_pair_alloc(lbk_ctx* c);
-void lbk_pair_free(lbk_ctx* c, double* p);
-void lbk_pair_view(const lbk_ctx* c, double* p, int paired, double** s, double** y);
 void* lbk_host_alloc(size_t bytes); /* pinned host memory (NULL on failure) */
 void lbk_host_free(void* p);
 int lbk_upload(lbk_ctx* c, double* dst, const double* host_global);     /* incl. ghosts */

@@ -69,7 +69,6 @@ struct lbfgs_ctx {
     /* device vectors */
     double *x, *g, *xn, *gn, *d, *q, *r, *gt;
     const double* rc;   /* the r the last two-loop pass wrote */
-    double* P[MMAX + 1]; /* pair storage (lbk_pair_alloc) when the library pairs the vector-free rows */
     double* S[MMAX + 1];
     double* Y[MMAX + 1];
     /* history: ring[0] oldest .. ring[h-1] newest, indices into the m+1 pair pool */
@@ -295,13 +294,9 @@ static void free_vectors(lbfgs_ctx* c) {
         *v[i] = NULL;
     }
     for (int i = 0; i <= MMAX; ++i) {
-        if (c->P[i]) {
-            lbk_pair_free(c->dev, c->P[i]);
-        } else {
-            lbk_vec_free(c->dev, c->S[i]);
-            lbk_vec_free(c->dev, c->Y[i]);
-        }
-        c->P[i] = c->S[i] = c->Y[i] = NULL;
+        lbk_vec_free(c->dev, c->S[i]);
+        lbk_vec_free(c->dev, c->Y[i]);
+        c->S[i] = c->Y[i] = NULL;
     }
 }
 
@@ -330,14 +325,6 @@ void lbfgs_host_group_destroy(lbfgs_host_group* h) {
     free(h);
 }
 
-/* the history's layout: the vector-free kernels' paired rows, or two vectors. Set when a solve
- * starts (its ring starts empty, so nothing stored in the other layout is read) and by the
- * primitive calls that upload pairs themselves */
-static void pair_views(lbfgs_ctx* c, int paired) {
-    for (int i = 0; i <= c->m; ++i)
-        if (c->P[i]) lbk_pair_view(c->dev, c->P[i], paired, &c->S[i], &c->Y[i]);
-}
-
 static int ctx_create(lbfgs_ctx** out, int64_t n, int m, int device, int rank, int world,
                       const void* unique_id, lbk_group* grp) {
     if (!out) return LBFGS_ERR_BAD_ARG;
@@ -363,13 +350,8 @@ static int ctx_create(lbfgs_ctx** out, int64_t n, int m, int device, int rank, i
     int ok = 1;
     for (size_t i = 0; i < sizeof v / sizeof v[0]; ++i) ok &= (*v[i] = lbk_vec_alloc(c->dev)) != NULL;
     for (int i = 0; i <= m; ++i) {
-        if (lbk_vf_paired(c->dev)) { /* one buffer per pair: the vector-free mode pairs its rows */
-            ok &= (c->P[i] = lbk_pair_alloc(c->dev)) != NULL;
-            if (c->P[i]) lbk_pair_view(c->dev, c->P[i], 0, &c->S[i], &c->Y[i]);
-        } else {
-            ok &= (c->S[i] = lbk_vec_alloc(c->dev)) != NULL;
-            ok &= (c->Y[i] = lbk_vec_alloc(c->dev)) != NULL;
-        }
+        ok &= (c->S[i] = lbk_vec_alloc(c->dev)) != NULL;
+        ok &= (c->Y[i] = lbk_vec_alloc(c->dev)) != NULL;
     }
     if (!ok) {
         fprintf(stderr, "lbfgs_ctx_create: %s\n", lbk_last_error(c->dev));
@@ -505,10 +487,8 @@ int lbfgs_stream_probe(lbfgs_ctx* c, int launches, double* us, double* bytes) {
      * (q - 0 * y is q only while y is finite) */
     double* scratch = lbk_vec_alloc(c->dev);
     if (!scratch) return dev_err(c, -2);
-    pair_views(c, 0); /* (a vector-free solve's paired rows are read as plain vectors here) */
     const int rc = lbk_stream_probe(c->dev, scratch, (const double* const*)c->Y, (const double* const*)c->S, c->m + 1,
                                     launches, us);
-    pair_views(c, c->vf);
     lbk_vec_free(c->dev, scratch);
     if (rc != 0) return dev_err(c, rc);
     if (bytes) *bytes = 32.0 * (double)c->geo->n_loc;
@@ -2406,7 +2386,6 @@ int lbfgs_solver_init(lbfgs_ctx* c, int objective, const lbfgs_host_fn* cb, int 
             if (!c->Gss || !c->Gsy || !c->Gyy || !c->Gsg || !c->Gyg) return LBFGS_ERR_NOMEM;
         }
     }
-    pair_views(c, c->vf);
     c->cuda = (flags & LBFGS_FLAG_CUDA_COMPAT) != 0;
     if ((flags & LBFGS_FLAG_CUDA_VARIANT) && !c->cuda) return LBFGS_ERR_BAD_ARG;
     if (c->cuda && (flags & LBFGS_FLAG_CUDA_VARIANT)) c->cuda = 2;
@@ -2636,7 +2615,6 @@ int lbfgs_dev_twoloop(lbfgs_ctx* c, const double* g, const double* const* S, con
                       int h, double* d_out, double* gd_out) {
     if (!c || !g || h < 1 || h > c->m || !S || !Y) return LBFGS_ERR_BAD_ARG;
     c->inited = 0;
-    pair_views(c, 0);
     const int m = c->m;
     DEVNC(lbk_upload(c->dev, c->g, g));
     for (int i = 0; i < h; ++i) {

@@ -571,49 +571,6 @@ void lbk_vec_free(lbk_ctx* c, double* v) {
     if (v) (void)hipFree(v - LBK_FRONT);
 }
 
-int lbk_vf_paired(const lbk_ctx* c) {
-    (void)c;
-    return LBK_VF_PAIRED;
-}
-
-// the second vector of view 0 starts where a separate hipMalloc would put it relative to the first
-// (allocations are whole 2-MiB pages), so the default mode's streams keep their channel phases
-static int64_t pair_stride(const lbk_ctx* c) {
-    const int64_t page = (2ll << 20) / (int64_t)sizeof(double);
-    return (c->vec_doubles + page - 1) / page * page;
-}
-
-double* lbk_pair_alloc(lbk_ctx* c) {
-    double* p = nullptr;
-    const int64_t nd = pair_stride(c) + c->vec_doubles;
-    if (hipMalloc(&p, sizeof(double) * nd) != hipSuccess) {
-        snprintf(c->err, sizeof c->err, "hipMalloc of %lld doubles failed", (long long)nd);
-        return nullptr;
-    }
-    if (hipMemsetAsync(p, 0, sizeof(double) * nd, c->stream) != hipSuccess) {
-        (void)hipFree(p);
-        return nullptr;
-    }
-    return p;
-}
-
-void lbk_pair_free(lbk_ctx* c, double* p) {
-    (void)c;
-    if (p) (void)hipFree(p);
-}
-
-void lbk_pair_view(const lbk_ctx* c, double* p, int paired, double** s, double** y) {
-    if (!paired) {
-        *s = p + LBK_FRONT;
-        *y = p + pair_stride(c) + LBK_FRONT;
-        return;
-    }
-    // s[-1] at -129: element 0 at 256 doubles (2 KiB, a whole number of rows' pairs) into the
-    // buffer; the last row of y ends at 256 + 2 roundup(n_loc, 128) + 128 < the two vectors' room
-    *s = p + 256;
-    *y = p + 256 + 128;
-}
-
 void* lbk_host_alloc(size_t bytes) {
     void* p = nullptr;
     return hipHostMalloc(&p, bytes, hipHostMallocDefault) == hipSuccess ? p : nullptr;

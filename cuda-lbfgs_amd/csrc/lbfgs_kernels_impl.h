@@ -1749,16 +1749,6 @@ __global__ __launch_bounds__(LB_BLOCK) void k_terms_dot(const double* __restrict
 // Gram rows. HB is the compile-time capacity (bucket) of h, with uniform runtime guards l < 2h,
 // so the basis registers and accumulators have static indices.
 // ---------------------------------------------------------------------------------------
-// History layout of the vector-free mode (LBK_VF_PAIRED): s_p and y_p of a pair share one
-// buffer in alternating 128-element rows (y_p = s_p + 128), so the same local row of a pair is one
-// 2-KiB run and a commit row touches 2 + h + 2 DRAM runs instead of 2h + 4 (tools/vfilprobe.hip).
-// Element i of either vector sits at vfi(i) = 2i - (i mod 128) from its pointer (i = -1, the
-// ghost cell, included: -129); element pairs (i, i + 1), i even, stay adjacent.
-#ifndef LBK_VF_PAIRED
-#define LBK_VF_PAIRED 0
-#endif
-__device__ __forceinline__ int64_t vfi(int64_t i) { return LBK_VF_PAIRED ? 2 * i - (i & 127) : i; }
-
 template <int HB>
 struct VfBasis {
     const double* b[2 * HB > 0 ? 2 * HB : 1];
@@ -1772,7 +1762,7 @@ __device__ __forceinline__ double vf_dir1(const VfBasis<HB>& B, const double* __
     double d = 0.0;
 #pragma unroll
     for (int l = 0; l < 2 * HB; ++l)
-        if (l < 2 * B.h) d = (l == 0) ? B.c[0] * B.b[0][vfi(i)] : d + B.c[l] * B.b[l][vfi(i)];
+        if (l < 2 * B.h) d = (l == 0) ? B.c[0] * B.b[0][i] : d + B.c[l] * B.b[l][i];
     return B.h == 0 ? B.cg * g[i] : d + B.cg * g[i];
 }
 
@@ -1804,7 +1794,7 @@ struct OpVfCommit {
         r.g = ldx<NT>(g + i);
 #pragma unroll
         for (int l = 0; l < 2 * HB; ++l)
-            if (l < 2 * B.h) r.b[l] = ldv<NT>(B.b[l] + vfi(i));
+            if (l < 2 * B.h) r.b[l] = ldv<NT>(B.b[l] + i);
         form(r);
     }
     // d, z = x + alpha d and the candidate points from the loaded row (every basis product
@@ -1859,8 +1849,8 @@ struct OpVfCommit {
         gn[i] = g2;
         xn[i] = zc;
         const double sv = zc - xv, yv = g2 - gv;
-        so[vfi(i)] = sv;
-        yo[vfi(i)] = yv;
+        so[i] = sv;
+        yo[i] = yv;
         acc[LBK_VF_SY] = fma(sv, yv, acc[LBK_VF_SY]);
         acc[LBK_VF_YY] = fma(yv, yv, acc[LBK_VF_YY]);
         acc[LBK_VF_GG] = fma(g2, g2, acc[LBK_VF_GG]);
@@ -1890,8 +1880,8 @@ struct OpVfCommit {
         sv.y = r.z.y - r.x.y;
         yv.x = g2.x - r.g.x;
         yv.y = g2.y - r.g.y;
-        st2h<MASK, NT>(so + vfi(i), sv, v0, v1);
-        st2h<MASK, NT>(yo + vfi(i), yv, v0, v1);
+        st2h<MASK, NT>(so + i, sv, v0, v1);
+        st2h<MASK, NT>(yo + i, yv, v0, v1);
         acc[LBK_VF_SY] = fma2<MASK>(sv, yv, acc[LBK_VF_SY], v0, v1);
         acc[LBK_VF_YY] = fma2<MASK>(yv, yv, acc[LBK_VF_YY], v0, v1);
         acc[LBK_VF_GG] = fma2<MASK>(g2, g2, acc[LBK_VF_GG], v0, v1);
@@ -2005,7 +1995,7 @@ __global__ __launch_bounds__(256) void k_vf_dir(double* __restrict__ d, const do
 #pragma unroll
         for (int l = 0; l < 2 * HB; ++l) {
             if (l < 2 * B.h) {
-                const double2 b = ldv<NT>(B.b[l] + vfi(i));
+                const double2 b = ldv<NT>(B.b[l] + i);
                 if (l == 0) {
                     v.x = B.c[0] * b.x;
                     v.y = B.c[0] * b.y;
@@ -2039,9 +2029,9 @@ __global__ void k_vf_edges(double* __restrict__ slot, const double* __restrict__
                            int g_hi) {
     if (threadIdx.x != 0) return;
     const double* v[4] = {x, g, s, y};
-    for (int k = 0; k < 4; ++k) {  // s, y in the vector-free history layout (vfi)
+    for (int k = 0; k < 4; ++k) {
         slot[g_lo * LBK_KW + LBK_VF_EDGE0 + k] = v[k] ? v[k][0] : 0.0;
-        slot[(g_hi - 1) * LBK_KW + LBK_VF_EDGE1 + k] = v[k] ? v[k][k >= 2 ? vfi(n_loc - 1) : n_loc - 1] : 0.0;
+        slot[(g_hi - 1) * LBK_KW + LBK_VF_EDGE1 + k] = v[k] ? v[k][n_loc - 1] : 0.0;
     }
 }
 
@@ -2052,8 +2042,8 @@ __global__ void k_vf_ghosts(const double* __restrict__ slot, double* x, double* 
     double* v[4] = {x, g, s, y};
     for (int k = 0; k < 4; ++k) {
         if (!v[k]) continue;
-        if (has_left) v[k][k >= 2 ? vfi(-1) : -1] = slot[(g_lo - 1) * LBK_KW + LBK_VF_EDGE1 + k];
-        if (has_right) v[k][k >= 2 ? vfi(n_loc) : n_loc] = slot[g_hi * LBK_KW + LBK_VF_EDGE0 + k];
+        if (has_left) v[k][-1] = slot[(g_lo - 1) * LBK_KW + LBK_VF_EDGE1 + k];
+        if (has_right) v[k][n_loc] = slot[g_hi * LBK_KW + LBK_VF_EDGE0 + k];
     }
 }
 

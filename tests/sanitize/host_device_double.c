@@ -170,22 +170,6 @@ void lbk_vec_free(lbk_ctx* c, double* v) {
     (void)c;
     if (v) free(v - DBL_FRONT);
 }
-/* the double keeps separate vectors (no paired vector-free rows) */
-int lbk_vf_paired(const lbk_ctx* c) {
-    (void)c;
-    return 0;
-}
-double* lbk_pair_alloc(lbk_ctx* c) {
-    snprintf(c->err, sizeof c->err, "double: no pair storage");
-    return NULL;
-}
-void lbk_pair_free(lbk_ctx* c, double* p) {
-    (void)c;
-    (void)p;
-}
-void lbk_pair_view(const lbk_ctx* c, double* p, int paired, double** s, double** y) {
-    (void)c, (void)p, (void)paired, (void)s, (void)y;
-}
 void* lbk_host_alloc(size_t bytes) { return malloc(bytes); }
 void lbk_host_free(void* p) { free(p); }
 int lbk_upload(lbk_ctx* c, double* dst, const double* h) {
