@@ -682,10 +682,15 @@ def reference_parity(traj, live, fixture, fsrc):
             out["live_reference_matches_fixture"] = bool(
                 np.array_equal(f64(fr["grad_norm"])[:k].view(np.uint64), rg[:k].view(np.uint64))
                 and np.array_equal(u64(fr["grad_c1"])[:k], rc1[:k]))
-    else:
+    elif "seq" in fixture:
         s = fixture["seq"]
         rf, rg, rc1, rc2 = f64(s["f"]), f64(s["gnorm"]), u64(s["c1"]), u64(s["c2"])
         out["reference"] = f"fixture: {fsrc} (the reference's own trace, tests/golden/make_fullsize.py)"
+    else:  # the reference at x0 only (configs[4]'s fixture: maxit 0, f and grad at x0)
+        r = fixture["reference"]
+        rf, rg = f64(r["f_calls"][:1]), f64(r["grad_norm"][:1])
+        rc1, rc2 = u64(r["grad_c1"][:1]), u64(r["grad_c2"][:1])
+        out["reference"] = f"fixture: {fsrc} (the reference's f and grad at x0, tests/golden/make_fullsize.py)"
     k = min(len(gf), len(rf))
     rel_f = np.abs(gf[:k] - rf[:k]) / np.maximum(np.abs(rf[:k]), 1e-300)
     rel_g = np.abs(gg[:k] - rg[:k]) / np.maximum(np.abs(rg[:k]), 1e-300)

@@ -179,3 +179,23 @@ def test_fullsize_fixture_lookup(bench):
     assert d is not None and src.endswith("config1_n1e7.json")
     assert bench.fullsize_fixture(a, 125_000_000) == (None, None)
     assert bench.fullsize_fixture(a, 50_000_000) == (None, None)
+
+
+def test_reference_parity_with_an_x0_only_fixture(bench):
+    """configs[4]'s fixture holds the reference at x0 only (no per-iteration trace): the line
+    compares that state and the canonical states instead of failing (KeyError 'seq', round 5)"""
+    import types
+
+    import numpy as np
+
+    a = types.SimpleNamespace(objective="rosenbrock", history=10, line_search="backtracking")
+    fx, src = bench.fullsize_fixture(a, 10 ** 9)
+    assert fx is not None and "seq" not in fx
+    c = fx["canon"]
+    f64 = lambda hs: np.array([int(h, 16) for h in hs], dtype=np.uint64).view(np.float64)  # noqa: E731
+    traj = {"tr_f": f64(c["f"]), "tr_gnorm": f64(c["gnorm"]), "tr_alpha": f64(c["alpha"] + ["0"]),
+            "tr_c1": np.array([int(v) for v in c["c1"]], dtype=np.uint64),
+            "tr_c2": np.array([int(v) for v in c["c2"]], dtype=np.uint64)}
+    out = bench.reference_parity(traj, None, fx, src)
+    assert out["iterations_compared"] == 1 and out["within_tolerance_iterations"]["f"] == 1
+    assert out["canonical"]["bit_exact"] is True
