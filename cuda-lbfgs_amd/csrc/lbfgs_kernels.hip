@@ -264,7 +264,7 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
     memset(c->wolfe_out_h, 0, sizeof(lbk_search));
     CK(hipHostGetDevicePointer((void**)&c->wolfe_out_d, c->wolfe_out_h, 0));
     {
-        const size_t llb = sizeof(unsigned long long) * 2 * LBK_KMAX * LBK_SEGS * LBK_COLL_WAVES;  // regular slots only
+        const size_t llb = sizeof(unsigned long long) * 2 * LBK_KMAX * LBK_SEGS;  // regular slots only
         CK(hipMalloc(&c->coll_ll, llb));
         CK(hipMemset(c->coll_ll, 0, llb));  // tag 0: no launch (tags start at 1)
     }

@@ -385,87 +385,6 @@ __device__ __forceinline__ void ll_load_batch(const unsigned long long* const (&
     for (int m = 0; m < M; ++m) out[m] = on[m] ? bitsd((w1[m] << 32) | (w0[m] & 0xffffffffull)) : 0.0;
 }
 
-// A/B (variant builds): collect mode with one flagged word per WAVE partial instead of per segment
-// partial - the producing workgroup then needs no LDS round and no barrier before its waves retire;
-// the collector forms each segment's ((w0 + w1) + (w2 + w3)) from the four words, the same bits
-#ifndef LBK_WAVE_PARTIALS
-#define LBK_WAVE_PARTIALS 0
-#endif
-#define LBK_COLL_WAVES (LBK_WAVE_PARTIALS ? 4 : 1)
-
-template <int K>
-__device__ __forceinline__ void collect_tree_waves(const Red& red, int64_t lbase, int64_t gseg0, int64_t nseg, int spg,
-                                                   double* slot_g, double* hslot_g, double (&lds)[4][K > 0 ? K : 1]) {
-    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    auto word = [&](int k, int64_t j, int v) { return red.ll + ((((int64_t)k * LBK_SEGS + lbase + j) * 4) + v) * 2; };
-    const int64_t nvalid = min((int64_t)spg, nseg - gseg0);
-    if (nvalid <= 64) {  // group_tree's short shape
-        constexpr int KQ = (K + 3) / 4;
-        const unsigned long long* pp[KQ * 4];
-        bool on[KQ * 4];
-        double p[KQ * 4];
-#pragma unroll
-        for (int i = 0; i < KQ; ++i) {
-            const int k = w + 4 * i;
-#pragma unroll
-            for (int v = 0; v < 4; ++v) {
-                on[4 * i + v] = k < K && lane < nvalid;
-                pp[4 * i + v] = on[4 * i + v] ? word(k, lane, v) : red.ll;
-            }
-        }
-        ll_load_batch<KQ * 4>(pp, on, red.seq, p, red.err, red.timeout);
-#pragma unroll
-        for (int i = 0; i < KQ; ++i) {
-            const int k = w + 4 * i;
-            const double seg = (p[4 * i] + p[4 * i + 1]) + (p[4 * i + 2] + p[4 * i + 3]);
-            const double v = wave_sum(seg) + 0.0;
-            if (k < K && lane == 0) {
-                slot_g[k] = v;
-                if (hslot_g) hslot_g[k] = v;
-            }
-        }
-        return;
-    }
-    double q[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-        double seg[4];
-#pragma unroll
-        for (int h2 = 0; h2 < 2; ++h2) {  // segments 4t + 2 h2, 4t + 2 h2 + 1: 8 words per batch
-            const unsigned long long* pp[8];
-            bool on[8];
-            double p[8];
-#pragma unroll
-            for (int e = 0; e < 2; ++e) {
-                const int64_t j = 4 * t + 2 * h2 + e;
-#pragma unroll
-                for (int v = 0; v < 4; ++v) {
-                    on[4 * e + v] = j < spg && gseg0 + j < nseg;
-                    pp[4 * e + v] = on[4 * e + v] ? word(k, j, v) : red.ll;
-                }
-            }
-            ll_load_batch<8>(pp, on, red.seq, p, red.err, red.timeout);
-            seg[2 * h2] = (p[0] + p[1]) + (p[2] + p[3]);
-            seg[2 * h2 + 1] = (p[4] + p[5]) + (p[6] + p[7]);
-        }
-        q[k] = wave_sum((seg[0] + seg[1]) + (seg[2] + seg[3]));
-    }
-    __syncthreads();  // lds reuse
-    if (lane == 0) {
-#pragma unroll
-        for (int k = 0; k < K; ++k) lds[w][k] = q[k];
-    }
-    __syncthreads();
-    if (t == 0) {
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const double v = (lds[0][k] + lds[1][k]) + (lds[2][k] + lds[3][k]);
-            slot_g[k] = v;
-            if (hslot_g) hslot_g[k] = v;
-        }
-    }
-}
-
 template <int K>
 __device__ __forceinline__ void collect_tree(const Red& red, int64_t lbase, int64_t gseg0, int64_t nseg, int spg,
                                              double* slot_g, double* hslot_g, double (&lds)[4][K > 0 ? K : 1]) {
@@ -547,25 +466,6 @@ __device__ __forceinline__ void reduce_publish(double (&acc)[K], const Geo& geo,
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
 #pragma unroll
     for (int k = 0; k < K; ++k) acc[k] = wave_sum(acc[k]);
-#if LBK_WAVE_PARTIALS
-    if constexpr (K <= LBK_KMAX) {
-        if (red.ll) {  // collect, per wave (see collect_tree_waves): no LDS round, no barrier
-            const int64_t bw = seg_block(geo);
-            if (lane == 0) {
-#pragma unroll
-                for (int k = 0; k < K; ++k) ll_store(red.ll + ((((int64_t)k * LBK_SEGS + bw) * 4) + w) * 2, acc[k], red.seq);
-            }
-            const int64_t sgw = geo.seg_lo + bw;
-            const int gw = (int)(sgw / geo.spg);
-            const int64_t gseg0 = (int64_t)gw * geo.spg;
-            const int64_t glast = min(geo.nseg, gseg0 + geo.spg) - 1;
-            if (sgw != (geo.rev ? gseg0 : glast)) return;  // uniform over the workgroup
-            collect_tree_waves<K>(red, gseg0 - geo.seg_lo, gseg0, geo.nseg, geo.spg, red.slot + gw * red.kstride,
-                                  red.hslot ? red.hslot + gw * red.kstride : nullptr, lds);
-            return;
-        }
-    }
-#endif
     if (lane == 0) {
 #pragma unroll
         for (int k = 0; k < K; ++k) lds[w][k] = acc[k];
