@@ -348,7 +348,8 @@ def cpu_model():
     return platform.processor() or "unknown"
 
 
-def measure(a, D, n, x0, dev, rank, world, uid, unfused=False, vector_free=False, box_probe=False):
+def measure(a, D, n, x0, dev, rank, world, uid, unfused=False, vector_free=False, box_probe=False,
+            defer_rccl=False):
     """W warm-up steps, then EXACTLY K timed steps (barrier + device sync on both sides, no
     instrumentation), then a separate event-instrumented pass for per-kernel durations.
 
@@ -367,12 +368,12 @@ def measure(a, D, n, x0, dev, rank, world, uid, unfused=False, vector_free=False
             ctx.close()
         raise err or L.LbfgsError("context creation failed on another rank")
     try:
-        return _measure(a, D, ctx, x0, rank, world, uid, unfused, vector_free, box_probe)
+        return _measure(a, D, ctx, x0, rank, world, uid, unfused, vector_free, box_probe, defer_rccl)
     finally:
         ctx.close()
 
 
-def _measure(a, D, ctx, x0, rank, world, uid, unfused, vector_free, box_probe):
+def _measure(a, D, ctx, x0, rank, world, uid, unfused, vector_free, box_probe, defer_rccl=False):
     failed = []  # this rank's first failure (sticky: later compute is skipped, collectives are not)
 
     def run(fn, *args, **kw):
@@ -467,27 +468,13 @@ def _measure(a, D, ctx, x0, rank, world, uid, unfused, vector_free, box_probe):
     lat = None
     if world > 1 and not vector_free and not unfused:
         lat = {}
-        if backend.startswith("xgmi") and uid is None and a.exchange == "auto":
+        uid_leg = uid is not None
+        if backend.startswith("xgmi") and uid is None and a.exchange == "auto" and not defer_rccl:
             # only now, with the measurement done: an RCCL communicator for the comparison leg
             lat["rccl_leg"] = rccl_leg(D, ctx, rank)
             uid_leg = lat["rccl_leg"]["ok"]
-        else:
-            uid_leg = uid is not None
         backends = (["xgmi"] if backend.startswith("xgmi") else []) + (["rccl"] if uid_leg else [])
-        for b in backends:
-            for k in (8, 96):
-                us = None
-                try:  # an RCCL wait is bounded in the library (LBFGS_RCCL_TIMEOUT): a stall costs this entry
-                    us = ctx.exchange_latency(b, k, 200) if not failed else None
-                except L.LbfgsError as e:
-                    if b != "rccl":
-                        failed.append(e)
-                    lat[f"{b}_{k * 8}doubles_error"] = str(e)
-                    print(f"rank {rank}: {b} exchange timing: {e}", file=sys.stderr, flush=True)
-                if b == "rccl" and not D.all_ok(us is not None):
-                    break  # a rank's RCCL timing failed: no rank enters another RCCL collective
-                if us is not None:
-                    lat[f"{b}_{k * 8}doubles"] = round(us, 2)
+        exchange_timings(D, ctx, rank, backends, lat, failed)
         vote("exchange latency")
     if trace:
         res["trajectory"] = ctx.trace()
@@ -496,6 +483,52 @@ def _measure(a, D, ctx, x0, rank, world, uid, unfused, vector_free, box_probe):
     res["box_probe"] = probe
     done_steps = a.steps if res["status"] == "running" else max(res["iterations"] - a.warmup - fill["iterations"], 1)
     return T, res, prof, bytes_all, done_steps, (backend, lat)
+
+
+def exchange_timings(D, ctx, rank, backends, lat, failed):
+    """200 back-to-back exchanges of 8 and 96 doubles per backend into lat (collective: every rank
+    makes the same calls); an RCCL wait is bounded in the library (LBFGS_RCCL_TIMEOUT), a stall
+    costs its entry, and a failed RCCL timing on any rank stops every rank's RCCL timings"""
+    for b in backends:
+        for k in (8, 96):
+            us = None
+            try:
+                us = ctx.exchange_latency(b, k, 200) if not failed else None
+            except L.LbfgsError as e:
+                if b != "rccl":
+                    failed.append(e)
+                lat[f"{b}_{k * 8}doubles_error"] = str(e)
+                print(f"rank {rank}: {b} exchange timing: {e}", file=sys.stderr, flush=True)
+            if b == "rccl" and not D.all_ok(us is not None):
+                break  # a rank's RCCL timing failed: no rank enters another RCCL collective
+            if us is not None:
+                lat[f"{b}_{k * 8}doubles"] = round(us, 2)
+
+
+def rccl_comparison(a, D, n, dev, rank, world):
+    """The RCCL leg last (round 5): after every measurement of the run - the headline, the
+    vector-free line, configs[4] - a fresh sharded context (no RCCL id, its vectors untouched)
+    takes an RCCL communicator (rccl_leg) and times the RCCL exchanges beside the mailboxes'. On one
+    card the init attempt of 8 processes (RCCL refuses two ranks on one device) left a later large
+    solve at half speed; nothing measured comes after it now. Returns the entries
+    for the headline's exchange_latency_us."""
+    out, ctx, err = {}, None, None
+    try:
+        ctx = L.Context(n, a.history, device=dev, rank=rank, world=world, uid=None)
+    except L.LbfgsError as e:
+        err = str(e)
+    if not D.all_ok(ctx is not None):
+        if ctx is not None:
+            ctx.close()
+        return {"rccl_leg": {"ok": False, "errors": [err or "context creation failed on another rank"]}}
+    try:
+        out["rccl_leg"] = rccl_leg(D, ctx, rank)
+        failed = []
+        if out["rccl_leg"]["ok"]:
+            exchange_timings(D, ctx, rank, ["rccl"], out, failed)
+    finally:
+        ctx.close()
+    return out
 
 
 RCCL_ABANDONED = False
@@ -535,7 +568,7 @@ def rccl_leg(D, ctx, rank):
     errs = [e for e in D.allgather_bytes(err or "") if e]
     return {"ok": ok, "init_s": round(time.perf_counter() - t0, 2),
             "errors": errs[:4] or None,
-            "note": "RCCL communicator created after the measurement (non-blocking init, bounded wait)"}
+            "note": "RCCL communicator created after every measurement of the run (non-blocking init, bounded wait)"}
 
 
 def shard_check(a, D, n, x0, dev, rank, world, res):
@@ -831,7 +864,8 @@ def main():
     fallback = None
     try:
         T, res, prof, bytes_all, done_steps, (backend, xlat) = measure(a, D, n, x0, dev, rank, world, uid,
-                                                      unfused=a.unfused, vector_free=a.vector_free, box_probe=True)
+                                                      unfused=a.unfused, vector_free=a.vector_free, box_probe=True,
+                                                      defer_rccl=True)
     except L.LbfgsError as e:
         # a mailbox failure across GPUs: measure() raises on every rank together (its votes), so
         # every rank lands here and the line is measured again over RCCL rather than lost, and
@@ -871,6 +905,9 @@ def main():
     c4 = None
     if world == 8 and n == 10 ** 8 and not (a.unfused or a.vector_free or a.no_config4):
         c4 = config4(a, D, dev, rank, world)
+    # the RCCL comparison leg after everything measured (rccl_comparison)
+    if xlat is not None and fallback is None and backend.startswith("xgmi") and uid is None and a.exchange == "auto":
+        xlat.update(rccl_comparison(a, D, n, dev, rank, world))
 
     out = None
     if rank == 0:

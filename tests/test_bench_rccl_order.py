@@ -2,7 +2,8 @@
 ranks run bench.measure() over a stub Context that records every call. The measurement runs on
 the peer mailboxes with no RCCL communicator; the communicator is created only afterwards
 (rccl_leg), and a failed or stalled init there is reported in the line instead of losing it:
-no rank enters an RCCL exchange unless every rank's init succeeded."""
+no rank enters an RCCL exchange unless every rank's init succeeded. As main() runs it (`_late`),
+the leg comes after every measurement of the run, on a context of its own (rccl_comparison)."""
 import os
 import socket
 import sys
@@ -86,10 +87,12 @@ class StubContext:
         StubContext.log.append(("close",))
 
 
-def _worker(rank, world, port, mode, q):
+def _worker(rank, world, port, mode_arg, q):
+    mode = mode_arg
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(port))
     os.environ.pop("BENCH_RCCL_STALL", None)
+    mode = mode.replace("_late", "") if mode.endswith("_late") else mode
     if mode == "stall":
         os.environ["BENCH_RCCL_STALL"] = "0"  # rank 0 never joins; rank 1's bounded init times out
         if rank == 1:
@@ -103,7 +106,12 @@ def _worker(rank, world, port, mode, q):
     bench.L.unique_id = lambda: bytes(128)
     a = bench.parse(["--gpus", str(world), "--steps", "5", "--warmup", "2"])
     D = bench.Dist(world)
-    T, res, prof, bytes_all, steps, (backend, lat) = bench.measure(a, D, 10 ** 8, None, 0, rank, world, None)
+    late = mode_arg.endswith("_late")
+    T, res, prof, bytes_all, steps, (backend, lat) = bench.measure(a, D, 10 ** 8, None, 0, rank, world, None,
+                                                                   defer_rccl=late)
+    if late:  # main()'s order: the leg after every measurement, on a context of its own
+        StubContext.log.append(("measurements done",))
+        lat.update(bench.rccl_comparison(a, D, 10 ** 8, 0, rank, world))
     D.close()
     q.put((rank, StubContext.log, backend, lat, steps))
 
@@ -123,9 +131,11 @@ def _run(mode, world=2):
     return out
 
 
-@pytest.mark.parametrize("mode", ["ok", "fail", "stall"])
+@pytest.mark.parametrize("mode", ["ok", "fail", "stall", "ok_late", "fail_late", "stall_late"])
 def test_rccl_created_after_the_measurement(mode):
     out = _run(mode)
+    late = mode.endswith("_late")
+    mode = mode.replace("_late", "")
     for rank, log, backend, lat, steps in out:
         assert backend == "xgmi+fold" and steps == 5
         assert log[0] == ("create", False)  # the measurement's context has no RCCL id
@@ -134,6 +144,11 @@ def test_rccl_created_after_the_measurement(mode):
         assert joined == (mode != "stall" or rank != 0)
         if joined:
             assert log.index(("rccl_attach",)) > timed  # the communicator only after the timed steps
+        if late:  # ... and, as main() runs it, only after every measurement, on its own context
+            done = log.index(("measurements done",))
+            assert log[done + 1] == ("create", False)
+            assert all(e != ("rccl_attach",) for e in log[:done])
+            assert log[-1] == ("close",)
         rccl_timings = [e for e in log if e == ("exchange_latency", "rccl")]
         leg = lat["rccl_leg"]
         if mode == "ok":
