@@ -20,6 +20,15 @@ def rows_of(path):
         return sorted(csv.DictReader(io.StringIO(fp.read())), key=lambda r: int(r["Start_Timestamp"]))
 
 
+def series(its):
+    """the whole block's iteration times: mean of each tenth, in order (drift over the solve)"""
+    if len(its) < 20:
+        return ""
+    k = len(its) // 10
+    return f"; {len(its)} iterations, mean per tenth (ms): " + " ".join(
+        f"{sum(its[i * k:(i + 1) * k]) / k:.1f}" for i in range(10))
+
+
 def main():
     d = sys.argv[1]
     tail = int(sys.argv[2]) if len(sys.argv) > 2 else 5
@@ -41,8 +50,11 @@ def main():
         for bi, blk in enumerate(blocks):
             gaps = [(b - a) / 1e6 for a, b in zip(blk, blk[1:])]
             # an iteration whose first step was rejected has a second (re)commit a few ms after the
-            # first: iteration times are the gaps between first commits (gaps > 20 ms here)
-            its = [g for g in gaps if g > 20.0][-tail:]
+            # first: iteration times are the gaps between first commits (gaps above 0.3x the block's
+            # upper quartile)
+            q3 = sorted(gaps)[3 * len(gaps) // 4] if gaps else 0.0
+            every = [g for g in gaps if g > 0.3 * q3]
+            its = every[-tail:]
             med = sorted(its)[len(its) // 2] if its else 0.0
             lo, hi = blk[0], blk[-1]
             ex = [r for r in rows if "xgmi" in r["Kernel_Name"] and lo <= int(r["Start_Timestamp"]) <= hi]
@@ -50,7 +62,7 @@ def main():
             out.append(f"block {bi}: {len(blk)} commits over {(hi - lo) / 1e6:.1f} ms; last {len(its)} iterations "
                        f"median {med:.1f} ms ({1e3 / med if med else 0:.2f} it/s; "
                        f"{', '.join(f'{g:.1f}' for g in its)}); exchange kernels {len(ex)}, {ex_ms:.1f} ms "
-                       f"({100 * ex_ms / max((hi - lo) / 1e6, 1e-9):.1f} %)")
+                       f"({100 * ex_ms / max((hi - lo) / 1e6, 1e-9):.1f} %)" + series(every))
         print(os.path.basename(f).split("_")[0], "|", " || ".join(out))
 
 
