@@ -5,6 +5,21 @@
 #include <atomic>
 #include <thread>
 
+// A slot the host reads whose launch leaves no completion word (stage 2 in several groups, the
+// sharded exchange): this launch, queued behind everything issued so far, copies the slot from
+// the device to its host mirror and then stores the epoch word the host polls (small_wait).
+// Waiting on the stream instead (hipStreamSynchronize) registers an asynchronous handler with
+// the runtime on every call, and the runtime thread serving them spins: ~1 core per process
+// beside the waiting thread (tools/thread_probe.py, profiles/r05/config4_cpu/; eight such ranks
+// exhausted a 16-CPU quota and configs[4] ran at half speed on one card).
+__global__ __launch_bounds__(256) void k_slot_publish(const double* __restrict__ src, double* dst, int n,
+                                                      unsigned long long* word, unsigned long long epoch) {
+    for (int i = (int)threadIdx.x; i < n; i += 256) dst[i] = src[i];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(word, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 extern "C" {
 
 void xfer_pool_free(lbk_ctx* c);  // staged transfers' pinned pool (below)
@@ -1210,12 +1225,22 @@ int lbk_search_dev(lbk_ctx* c, int obj, int ls, const double* x, const double* d
 
 // spin on the pinned completion word; every 64k polls ask the stream whether it still runs (a
 // faulted or finished stream with the word unset ends the wait with the stream's error)
+// A hipStreamQuery on a busy stream keeps one of the runtime's own threads spinning beside the
+// waiting one, and more so the more queries are outstanding (tools/query_probe.hip: 0.6-0.9 of a
+// core; profiles/r05/config4_cpu/: eight such ranks on one box exhausted its 16-CPU quota and
+// configs[4] ran at half speed). The stream is asked only once a wait has lasted 0.25 s - a
+// launch that faulted or never wrote its record - never on the way to a normal completion.
 static int small_wait(lbk_ctx* c, unsigned long long epoch, int word = 0) {
     const volatile unsigned long long* done = c->sp_h + word;
+    double t_query = 0.0;
     for (unsigned long it = 1;; ++it) {
         if (__atomic_load_n(const_cast<unsigned long long*>(done), __ATOMIC_ACQUIRE) >= epoch) return 0;
         if ((it & 0xffff) == 0) {
             if (*(volatile unsigned*)c->coop_err_h) break;
+            const double now = mono_s();
+            if (t_query == 0.0) t_query = now + 0.25;
+            if (now < t_query) continue;
+            t_query = now + 0.25;
             const hipError_t q = hipStreamQuery(c->stream);
             if (q == hipErrorNotReady) continue;
             if (__atomic_load_n(const_cast<unsigned long long*>(done), __ATOMIC_ACQUIRE) >= epoch) return 0;
@@ -1422,9 +1447,20 @@ int lbk_fetch_groups(lbk_ctx* c, int slot, double* groups64) {
         memcpy(groups64, h, bytes);
         return 0;
     }
-    if (!c->slot_mirror[slot < LBK_NSLOTS ? slot : LBK_NSLOTS + slot - LBK_WSLOT0])
-        HIPCHK(c, hipMemcpyAsync(h, slot_base(c, slot), bytes, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (!c->comm && !c->grp) {
+        // behind everything queued so far, as a stream synchronisation would wait for, but polled
+        // on a completion word (k_slot_publish)
+        double* hd = slot < LBK_NSLOTS ? c->dh_slots + (int64_t)slot * LBK_SLOT
+                                       : c->dh_wslots + (int64_t)(slot - LBK_WSLOT0) * LBK_WSLOT;
+        hipLaunchKernelGGL(k_slot_publish, dim3(1), dim3(256), 0, c->stream, (const double*)slot_base(c, slot), hd,
+                           (int)(LBK_GROUPS * slot_stride(slot)), c->sp_dh + 2, ++c->pub_epoch);
+        HIPCHK(c, hipGetLastError());
+        const int rc = small_wait(c, c->pub_epoch, 2);
+        if (rc) return rc;
+    } else {
+        if (!c->slot_mirror[si]) HIPCHK(c, hipMemcpyAsync(h, slot_base(c, slot), bytes, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
     if (c->xg_on && lbk_xgmi_failed(c->xg)) {
         snprintf(c->err, sizeof c->err, "xgmi exchange timed out waiting for a peer");
         return -3;

@@ -3123,6 +3123,8 @@ struct lbk_ctx {
     // slot the epoch of the launch that last wrote its mirror (0: none, fetch synchronises)
     unsigned long long s2_epoch;
     unsigned long long slot_s2[LBK_NSLOTS + LBK_NWSLOTS];
+    // a slot fetch without one: k_slot_publish's epoch (sp_h[2]), the last issued
+    unsigned long long pub_epoch;
     double *dq_A, *dq_b, *dq_t;  // dense quadratic objective (lbk_dense_set): A (n x n), b, terms
     // folded exchanges (sharded over the mailboxes; LBFGS_XGMI_FOLD=0: off): the two-loop's
     // single-component reductions travel from the producing pass straight into the consuming pass
