@@ -100,6 +100,13 @@ def self_launch(argv, world, timeout, script=None):
     base = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world),
                 LOCAL_WORLD_SIZE=str(world))
     base.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC for the peer mailboxes / RCCL
+    if "BENCH_DEVICE_MOD" in base:
+        # several ranks on one card (a rehearsal): one unmasked hardware queue per rank, its
+        # CU-masked solver queue on top. With the runtime's default each rank holds 3 compute
+        # queues and rank 0's one-GPU check adds a 25th on the card, past what its scheduler maps
+        # at once: the ranks' passes then run in turns (configs[4] 2.5-5 it/s instead of 8.7;
+        # DESIGN.md §5, profiles/r05/config4_queues/). One process per GPU never gets near that.
+        base.setdefault("GPU_MAX_HW_QUEUES", "1")
 
     def stop(reason):
         alive = [p for p in procs if p.poll() is None]

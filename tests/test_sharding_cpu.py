@@ -97,17 +97,20 @@ D.barrier()
 tmax = D.allreduce(float(rank), "max")
 if rank == 0:
     print(json.dumps({{"world": world, "tmax": tmax, "local_rank": os.environ["LOCAL_RANK"],
-                      "master": os.environ["MASTER_ADDR"], "argv": sys.argv[1:]}}), flush=True)
+                      "master": os.environ["MASTER_ADDR"], "argv": sys.argv[1:],
+                      "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES")}}), flush=True)
 D.close()
 '''
 
 
-def _launch(tmp_path, world, mode, timeout=120.0):
+def _launch(tmp_path, world, mode, timeout=120.0, extra_env=None):
     import subprocess
 
     stub = tmp_path / "stub_rank.py"
     stub.write_text(STUB.format(root=ROOT))
-    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_PORT")}
+    drop = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_PORT", "GPU_MAX_HW_QUEUES", "BENCH_DEVICE_MOD")
+    env = {k: v for k, v in os.environ.items() if k not in drop}
+    env.update(extra_env or {})
     code = (f"import sys; sys.path.insert(0, {ROOT!r}); import bench; "
             f"sys.exit(bench.self_launch([{mode!r}], {world}, {timeout}, script={str(stub)!r}))")
     return subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=180)
@@ -125,7 +128,22 @@ def test_bench_self_launch_starts_ranks(tmp_path, world):
     lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
     assert len(lines) == 1, p.stdout
     d = json.loads(lines[0])
-    assert d == {"world": world, "tmax": float(world - 1), "local_rank": "0", "master": "127.0.0.1", "argv": ["ok"]}
+    assert d == {"world": world, "tmax": float(world - 1), "local_rank": "0", "master": "127.0.0.1", "argv": ["ok"],
+                 "hw_queues": None}
+
+
+def test_bench_self_launch_rehearsal_holds_ranks_to_one_unmasked_queue(tmp_path):
+    """several ranks on one card (BENCH_DEVICE_MOD): each rank gets GPU_MAX_HW_QUEUES=1, so the
+    card holds 2 compute queues per rank instead of 3 and stays under what its scheduler maps at
+    once (DESIGN.md §5, configs[4] on one card); a value the caller set is kept"""
+    import json
+
+    p = _launch(tmp_path, 2, "ok", extra_env={"BENCH_DEVICE_MOD": "1"})
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert json.loads(p.stdout.strip().splitlines()[-1])["hw_queues"] == "1"
+    p = _launch(tmp_path, 2, "ok", extra_env={"BENCH_DEVICE_MOD": "1", "GPU_MAX_HW_QUEUES": "2"})
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert json.loads(p.stdout.strip().splitlines()[-1])["hw_queues"] == "2"
 
 
 def test_bench_self_launch_stops_on_a_failed_rank(tmp_path):
