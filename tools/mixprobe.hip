@@ -60,7 +60,11 @@ __device__ __forceinline__ void st(double* p, dvec2 v) {
 // blocks of IL rows of 128 elements alternating between them
 // RUN: wave w takes the contiguous rows [w R, (w + 1) R), R = ceil(rows / 4) (the vector-free
 // commit's ORC_CANON_VF walk) instead of rows 4u + w
-template <int NR, int NW, int U, bool LNT, bool SNT, int TWL, int TWS, bool INPL, int IL = 0, bool RUN = false>
+// TAIL: the end of a product pass's workgroup (reduce_publish): 1 - wave butterflies, the four wave
+// sums through LDS, a barrier and one plain store of the segment's partial; 2 - the same with the
+// partial stored write-through at agent scope (the ticket / collect forms' stores)
+template <int NR, int NW, int U, bool LNT, bool SNT, int TWL, int TWS, bool INPL, int IL = 0, bool RUN = false,
+          int TAIL = 0>
 __global__ __launch_bounds__(256) void k_mix(Vecs v, int64_t n, int64_t L, int rev, double* sink) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int64_t seg = rev ? (int64_t)gridDim.x - 1 - blockIdx.x : blockIdx.x;
@@ -107,7 +111,24 @@ __global__ __launch_bounds__(256) void k_mix(Vecs v, int64_t n, int64_t L, int r
             }
         }
     }
-    if (acc == 1234.5678) sink[0] = acc;
+    if constexpr (TAIL > 0) {
+        __shared__ double wl[4];
+        double a = acc;
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) a += __shfl_xor(a, m, 64);
+        if (lane == 0) wl[w] = a;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const double p = (wl[0] + wl[1]) + (wl[2] + wl[3]);
+            if (TAIL == 1)
+                sink[seg] = p;
+            else
+                __hip_atomic_store(reinterpret_cast<unsigned long long*>(sink + seg), __double_as_longlong(p),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    } else {
+        if (acc == 1234.5678) sink[0] = acc;
+    }
 }
 
 struct Case {
@@ -120,9 +141,9 @@ struct Case {
 // LDSK > 0: LDSK KiB of dynamic LDS per workgroup (caps the workgroups per CU: 60 KiB -> 2, the
 // vector-free commit's occupancy of 2 waves per SIMD)
 template <int NR, int NW, int U, bool LNT, bool SNT, int TWL, int TWS, bool INPL, int IL = 0, bool RUN = false,
-          int LDSK = 0>
+          int LDSK = 0, int TAIL = 0>
 void launch(Vecs v, int64_t n, int64_t L, int nseg, int rev, double* sink) {
-    hipLaunchKernelGGL((k_mix<NR, NW, U, LNT, SNT, TWL, TWS, INPL, IL, RUN>), dim3(nseg), dim3(256), LDSK * 1024, 0, v,
+    hipLaunchKernelGGL((k_mix<NR, NW, U, LNT, SNT, TWL, TWS, INPL, IL, RUN, TAIL>), dim3(nseg), dim3(256), LDSK * 1024, 0, v,
                        n, L, rev, sink);
 }
 
@@ -140,7 +161,7 @@ int main(int argc, char** argv) {
         CK(hipMemset(bufs[k], 0, sizeof(double) * npad));
     }
     double* sink;
-    CK(hipMalloc(&sink, 64));
+    CK(hipMalloc(&sink, std::max<size_t>(64, sizeof(double) * (size_t)nseg)));  // TAIL: one partial per segment
     double* pair;
     CK(hipMalloc(&pair, sizeof(double) * 2 * npad));
     CK(hipMemset(pair, 0, sizeof(double) * 2 * npad));
@@ -176,6 +197,11 @@ int main(int argc, char** argv) {
         {"commit_4r4w_u4_allnt", 4, 4, launch<4, 4, 4, true, true, 0, 0, false>, false},
         {"mid_2r1w_u8_alt", 2, 1, launch<2, 1, 8, true, true, 1, 1, false>, true},
         {"axpy_3r1w_u4_alt", 3, 1, launch<3, 1, 4, true, true, 1, 1, true>, true},
+        // the workgroup's reduction tail of the product pass (TAIL 1: plain store, 2: write-through)
+        {"axpy_3r1w_u4_tail1", 3, 1, launch<3, 1, 4, true, true, 1, 1, true, 0, false, 0, 1>, false},
+        {"axpy_3r1w_u4_tail2", 3, 1, launch<3, 1, 4, true, true, 1, 1, true, 0, false, 0, 2>, false},
+        {"axpy_3r1w_u4_tail1_alt", 3, 1, launch<3, 1, 4, true, true, 1, 1, true, 0, false, 0, 1>, true},
+        {"axpy_3r1w_u4_tail2_alt", 3, 1, launch<3, 1, 4, true, true, 1, 1, true, 0, false, 0, 2>, true},
         {"commit_4r4w_u4_alt", 4, 4, launch<4, 4, 4, true, true, 1, 0, false>, true},
         // s_i / y_{i+1} interleaved in one buffer (blocks of 1, 4, 16, 96 rows), q in place
         {"axpy_3r1w_u4_il1", 3, 1, launch<3, 1, 4, true, true, 1, 1, true, 1>, false},
