@@ -106,7 +106,8 @@ def self_launch(argv, world, timeout, script=None):
         # queues and rank 0's one-GPU check adds a 25th on the card, past what its scheduler maps
         # at once: the ranks' passes then run in turns (configs[4] 2.5-5 it/s instead of 8.7;
         # DESIGN.md §5, profiles/r05/config4_queues/). One process per GPU never gets near that.
-        base.setdefault("GPU_MAX_HW_QUEUES", "1")
+        # (Set, not defaulted: the runtime's default, 4, is often already in the environment.)
+        base["GPU_MAX_HW_QUEUES"] = "1"
 
     def stop(reason):
         alive = [p for p in procs if p.poll() is None]
