@@ -2,4 +2,4 @@
 # oracle's canonical restatement, bit for bit
 set -o pipefail
 cd /root/repo && mkdir -p gpurun_out/soak
-timeout -k 10 800 python -u tools/fetch_soak.py 30 gpurun_out/soak/fetch_soak_30.json > gpurun_out/soak/fetch_soak.txt 2>&1
+timeout -k 10 800 python -u tools/fetch_soak.py 150 gpurun_out/soak/fetch_soak_150.json > gpurun_out/soak/fetch_soak.txt 2>&1
