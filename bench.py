@@ -61,6 +61,10 @@ def parse(argv=None):
                    help="one launch per BLAS-1 op (BASELINE configs[1] shape), same iterates")
     p.add_argument("--vector-free", action="store_true",
                    help="Gram-matrix two-loop, one fused pass per iteration (opt-in mode)")
+    p.add_argument("--no-persistent", action="store_true",
+                   help="skip the persistent-block two-loop line (LBFGS_PERSIST=2) beside the default")
+    p.add_argument("--persistent", action="store_true",
+                   help="measure the headline itself with the persistent-block two-loop (LBFGS_PERSIST=2)")
     p.add_argument("--no-vector-free", action="store_true",
                    help="skip the vector-free measurement reported beside the default mode")
     p.add_argument("--no-config4", action="store_true",
@@ -845,6 +849,8 @@ def main():
     # load liblbfgs_hip.so (and through it /opt/rocm's HIP runtime and RCCL) before torch can load
     # its bundled copies: libraries with the same soname are then shared, not duplicated
     L.lib()
+    if a.persistent:  # read by every context this process creates (lbk_create)
+        os.environ["LBFGS_PERSIST"] = "2"
     n = int(a.size)
     D = Dist(a.gpus)
     world, rank = a.gpus, D.rank
@@ -909,6 +915,36 @@ def main():
                               "(tests/test_gpu_vector_free.py)"))
         except L.LbfgsError as e:
             vf = {"error": str(e)}
+    # BASELINE configs[2] names the "fused persistent-block two-loop": the same steps with the
+    # two-loop's 2h - 1 passes in one resident launch per iteration (k_persist_twoloop,
+    # LBFGS_PERSIST=2; one GPU), beside the launch sequence on the same box, with its trajectory
+    # checked bit for bit against the default run's
+    pers = None
+    if world == 1 and not (a.unfused or a.vector_free or a.no_persistent or a.persistent):
+        prev = os.environ.get("LBFGS_PERSIST")
+        os.environ["LBFGS_PERSIST"] = "2"
+        try:
+            Tp, rp, pp, bp, dp, _ = measure(a, D, n, x0, dev, rank, world, None)
+            same = None
+            if res.get("trajectory") is not None and rp.get("trajectory") is not None:
+                ta, tb = res["trajectory"], rp["trajectory"]
+                k = min(len(ta["tr_f"]), len(tb["tr_f"]))
+                same = bool(k > 0 and all(np.array_equal(ta[key][:k].view(np.uint64), tb[key][:k].view(np.uint64))
+                                          for key in ("tr_f", "tr_gnorm", "tr_c1", "tr_c2")))
+            pers = dict(value=round(dp / Tp, 4), ms_per_step=round(Tp / dp * 1e3, 4), steps=dp,
+                        vs_default=round((dp / Tp) / (done_steps / T), 4),
+                        achieved_hbm_gbps=round(bp / Tp / 1e9, 1), roofline=roofline(pp, n, world),
+                        kernel="k_persist_twoloop (LBFGS_PERSIST=2): the 2h - 1 two-loop passes in one launch",
+                        launches_persistent=(pp.get("small_iter") or {}).get("launches"),
+                        trajectory_bit_identical_to_default=same,
+                        solver={"status": rp["status"], "f": rp["f"], "gnorm": rp["gnorm"], "passes": rp["passes"]})
+        except L.LbfgsError as e:
+            pers = {"error": str(e)}
+        finally:
+            if prev is None:
+                os.environ.pop("LBFGS_PERSIST", None)
+            else:
+                os.environ["LBFGS_PERSIST"] = prev
     del x0
     c4 = None
     if world == 8 and n == 10 ** 8 and not (a.unfused or a.vector_free or a.no_config4):
@@ -969,9 +1005,11 @@ def main():
             "config": {"workload": (f"{a.objective} n={n:.0e} m={a.history} {a.line_search}, "
                                     f"{'sharded over ' + str(world) + ' GPUs' if world > 1 else 'one GPU'}"
                                     + (", unfused per-vector kernels" if a.unfused else
-                                       ", vector-free (Gram-matrix) mode" if a.vector_free else ", fused passes")
+                                       ", vector-free (Gram-matrix) mode" if a.vector_free else
+                                       ", persistent-block fused two-loop" if a.persistent else ", fused passes")
                                     + (" (BASELINE configs[2])" if n == 10 ** 8 else "")),
-                       "kernels": "unfused" if a.unfused else "vector_free" if a.vector_free else "fused",
+                       "kernels": ("unfused" if a.unfused else "vector_free" if a.vector_free else
+                                   "persistent" if a.persistent else "fused"),
                        "n": n, "m": a.history, "line_search": a.line_search,
                        "parallelism": f"shard{world}" if world > 1 else "single",
                        "exchange": backend},
@@ -992,6 +1030,7 @@ def main():
                        "passes": res["passes"]},
             "shard_check": check,
             "vector_free": vf,
+            "persistent": pers,
             "config4_n1e9": c4,
             "build": dict(zip(("library", "tree_sources", "current"), L.build_info())),
         }

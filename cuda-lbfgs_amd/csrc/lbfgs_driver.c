@@ -481,14 +481,18 @@ int lbfgs_coop_info(const lbfgs_ctx* c, int* coop_max, int* search_max, int* fal
 }
 
 int lbfgs_stream_probe(lbfgs_ctx* c, int launches, double* us, double* bytes) {
-    if (!c || !us || launches < 1) return LBFGS_ERR_BAD_ARG;
+    return lbfgs_stream_probe_variant(c, 0, launches, us, bytes);
+}
+
+int lbfgs_stream_probe_variant(lbfgs_ctx* c, int variant, int launches, double* us, double* bytes) {
+    if (!c || !us || launches < 1 || variant < 0 || variant > 5) return LBFGS_ERR_BAD_ARG;
     if (!c->inited) return LBFGS_ERR_STATE;
     /* the written operand is a scratch vector, not the solver's q: nothing of the solve is touched
      * (q - 0 * y is q only while y is finite) */
     double* scratch = lbk_vec_alloc(c->dev);
     if (!scratch) return dev_err(c, -2);
     const int rc = lbk_stream_probe(c->dev, scratch, (const double* const*)c->Y, (const double* const*)c->S, c->m + 1,
-                                    launches, us);
+                                    launches, us, variant);
     lbk_vec_free(c->dev, scratch);
     if (rc != 0) return dev_err(c, rc);
     if (bytes) *bytes = 32.0 * (double)c->geo->n_loc;

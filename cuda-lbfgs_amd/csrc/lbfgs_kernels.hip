@@ -128,16 +128,6 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
     c->ticket_env = -1;
     if (const char* e = getenv("LBFGS_TICKET")) c->ticket = c->ticket_env = atoi(e) != 0;
     c->vec_doubles = LBK_FRONT + ((G.n_loc + 511) / 512) * 512 + 512;
-    // small n: the whole two-loop + commit in one single-workgroup launch (LBFGS_SMALL_SEGS=N
-    // enables it for nseg <= N). Measured 1.8x slower at n=1e4 and 5x at 3e4 than the launch
-    // sequence (profiles/r01/small_persistent.txt): one workgroup pays an L2 round trip per
-    // segment step, more than the kernel boundaries it removes. Off by default.
-    // (variant builds only: -DLBK_SMALL_SEGS=<segments>, tools/build_variant.sh)
-#ifdef LBK_SMALL_SEGS
-    c->small_seg_max = LBK_SMALL_SEGS;
-#else
-    c->small_seg_max = 0;
-#endif
     // measured (profiles/r01/coop_ab.txt): +48 % at n = 1e4 (14-15k -> 22k it/s), +41 % at 3e4,
     // +22 % at 1e5 (196 segments); -22 % at 391 segments and -38 % at 508, where the barrier's
     // fan-in and every workgroup's read of all partials outweigh the saved launches. Bit-identical
@@ -162,6 +152,7 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
     if (const char* e = getenv("LBFGS_SEARCH_TIMEOUT")) c->search_timeout_s = std::max(0.0, atof(e));
     c->rccl_timeout_s = 60.0;
     if (const char* e = getenv("LBFGS_RCCL_TIMEOUT")) c->rccl_timeout_s = std::max(0.5, atof(e));
+    if (const char* e = getenv("LBFGS_DEBUG_RCCL_STALL_MS")) c->rccl_stall_ms = std::max(0.0, atof(e));
     c->pend_slot = -1;
     c->xf_slot = -1;
     // folded exchanges over the mailboxes: 1 (default) when every peer has a GPU of
@@ -190,14 +181,6 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
     // sharded slots are completed by the exchange on the device: those fetch with a copy
     c->direct = world == 1 ? 1 : 0;
     if (const char* e = getenv("LBFGS_DIRECT")) c->direct = world == 1 && atoi(e) != 0;
-    // measured neutral in 4-rank rehearsals on one GPU (profiles/r01/xgmi_mirror_ab.txt), where
-    // the ranks share the card; the saved copy is ~1 % of an 8-GPU iteration at best: variant
-    // builds only (-DLBK_XGMI_MIRROR=1)
-#ifdef LBK_XGMI_MIRROR
-    c->xg_mirror = LBK_XGMI_MIRROR;
-#else
-    c->xg_mirror = 0;
-#endif
     *out = c;
 #define CK(expr)                                                                             \
     do {                                                                                     \
@@ -432,7 +415,6 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
         c->direct = 0;
         c->coop_max = 0;
         c->wolfe_max = 0;
-        c->small_seg_max = 0;
     }
     if (!grp && nccl_id) return rccl_init(c, nccl_id);
     return 0;
@@ -444,13 +426,17 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
 // RCCL the call itself blocked in its bootstrap when a peer never joined, profiles/r05/rccl_leg/.)
 // On a timeout the thread is abandoned, still waiting inside RCCL, and ends with the process.
 namespace {
+// One state word decides who owns the finished communicator and the job: the helper thread moves
+// RUNNING -> DONE when the init returns (the caller then takes both), the caller moves RUNNING ->
+// ABANDONED when its wait runs out (the thread then aborts the communicator and frees the job).
+// Exactly one of the two compare-exchanges succeeds.
+enum { RCCL_JOB_RUNNING = 0, RCCL_JOB_DONE = 1, RCCL_JOB_ABANDONED = 2 };
 struct RcclInitJob {
     ncclUniqueId id;
     int device, world, rank;
     ncclComm_t comm = nullptr;
     ncclResult_t r = ncclInProgress;
-    std::atomic<int> done{0};
-    std::atomic<int> abandoned{0};
+    std::atomic<int> state{RCCL_JOB_RUNNING};
 };
 }  // namespace
 
@@ -470,9 +456,11 @@ static int rccl_init(lbk_ctx* c, const void* nccl_id) {
             const ncclResult_t r = ncclCommInitRankConfig(&comm, job->world, job->id, job->rank, &cfg);
             job->comm = comm;
             job->r = r;
-            job->done.store(1, std::memory_order_release);
-            if (job->abandoned.load(std::memory_order_acquire)) {  // the caller gave up: nobody owns it
+            int expect = RCCL_JOB_RUNNING;
+            if (!job->state.compare_exchange_strong(expect, RCCL_JOB_DONE, std::memory_order_acq_rel)) {
+                // the caller gave up (ABANDONED): this thread owns the communicator and the job
                 if (comm) (void)ncclCommAbort(comm);
+                delete job;
             }
         }).detach();
     } catch (...) {
@@ -481,16 +469,16 @@ static int rccl_init(lbk_ctx* c, const void* nccl_id) {
         return -3;
     }
     const double t_end = mono_s() + c->rccl_timeout_s;
-    while (!job->done.load(std::memory_order_acquire) && mono_s() < t_end) usleep(200);
-    if (!job->done.load(std::memory_order_acquire)) {
-        job->abandoned.store(1, std::memory_order_release);
+    while (job->state.load(std::memory_order_acquire) == RCCL_JOB_RUNNING && mono_s() < t_end) usleep(200);
+    int expect = RCCL_JOB_RUNNING;
+    if (job->state.compare_exchange_strong(expect, RCCL_JOB_ABANDONED, std::memory_order_acq_rel)) {
         snprintf(c->err, sizeof c->err, "ncclCommInitRankConfig: no progress in %.0f s (RCCL communicator abandoned)",
                  c->rccl_timeout_s);
         fprintf(stderr, "lbfgs rank %d: %s\n", c->geo.rank, c->err);
         c->rccl_hung = 1;
-        return -3;  // job stays with the thread (a race with a late completion costs one leaked job)
+        return -3;  // the thread owns the job now; a late communicator is aborted there
     }
-    const ncclResult_t r = job->r;
+    const ncclResult_t r = job->r;  // DONE: the thread has let go of the job
     ncclComm_t comm = job->comm;
     delete job;
     if (r != ncclSuccess) {
@@ -686,16 +674,17 @@ int xfer(lbk_ctx* c, void* dst, const void* src, size_t bytes, bool h2d) {
         const size_t len = (((uintptr_t)host + bytes + 4095) & ~(uintptr_t)4095) - a;
         if (hipHostRegister((void*)a, len, hipHostRegisterDefault) == hipSuccess) {
             hipError_t e = hipMemcpyAsync(dst, src, bytes, h2d ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost, c->stream);
-            if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+            const int wrc = e == hipSuccess ? stream_wait(c, "vector transfer") : 0;
             (void)hipHostUnregister((void*)a);
             HIPCHK(c, e);
-            return 0;
+            return wrc;
         }
         (void)hipGetLastError();  // not registrable (already pinned, ...): the pageable copy
     } else if (mode == 2) {
         XferPool* P = xfer_pool(c);
         if (P) {
-            HIPCHK(c, hipStreamSynchronize(c->stream));  // the solver stream's work on the vector is done
+            const int wrc = stream_wait(c, "vector transfer");  // the solver stream's work on the vector is done
+            if (wrc) return wrc;
             const int T = P->threads;
             const size_t per = ((bytes / T) + 4095) & ~(size_t)4095;
             std::vector<std::thread> th;
@@ -717,8 +706,7 @@ int xfer(lbk_ctx* c, void* dst, const void* src, size_t bytes, bool h2d) {
         }
     }
     HIPCHK(c, hipMemcpyAsync(dst, src, bytes, h2d ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    return 0;
+    return stream_wait(c, "vector transfer");
 }
 }  // namespace
 
@@ -1133,13 +1121,8 @@ int lbk_small_iter(lbk_ctx* c, int obj, int h, const double* g, double* q, doubl
             }
         });
     }
-    return launch(c, LBK_K_SMALL_ITER, vec, -1, [&] {
-        switch (obj) {
-            case LBK_OBJ_ROSENBROCK: hipLaunchKernelGGL(k_small_iter<LBK_OBJ_ROSENBROCK>, dim3(1), dim3(LBK_SMALL_THREADS), 0, c->stream, a, geo); break;
-            case LBK_OBJ_QUAD_TRIDIAG: hipLaunchKernelGGL(k_small_iter<LBK_OBJ_QUAD_TRIDIAG>, dim3(1), dim3(LBK_SMALL_THREADS), 0, c->stream, a, geo); break;
-            default: hipLaunchKernelGGL(k_small_iter<LBK_OBJ_QUAD_SEPARABLE>, dim3(1), dim3(LBK_SMALL_THREADS), 0, c->stream, a, geo); break;
-        }
-    });
+    snprintf(c->err, sizeof c->err, "lbk_small_iter: no one-launch form for this size");
+    return -1;
 }
 
 int lbk_small_spec_ok(const lbk_ctx* c, int h) {
@@ -1150,6 +1133,8 @@ int lbk_search_dev_ok(const lbk_ctx* c, int obj) {
     return c->dev_wolfe && c->geo.world == 1 && !c->comm && c->wolfe_max > 0 && c->geo.nseg <= c->wolfe_max &&
            (obj == LBK_OBJ_ROSENBROCK || obj == LBK_OBJ_QUAD_TRIDIAG || obj == LBK_OBJ_QUAD_SEPARABLE);
 }
+
+static int small_wait(lbk_ctx* c, unsigned long long epoch, int word = 0);
 
 int lbk_search_dev(lbk_ctx* c, int obj, int ls, const double* x, const double* d, lbk_search* st,
                    const lbk_search_commit* cm) {
@@ -1163,6 +1148,8 @@ int lbk_search_dev(lbk_ctx* c, int obj, int ls, const double* x, const double* d
     a.seq_base = (unsigned)c->wolfe_seq;
     a.err = c->coop_err_d;
     a.timeout = (unsigned long long)(c->search_timeout_s * c->wall_khz * 1e3);  // 2 s per barrier
+    a.done = c->sp_dh + 3;  // completion word: the host polls it instead of synchronising the stream
+    a.epoch = ++c->search_epoch;
     c->wolfe_seq += LBK_SEARCH_PASSES + 1;                                     // trial passes + the commit
     SearchCommit k;
     memset(&k, 0, sizeof k);
@@ -1198,18 +1185,22 @@ int lbk_search_dev(lbk_ctx* c, int obj, int ls, const double* x, const double* d
 #undef SEARCH_LAUNCH
     });
     if (rc) return rc;
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const int wrc = small_wait(c, c->search_epoch, 3);  // polls the word; no runtime thread spins
     if (*(volatile unsigned*)c->coop_err_h) {
-        // the grid was not resident together (or a barrier waited past its bound): every workgroup
-        // has left the launch, which stored no vector (the commit pass comes after every trial
-        // pass's barrier), so the caller goes on with the host loop from the same state; the device
+        // the grid was not resident together (or a barrier waited past its bound): each workgroup
+        // leaves at its first failed barrier (or at the next one, which finds the error flag set)
+        // and no trial pass or commit runs after it; a workgroup that passed every barrier may have
+        // run the commit pass on its own segments, so the caller goes on with the host loop from the
+        // same state and commits again even at the first trial's step (recommit_a0); the device
         // form stays off for this context
+        HIPCHK(c, hipStreamSynchronize(c->stream));  // the whole grid has drained
         *(volatile unsigned*)c->coop_err_h = 0;
         c->dev_wolfe = 0;
         c->coop_fallbacks++;
         snprintf(c->err, sizeof c->err, "device line search: grid barrier timed out (search redone on the host loop)");
         return -6;
     }
+    if (wrc) return wrc;
     lbk_search r;
     memcpy(&r, (const void*)c->wolfe_out_h, sizeof r);
     *st = r;
@@ -1230,7 +1221,7 @@ int lbk_search_dev(lbk_ctx* c, int obj, int ls, const double* x, const double* d
 // core; profiles/r05/config4_cpu/: eight such ranks on one box exhausted its 16-CPU quota and
 // configs[4] ran at half speed). The stream is asked only once a wait has lasted 0.25 s - a
 // launch that faulted or never wrote its record - never on the way to a normal completion.
-static int small_wait(lbk_ctx* c, unsigned long long epoch, int word = 0) {
+static int small_wait(lbk_ctx* c, unsigned long long epoch, int word) {
     const volatile unsigned long long* done = c->sp_h + word;
     double t_query = 0.0;
     for (unsigned long it = 1;; ++it) {
@@ -1329,8 +1320,7 @@ int lbk_fetch_marked(lbk_ctx* c, int slot, int ncomp, double* totals) {
 int lbk_small_ok(const lbk_ctx* c, int h) {
     if (c->geo.world != 1 || c->comm || h < 1 || h > LBK_SMALL_HMAX) return 0;
     if (c->coop_max > 0 && c->geo.nseg <= c->coop_max) return 1;
-    if (persist_fits(c)) return 1;
-    return c->small_seg_max > 0 && c->geo.nseg <= c->small_seg_max && c->geo.nseg <= LBK_SMALL_SEGMAX;
+    return persist_fits(c) ? 1 : 0;
 }
 
 int lbk_update(lbk_ctx* c, int op, double* out, const double* a, const double* b, double rho, int slot_a,
@@ -1404,12 +1394,16 @@ int lbk_checksum(lbk_ctx* c, const double* x, uint64_t* c1, uint64_t* c2) {
             snprintf(c->err, sizeof c->err, "sharded context has no exchange backend");
             return -3;
         }
+        rccl_debug_stall(c);
         const int rrc = rccl_settle(c, ncclAllReduce(c->d_ck, c->d_ck, 2, ncclUint64, ncclSum, c->comm, c->stream),
                                     "ncclAllReduce");
         if (rrc) return rrc;
     }
     HIPCHK(c, hipMemcpyAsync(c->h_ck, c->d_ck, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    {
+        const int wrc = stream_wait(c, "trajectory checksum (ncclAllReduce)");
+        if (wrc) return wrc;
+    }
     *c1 = c->h_ck[0];
     *c2 = c->h_ck[1];
     if (c->grp) {  // integer sums: exact in any order
@@ -1459,7 +1453,8 @@ int lbk_fetch_groups(lbk_ctx* c, int slot, double* groups64) {
         if (rc) return rc;
     } else {
         if (!c->slot_mirror[si]) HIPCHK(c, hipMemcpyAsync(h, slot_base(c, slot), bytes, hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(c, hipStreamSynchronize(c->stream));
+        const int wrc = stream_wait(c, "result slot (ncclAllGather)");
+        if (wrc) return wrc;
     }
     if (c->xg_on && lbk_xgmi_failed(c->xg)) {
         snprintf(c->err, sizeof c->err, "xgmi exchange timed out waiting for a peer");
@@ -1488,7 +1483,8 @@ int lbk_fetch(lbk_ctx* c, int slot, int ncomp, double* totals) {
 }
 
 int lbk_sync(lbk_ctx* c) {
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const int wrc = stream_wait(c, "stream synchronisation");
+    if (wrc) return wrc;
     if (c->xg_on && lbk_xgmi_failed(c->xg)) {
         snprintf(c->err, sizeof c->err, "xgmi exchange timed out waiting for a peer");
         return -3;
@@ -1532,7 +1528,7 @@ int lbk_coop_info(const lbk_ctx* c, int* coop_max, int* search_max, int* fallbac
 }
 
 int lbk_stream_probe(lbk_ctx* c, double* q, const double* const* ys, const double* const* ss, int npairs,
-                     int launches, double* us) {
+                     int launches, double* us, int variant) {
     if (launches < 1 || !us || !q || !ys || !ss || npairs < 1) return -1;
     for (int k = 0; k < npairs; ++k)
         if (!ys[k] || !ss[k]) return -1;
@@ -1550,20 +1546,53 @@ int lbk_stream_probe(lbk_ctx* c, double* q, const double* const* ys, const doubl
         snprintf(c->err, sizeof c->err, "hipEventCreate failed");
         return -2;
     }
+    // variants (gap analysis against k_axpy_dot): 0 the box probe (alpha = 0, no
+    // reduction); 1 the same with alpha != 0; 2 + the pass's segment reduction stored plainly (no
+    // stage 2); 3 + the collect stage 2 into a scratch slot; 4 / 5 the product's own k_axpy_dot
+    // launch (lbk_axpy_dot: source slot read, collect stage 2), alpha = 0 / != 0, chained through
+    // two scratch slots as the passes chain theirs
+    constexpr int kProbeSlot = LBK_NSLOTS - 2;  // scratch slots no solver path uses
+    if (variant >= 4) {  // the chained source slot starts at 0.0
+        HIPCHK(c, hipMemsetAsync(c->slots + (int64_t)kProbeSlot * LBK_SLOT, 0, 2 * LBK_SLOT * sizeof(double),
+                                 c->stream));
+    }
     HIPCHK(c, hipEventRecord(a, c->stream));
     const int par = c->rev_par;  // the solver's walk parity is left as it was
+    const double bytes_before = c->bytes_total;
     for (int i = 0; i < launches; ++i) {
-        const Geo g = kgeo(c);  // alternating walk, as the passes
         const double* y = ys[(i + 1) % npairs];
         const double* s = ss[i % npairs];
-        NT_DISPATCH(c, hipLaunchKernelGGL(k_probe_stream<NT_>, dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, q, y, s,
-                                          g, c->partials));
+        hipError_t e = hipSuccess;
+        if (variant >= 4) {
+            const int src = kProbeSlot + (i & 1), dst = kProbeSlot + ((i + 1) & 1);
+            const int rc = lbk_axpy_dot(c, q, q, y, s, variant == 5 ? 1e-12 : 0.0, src * LBK_KMAX, dst);
+            if (rc) {
+                c->rev_par = par;
+                return rc;
+            }
+            continue;  // launch() flips the walk
+        }
+        const Geo g = kgeo(c);  // alternating walk, as the passes
+        const double alpha = variant == 1 ? 1e-3 : 0.0;
+        if (variant <= 1) {
+            NT_DISPATCH(c, hipLaunchKernelGGL(k_probe_stream<NT_>, dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, q, y,
+                                              s, alpha, g, c->partials));
+        } else {
+            Red r = kred(c, kProbeSlot);
+            if (variant == 2) {
+                r.ll = nullptr;
+                r.ticket = 0;
+            }
+            NT_DISPATCH(c, hipLaunchKernelGGL(k_probe_stream2<NT_>, dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, q, y,
+                                              s, alpha, g, r));
+        }
         c->rev_par ^= 1;
-        const hipError_t e = hipGetLastError();
+        e = hipGetLastError();
         if (e != hipSuccess) c->rev_par = par;
         HIPCHK(c, e);
     }
     c->rev_par = par;
+    c->bytes_total = bytes_before;  // probe launches are not solver traffic
     HIPCHK(c, hipEventRecord(b, c->stream));
     HIPCHK(c, hipEventSynchronize(b));
     float ms = 0.f;

@@ -203,9 +203,12 @@ __device__ __forceinline__ void ll_store(unsigned long long* p, double v, unsign
     __hip_atomic_store(p, tag | (u & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(p + 1, tag | (u >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// spins until both halves carry `seq`; past `timeout` wall-clock ticks sets *err and returns NaN
+// spins until both halves carry `seq`; past `timeout` wall-clock ticks sets *err and returns NaN.
+// Once a wait has lasted 1/1024 of the timeout it also ends (NaN) as soon as *err shows that another
+// workgroup's wait already timed out: a launch whose grid broke apart drains in about one timeout,
+// not one per remaining barrier. `failed` is set whenever NaN comes from either exit.
 __device__ __forceinline__ double ll_load(const unsigned long long* p, unsigned seq, unsigned* err,
-                                          unsigned long long timeout) {
+                                          unsigned long long timeout, bool& failed) {
     unsigned long long w0 = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     unsigned long long w1 = __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if ((unsigned)(w0 >> 32) != seq || (unsigned)(w1 >> 32) != seq) {
@@ -215,13 +218,24 @@ __device__ __forceinline__ double ll_load(const unsigned long long* p, unsigned 
             w0 = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             w1 = __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if ((unsigned)(w0 >> 32) == seq && (unsigned)(w1 >> 32) == seq) break;
-            if (wall_clock64() - t0 > timeout) {
+            const unsigned long long el = wall_clock64() - t0;
+            if (el > timeout) {
                 if (err) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                failed = true;
+                return __builtin_nan("");
+            }
+            if (err && el > (timeout >> 10) && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) {
+                failed = true;
                 return __builtin_nan("");
             }
         }
     }
     return bitsd((w1 << 32) | (w0 & 0xffffffffull));
+}
+__device__ __forceinline__ double ll_load(const unsigned long long* p, unsigned seq, unsigned* err,
+                                          unsigned long long timeout) {
+    bool failed = false;
+    return ll_load(p, seq, err, timeout, failed);
 }
 
 // Per-workgroup view of its segment.
@@ -2020,19 +2034,12 @@ __global__ void k_vf_ghosts(const double* __restrict__ slot, double* x, double* 
 }
 
 // ---------------------------------------------------------------------------------------
-// Small-n persistent iteration (one workgroup): the whole two-loop recursion and the fused
-// first-trial commit of one iteration in ONE launch, for n small enough that the m-deep ring
-// sits in L2 and kernel boundaries, not bytes, set the time (SURVEY §7 step 5's persistent
-// two-loop, in the regime where it pays). The workgroup's 256-thread quarters each take a
-// segment and compute exactly what a workgroup of the multi-launch path computes for it; segment
-// partials stay in LDS; stage 2 (group trees, fixed-order total) runs in-kernel and every pass's
-// alpha / beta feeds the next pass from LDS. Each pass's 8 group values are also written to its
-// result slot, so everything after it (line search, a materialised d, a recommit) reads the same
-// slots as after the multi-launch sequence: bit-identical results.
+// Arguments of the one-launch iterations (the cooperative iteration k_coop_iter, the device line
+// search k_coop_search and the persistent forms): the two-loop recursion and the fused first-trial
+// commit of one iteration in ONE launch. (A single-workgroup form for the smallest n measured 1.8x
+// slower at n = 1e4 than the launch sequence, profiles/r01/small_persistent.txt, and was removed.)
 // ---------------------------------------------------------------------------------------
 #define LBK_SMALL_HMAX 16
-#define LBK_SMALL_SEGMAX 256
-#define LBK_SMALL_THREADS 512  // two segments at a time; 1024 would cap VGPRs at 128 and spill
 
 struct SmallArgs {
     int h, p0_from_slot;
@@ -2091,117 +2098,7 @@ __device__ __forceinline__ Seg seg_at(const Geo& geo, int64_t sidx, int tq) {
     return s;
 }
 
-// one pass of Op over all segments; the K fixed-order totals land in tot[] (every thread)
-template <int K, class Op>
-__device__ void small_pass(const Op& op, const Geo& geo, double* slot, double* hslot, double (&tot)[K],
-                           double (*part)[LBK_SMALL_SEGMAX], double (*wl)[16]) {
-    const int t = threadIdx.x, qtr = t >> 8, tq = t & 255, lane = t & 63, wv = t >> 6;
-    for (int64_t s0 = 0; s0 < geo.nseg; s0 += LBK_SMALL_THREADS / 256) {
-        const int64_t sidx = s0 + qtr;
-        double acc[K];
-#pragma unroll
-        for (int k = 0; k < K; ++k) acc[k] = 0.0;
-        if (sidx < geo.nseg) {
-            const Seg sg = seg_at(geo, sidx, tq);
-            stream(op, sg, geo, acc);
-        }
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const double v = wave_sum(acc[k]);
-            if (lane == 0) wl[k][wv] = v;
-        }
-        __syncthreads();
-        if (tq == 0 && sidx < geo.nseg) {
-            const int w0 = 4 * qtr;
-#pragma unroll
-            for (int k = 0; k < K; ++k)
-                part[k][sidx] = (wl[k][w0] + wl[k][w0 + 1]) + (wl[k][w0 + 2] + wl[k][w0 + 3]);
-        }
-        __syncthreads();
-    }
-    // stage 2: group 0 holds every segment (nseg <= 1024); groups 1..7 are trees of zeros
-    if (t < 256) {
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            double p[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int j = 4 * t + i;
-                p[i] = j < geo.nseg ? part[k][j] : 0.0;
-            }
-            const double v = wave_sum((p[0] + p[1]) + (p[2] + p[3]));
-            if (lane == 0) wl[k][wv] = v;
-        }
-    }
-    __syncthreads();
-    if (t < K) {
-        const int k = t;
-        const double q0 = (wl[k][0] + wl[k][1]) + (wl[k][2] + wl[k][3]);
-        for (int g = 0; g < LBK_GROUPS; ++g) {
-            slot[g * LBK_KMAX + k] = g == 0 ? q0 : 0.0;
-            if (hslot) hslot[g * LBK_KMAX + k] = g == 0 ? q0 : 0.0;
-        }
-        double tt = q0;
-        for (int g = 1; g < LBK_GROUPS; ++g) tt = tt + 0.0;
-        wl[k][8] = tt;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < K; ++k) tot[k] = wl[k][8];
-    // this pass's vector writes are read by other waves in the next one (the commit's halo)
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __syncthreads();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-}
-
 #define HS(sl) (a.hslots ? a.hslots + (int64_t)(sl) * LBK_SLOT : nullptr)  // host-fetched slots only
-template <int OBJ>
-__global__ __launch_bounds__(LBK_SMALL_THREADS) void k_small_iter(SmallArgs a, Geo geo) {
-    __shared__ double part[LBK_KMAX][LBK_SMALL_SEGMAX];
-    __shared__ double wl[LBK_KMAX][16];
-    __shared__ double TA[LBK_SMALL_HMAX], TB[LBK_SMALL_HMAX];
-    const int h = a.h;
-    double t1[1];
-    // alpha_{h-1} = rho_{h-1} (s_{h-1} . g): from the previous commit (SG) or a dot pass
-    if (a.p0_from_slot) {
-        t1[0] = slot_total(a.p0_slot);
-    } else {
-        small_pass<1>(OpDot<false>{a.S[h - 1], a.g}, geo, a.slots + (int64_t)a.slot_p0 * LBK_SLOT, nullptr, t1, part, wl);
-    }
-    if (threadIdx.x == 0) TA[h - 1] = t1[0];
-    double alpha = a.rho[h - 1] * t1[0];
-    const double* qsrc = a.g;
-    for (int i = h - 2; i >= 0; --i) {  // q = q - alpha_{i+1} y_{i+1};  s_i . q
-        small_pass<1>(OpAxpyDot<false>{a.q, qsrc, a.Y[i + 1], a.S[i], alpha}, geo,
-                      a.slots + (int64_t)(a.slot_a0 + i) * LBK_SLOT, nullptr, t1, part, wl);
-        if (threadIdx.x == 0) TA[i] = t1[0];
-        alpha = a.rho[i] * t1[0];
-        qsrc = a.q;
-    }
-    small_pass<1>(OpMid<false>{a.r, qsrc, a.Y[0], alpha, a.gamma}, geo, a.slots + (int64_t)a.slot_b0 * LBK_SLOT, nullptr, t1,
-                  part, wl);
-    if (threadIdx.x == 0) TB[0] = t1[0];
-    __syncthreads();
-    for (int i = 0; i + 1 < h; ++i) {  // r += s_i (alpha_i - beta_i);  y_{i+1} . r
-        const double beta = a.rho[i] * TB[i];
-        const double alph = a.rho[i] * TA[i];
-        small_pass<1>(OpAxpy2Dot<false>{a.r, a.r, a.S[i], a.Y[i + 1], alph - beta}, geo,
-                      a.slots + (int64_t)(a.slot_b0 + i + 1) * LBK_SLOT, nullptr, t1, part, wl);
-        if (threadIdx.x == 0) TB[i + 1] = t1[0];
-        __syncthreads();
-    }
-    // the last second-loop update, the first trial at a0 and the commit (k_commit TWOLOOP)
-    DirArgs da = {a.r, a.S[h - 1], a.g, 0.0, nullptr, nullptr, a.rho[h - 1], nullptr, geo.g_lo, geo.g_hi};
-    {
-        const double beta = a.rho[h - 1] * TB[h - 1];
-        const double alph = a.rho[h - 1] * TA[h - 1];
-        da.coef = alph - beta;
-    }
-    double t7[7];
-    small_pass<7>(OpCommit<OBJ, LBK_D_TWOLOOP, false>{a.x, da, a.a0, a.xn, a.gn, a.so, a.yo, geo.n, geo.n_loc}, geo,
-                  a.slots + (int64_t)a.slot_c * LBK_SLOT, HS(a.slot_c), t7, part, wl);
-}
-
 // ---------------------------------------------------------------------------------------
 // Cooperative iteration for small n (the persistent-block two-loop of SURVEY §7 step 5): one
 // workgroup per canonical segment (nseg <= LBK_COOP_SEGMAX, all resident), the whole two-loop
@@ -2281,12 +2178,17 @@ __device__ __forceinline__ void coop_publish(const SmallArgs& a, int went, doubl
     if (threadIdx.x == 0) __hip_atomic_store(a.done, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// Returns false (uniformly over the workgroup) when one of its waits timed out or found another
+// workgroup's time-out (ll_load): the totals are then NaN and the caller leaves the launch.
 template <int K, class Op>
-__device__ __forceinline__ void coop_pass(const Op& op, const Geo& geo, const SmallArgs& a, int pass,
+__device__ __forceinline__ bool coop_pass(const Op& op, const Geo& geo, const SmallArgs& a, int pass,
                                           double* slot, double* hslot, const double* rvec, double (&tot)[K],
                                           double (&lds)[4][8], double (&tl)[8]) {
     static_assert(K + 2 <= LBK_LL_COMPS, "flagged components");
+    __shared__ int wg_failed;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    if (t == 0) wg_failed = 0;  // read after two barriers below
+    bool failed = false;
     const int64_t b = blockIdx.x;
     const Seg s = seg_setup(geo);
     double acc[K];
@@ -2319,7 +2221,7 @@ __device__ __forceinline__ void coop_pass(const Op& op, const Geo& geo, const Sm
 #pragma unroll
         for (int k = w; k < K; k += 4) {
             const double p =
-                lane < geo.nseg ? ll_load(P + ((int64_t)k * LBK_LL_SEGS + lane) * 2, seq, a.err, a.timeout) : 0.0;
+                lane < geo.nseg ? ll_load(P + ((int64_t)k * LBK_LL_SEGS + lane) * 2, seq, a.err, a.timeout, failed) : 0.0;
             const double q0 = wave_sum(p) + 0.0;  // group 0: the tree's levels above 64 add 0.0
             if (lane == 0) {
                 double tt = q0;
@@ -2336,7 +2238,8 @@ __device__ __forceinline__ void coop_pass(const Op& op, const Geo& geo, const Sm
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int j = 4 * t + i;
-                p[k][i] = j < geo.nseg ? ll_load(P + ((int64_t)k * LBK_LL_SEGS + j) * 2, seq, a.err, a.timeout) : 0.0;
+                p[k][i] = j < geo.nseg ? ll_load(P + ((int64_t)k * LBK_LL_SEGS + j) * 2, seq, a.err, a.timeout, failed)
+                                       : 0.0;
             }
 #pragma unroll
         for (int k = 0; k < K; ++k) {
@@ -2353,10 +2256,13 @@ __device__ __forceinline__ void coop_pass(const Op& op, const Geo& geo, const Sm
             if (b == 0 && slot) coop_store_total(slot, hslot, t, q0);
         }
     }
+    if (failed) wg_failed = 1;
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < K; ++k) tot[k] = tl[k];
-    __syncthreads();  // lds / tl reuse by the next pass
+    const bool ok = wg_failed == 0;
+    __syncthreads();  // lds / tl / wg_failed reuse by the next pass
+    return ok;
 }
 
 #define SL(sl) (a.slots + (int64_t)(sl) * LBK_SLOT)
@@ -2478,8 +2384,12 @@ __global__ __launch_bounds__(LB_BLOCK) void k_coop_search(SmallArgs a, Geo geo, 
     constexpr int NC = LBK_TRIALS_NC;
     DirArgs da = {d, nullptr, nullptr, 0.0, nullptr, nullptr, 0.0, nullptr, geo.g_lo, geo.g_hi};
     int pass = 0;
+    // a grid barrier of this workgroup timed out (or found another's time-out): no further pass and
+    // no commit; the host sees the error flag, ignores *out and redoes the search on its loop
+    bool broken = false;
     // lbfgs_driver.c trial() / trial_batched() for a device objective: the caches, else one pass;
-    // false: the launch's pass budget is spent (the state stays at the top of this iteration)
+    // false: the launch's pass budget is spent (the state stays at the top of this iteration), or
+    // the grid broke apart
     auto trial = [&](double alpha, bool need_g, double& f, double& dphi) -> bool {
         if (s.have_spec && alpha == s.spec_a) {
             f = s.spec_f;
@@ -2496,11 +2406,14 @@ __global__ __launch_bounds__(LB_BLOCK) void k_coop_search(SmallArgs a, Geo geo, 
                 dphi = s.tc_dphi;
                 return true;
             }
-        if (pass >= LBK_SEARCH_PASSES) return false;
+        if (pass >= LBK_SEARCH_PASSES || broken) return false;
         if (FG) {
             OpTrials<OBJ, LBK_D_BUF, 1, true, false> op{x, da, {alpha}, geo.n, geo.n_loc};
             double t[2];
-            coop_pass<2>(op, geo, a, pass++, nullptr, nullptr, nullptr, t, lds, tl);
+            if (!coop_pass<2>(op, geo, a, pass++, nullptr, nullptr, nullptr, t, lds, tl)) {
+                broken = true;
+                return false;
+            }
             s.tc_n = 1;
             s.tc_a[0] = alpha;
             s.tc_f[0] = t[0];
@@ -2516,7 +2429,10 @@ __global__ __launch_bounds__(LB_BLOCK) void k_coop_search(SmallArgs a, Geo geo, 
 #pragma unroll
             for (int j = 1; j < NC; ++j) op.a[j] = op.a[j - 1] * ratio;
             double t[NC];
-            coop_pass<NC>(op, geo, a, pass++, nullptr, nullptr, nullptr, t, lds, tl);
+            if (!coop_pass<NC>(op, geo, a, pass++, nullptr, nullptr, nullptr, t, lds, tl)) {
+                broken = true;
+                return false;
+            }
             s.tc_n = NC;
 #pragma unroll
             for (int j = 0; j < NC; ++j) {
@@ -2654,7 +2570,10 @@ __global__ __launch_bounds__(LB_BLOCK) void k_coop_search(SmallArgs a, Geo geo, 
     s.alpha = alpha;
     // the commit at the decided step (lbfgs_driver.c commit(), D_BUF, cand 0), unless the commit
     // already taken was at that step
-    if (s.done && cm.slot && !(s.have_spec && s.step == s.spec_a)) {
+    // (a workgroup whose barriers all completed can still reach this pass while another one timed
+    // out at the last trial barrier; it then writes its own segments of xn, gn, s and y, which is
+    // why the host's redo commits again even at the first trial's step, recommit_a0)
+    if (!broken && s.done && cm.slot && !(s.have_spec && s.step == s.spec_a)) {
         DirArgs dc = {d, nullptr, cm.g, 0.0, nullptr, nullptr, 0.0, nullptr, geo.g_lo, geo.g_hi};
         double t7[7];
         coop_pass<7>(OpCommit<OBJ, LBK_D_BUF, false>{x, dc, s.step, cm.xn, cm.gn, cm.so, cm.yo, geo.n, geo.n_loc,
@@ -2662,7 +2581,17 @@ __global__ __launch_bounds__(LB_BLOCK) void k_coop_search(SmallArgs a, Geo geo, 
                      geo, a, pass++, cm.slot, cm.hslot, nullptr, t7, lds, tl);
         s.committed = 1;
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0) *out = s;
+    // block 0: the search state, then the completion word the host polls (lbk_search_dev): block 0
+    // leaves only after every barrier of the launch completed or failed, and a failure has set the
+    // error flag before this word
+    if (blockIdx.x == 0) {
+        if (threadIdx.x == 0) *out = s;
+        if (a.done) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+            __syncthreads();
+            if (threadIdx.x == 0) __hip_atomic_store(a.done, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -2998,11 +2927,21 @@ __global__ void k_checksum(const double* __restrict__ x, int64_t n_loc, int64_t 
 // the s loads are not dropped.
 template <bool NT>
 __global__ __launch_bounds__(LB_BLOCK) void k_probe_stream(double* q, const double* __restrict__ y,
-                                                           const double* __restrict__ sv, Geo geo, double* sink) {
+                                                           const double* __restrict__ sv, double alpha, Geo geo,
+                                                           double* sink) {
     const Seg s = seg_setup(geo);
     double acc[1] = {0.0};
-    stream(OpAxpyDot<NT>{q, q, y, sv, 0.0}, s, geo, acc);
+    stream(OpAxpyDot<NT>{q, q, y, sv, alpha}, s, geo, acc);
     if (acc[0] == 1.0) sink[blockIdx.x] = acc[0];
+}
+// Gap analysis (lbfgs_stream_probe_variant): the probe's stream with the pass's own segment
+// reduction after it - reduce_publish with the given Red (a plain partial store, or the collect
+// stage 2) - but no source slot read: k_axpy_dot without src_total.
+template <bool NT>
+__global__ __launch_bounds__(LB_BLOCK) void k_probe_stream2(double* q, const double* __restrict__ y,
+                                                            const double* __restrict__ sv, double alpha, Geo geo,
+                                                            Red red) {
+    run_pass<OpAxpyDot<NT>, 1>(OpAxpyDot<NT>{q, q, y, sv, alpha}, geo, red);
 }
 
 }  // namespace
@@ -3045,6 +2984,7 @@ struct lbk_ctx {
     // communicator abandoned or aborted, never in a hang; rccl_hung: an aborted collective may
     // still sit on the stream, which destroy then does not wait for
     double rccl_timeout_s;
+    double rccl_stall_ms;  // test hook: LBFGS_DEBUG_RCCL_STALL_MS (rccl_debug_stall)
     int rccl_hung;
     char err[256];
     // profiling
@@ -3068,9 +3008,7 @@ struct lbk_ctx {
     int nt_vf;       // the vector-free passes' NT policy (c->nt while they launch)
     int ticket_env;  // LBFGS_TICKET override (-1: none)
     int xg_on;       // 1: exchanges go through xg instead of RCCL
-    int xg_mirror;   // 1: xg exchanges of host-read slots also fill the host mirror
     uint64_t* d_ckslot;  // [LBK_GROUPS][2] checksum words for the peer exchange
-    int small_seg_max;  // persistent single-workgroup iteration when nseg <= this (0: off)
     // LBFGS_REV=1: every other pass walks its segments last to first, so a pass starts on the
     // tail of the vector its predecessor wrote last (still in the Infinity Cache / L2)
     int rev_on, rev_par;
@@ -3125,6 +3063,8 @@ struct lbk_ctx {
     unsigned long long slot_s2[LBK_NSLOTS + LBK_NWSLOTS];
     // a slot fetch without one: k_slot_publish's epoch (sp_h[2]), the last issued
     unsigned long long pub_epoch;
+    // the device line search's completion word (sp_h[3], written by k_coop_search's block 0)
+    unsigned long long search_epoch;
     double *dq_A, *dq_b, *dq_t;  // dense quadratic objective (lbk_dense_set): A (n x n), b, terms
     // folded exchanges (sharded over the mailboxes; LBFGS_XGMI_FOLD=0: off): the two-loop's
     // single-component reductions travel from the producing pass straight into the consuming pass
@@ -3356,6 +3296,29 @@ int rccl_stream_wait(lbk_ctx* c, const char* what) {
     return -3;
 }
 
+// A host wait on the solver stream. With an RCCL communicator, collectives may sit on the stream,
+// and a peer that dies mid-solve would leave a plain hipStreamSynchronize waiting forever: the wait
+// is then bounded (rccl_stream_wait, LBFGS_RCCL_TIMEOUT) and ends in LBFGS_ERR_RCCL. Without one
+// every wait on the stream is on this process's own kernels, whose in-kernel waits are bounded.
+int stream_wait(lbk_ctx* c, const char* what) {
+    if (c->comm) return rccl_stream_wait(c, what);
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+// Test hook (LBFGS_DEBUG_RCCL_STALL_MS): a one-thread kernel queued ahead of every RCCL collective
+// that sleeps that long on the device, standing in for a peer that stops answering; it ends on its
+// own, so the GPU is never held. tests/test_gpu_rccl.py sets it above LBFGS_RCCL_TIMEOUT.
+__global__ void k_stall(unsigned long long ticks) {
+    const unsigned long long t0 = wall_clock64();
+    while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
+}
+void rccl_debug_stall(lbk_ctx* c) {
+    if (c->rccl_stall_ms <= 0.0) return;
+    hipLaunchKernelGGL(k_stall, dim3(1), dim3(1), 0, c->stream,
+                       (unsigned long long)(c->rccl_stall_ms * c->wall_khz));
+}
+
 // Sharded runs: each rank owns groups [g_lo, g_hi) of every result slot; gather them so
 // every rank holds all 8 (one RCCL all-gather of (8/world) x KMAX doubles per reduction, in
 // place, on the solver stream), or through the host group for emulated ranks.
@@ -3387,6 +3350,7 @@ int exchange_buf(lbk_ctx* c, double* base, int ks, double* host_mirror = nullptr
         snprintf(c->err, sizeof c->err, "sharded context has no exchange backend (no RCCL id, peers not enabled)");
         return -3;
     }
+    rccl_debug_stall(c);
     return rccl_settle(c, ncclAllGather(base + c->geo.g_lo * ks, base, (size_t)per, ncclDouble, c->comm, c->stream),
                        "ncclAllGather");
 }
@@ -3395,10 +3359,9 @@ int exchange_buf(lbk_ctx* c, double* base, int ks, double* host_mirror = nullptr
 // host reads back (as the stage 2 does on one rank, see mirrored()): no device-to-host copy
 // before those reads
 int exchange_slot(lbk_ctx* c, int slot, int K = 1, bool host_read = true) {
-    double* hm = nullptr;
-    if (host_read && c->xg_on && c->xg_mirror && !c->grp && (K >= 2 || slot >= LBK_NSLOTS))
-        hm = slot < LBK_NSLOTS ? c->dh_slots + (int64_t)slot * LBK_SLOT
-                               : c->dh_wslots + (int64_t)(slot - LBK_WSLOT0) * LBK_WSLOT;
+    double* hm = nullptr;  // (a host-mirroring exchange measured neutral, profiles/r01/xgmi_mirror_ab.txt)
+    (void)K;
+    (void)host_read;
     const int rc = exchange_buf(c, slot_base(c, slot), slot_stride(slot), hm);
     c->slot_mirror[slot < LBK_NSLOTS ? slot : LBK_NSLOTS + slot - LBK_WSLOT0] = rc == 0 && hm != nullptr;
     return rc;

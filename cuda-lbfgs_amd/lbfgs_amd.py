@@ -124,6 +124,7 @@ def lib():
     L.lbfgs_cu_partition.argtypes = [vp]
     L.lbfgs_coop_info.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]
     L.lbfgs_stream_probe.argtypes = [vp, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double)]
+    L.lbfgs_stream_probe_variant.argtypes = [vp, C.c_int, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double)]
     L.lbfgs_prof_enable.argtypes = [vp, C.c_int]
     L.lbfgs_prof_enable.restype = None
     L.lbfgs_prof_reset.argtypes = [vp]
@@ -145,7 +146,7 @@ EXPORTED_SYMBOLS = [
     "lbfgs_dev_twoloop", "lbfgs_dev_elementwise", "lbfgs_line_search", "lbfgs_prof_enable",
     "lbfgs_prof_reset", "lbfgs_prof_get", "lbfgs_peer_handle", "lbfgs_peer_connect", "lbfgs_peer_enable", "lbfgs_rccl_attach",
     "lbfgs_exchange_backend", "lbfgs_exchange_fold", "lbfgs_exchange_latency", "lbfgs_device_count", "lbfgs_set_dense_quadratic", "lbfgs_build_info",
-    "lbfgs_spec_stats", "lbfgs_cu_partition", "lbfgs_stream_probe", "lbfgs_coop_info", "lbfgs_search_stats",
+    "lbfgs_spec_stats", "lbfgs_cu_partition", "lbfgs_stream_probe", "lbfgs_stream_probe_variant", "lbfgs_coop_info", "lbfgs_search_stats",
 ]
 PEER_HANDLE_BYTES = 64
 BACKENDS = {0: "single", 1: "rccl", 2: "xgmi", 3: "host-group"}
@@ -375,11 +376,12 @@ class Context:
         """CUs this rank's solver stream is confined to (LBFGS_CU_PARTITION=1), 0 if not"""
         return int(lib().lbfgs_cu_partition(self.h))
 
-    def stream_probe(self, launches=20):
+    def stream_probe(self, launches=20, variant=0):
         """This box's rate for the two-loop passes' 3 R + 1 W access pattern over the context's own
-        buffers (lbfgs_stream_probe; after init): dict(avg_launch_us, bytes_per_launch, gbps)."""
+        buffers (lbfgs_stream_probe; after init): dict(avg_launch_us, bytes_per_launch, gbps).
+        variant > 0: the pass's machinery added piece by piece (lbfgs_stream_probe_variant)."""
         us, b = C.c_double(), C.c_double()
-        rc = lib().lbfgs_stream_probe(self.h, int(launches), C.byref(us), C.byref(b))
+        rc = lib().lbfgs_stream_probe_variant(self.h, int(variant), int(launches), C.byref(us), C.byref(b))
         if rc != 0:
             self._err("lbfgs_stream_probe", rc)
         return dict(avg_launch_us=us.value, bytes_per_launch=b.value,

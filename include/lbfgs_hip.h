@@ -254,6 +254,12 @@ int lbfgs_coop_info(const lbfgs_ctx* ctx, int* coop_max, int* search_max, int* f
  * the passes' access pattern beside the solver's. Call between lbfgs_solver_step calls of an
  * initialised solve. */
 int lbfgs_stream_probe(lbfgs_ctx* ctx, int launches, double* us, double* bytes);
+/* The same with the two-loop pass's machinery added piece by piece (the gap between
+ * k_axpy_dot and the probe): variant 0 = lbfgs_stream_probe; 1 = alpha != 0 (the work vector
+ * changes); 2 = + the pass's segment reduction, partials stored plainly (no stage 2); 3 = + the
+ * collect stage 2 into a scratch result slot; 4 / 5 = the product's k_axpy_dot launch itself (source
+ * slot read, collect stage 2) with alpha = 0 / != 0, chained through two scratch slots. */
+int lbfgs_stream_probe_variant(lbfgs_ctx* ctx, int variant, int launches, double* us, double* bytes);
 /* Emulated ranks: 'world' contexts driven by threads of ONE process (e.g. on one GPU, one
  * stream each) exchange their reductions through host memory instead of RCCL. Same data path
  * and results as the RCCL shards; used to test sharding on a single GPU. */

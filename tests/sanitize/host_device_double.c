@@ -155,8 +155,8 @@ int lbk_coop_info(const lbk_ctx* c, int* a, int* b, int* f) {
     return 0;
 }
 int lbk_stream_probe(lbk_ctx* c, double* q, const double* const* ys, const double* const* ss, int npairs,
-                     int launches, double* us) {
-    (void)c, (void)q, (void)ys, (void)ss, (void)npairs, (void)launches;
+                     int launches, double* us, int variant) {
+    (void)c, (void)q, (void)ys, (void)ss, (void)npairs, (void)launches, (void)variant;
     *us = 0.0;  /* no device: nothing to time */
     return 0;
 }

@@ -65,14 +65,27 @@ def horizon(a, b):
     return int(bad[0]) if len(bad) else int(k)
 
 
-@pytest.mark.parametrize("name,unfused", [("config1_n1e7", True), ("config2_n1e8", False), ("config3_n1e8", False)])
-def test_fullsize_parity(name, unfused):
+@pytest.mark.parametrize("name,unfused,persist", [("config1_n1e7", True, False), ("config2_n1e8", False, False),
+                                                  ("config2_n1e8", False, True), ("config3_n1e8", False, False)],
+                         ids=["config1_n1e7-unfused", "config2_n1e8", "config2_n1e8-persist2", "config3_n1e8"])
+def test_fullsize_parity(monkeypatch, name, unfused, persist):
+    """persist: configs[2] as BASELINE names it, through the persistent-block fused two-loop
+    (LBFGS_PERSIST=2, k_persist_twoloop: the 2h - 1 two-loop passes of an iteration in one resident
+    launch), against the same fixture as the launch sequence"""
     fx = json.load(open(os.path.join(FULLSIZE, name + ".json")))
     n, m = fx["n"], fx["m"]
     x0 = L.x0_uniform(n, fx["seed"], fx["lo"], fx["hi"])
+    if persist:
+        monkeypatch.setenv("LBFGS_PERSIST", "2")
     with L.Context(n, m) as c:
+        c.prof_reset()
+        c.prof_enable(persist)
         r = c.minimize(fx["objective"], x0, fx["method"], fx["maxit"], tolerance=fx["tol"], trace=True,
                        unfused=unfused)
+        c.prof_enable(False)
+        if persist:  # the persistent kernel ran once per iteration with a history, no pass kernels
+            assert c.prof_get("small_iter")["launches"] >= fx["maxit"] - 1
+            assert c.prof_get("axpy_dot")["launches"] == 0 and c.prof_get("axpy2_dot")["launches"] == 0
         if unfused:
             # the same context through the fused passes: the unfused launch shape changes no bit
             rf = c.minimize(fx["objective"], x0, fx["method"], fx["maxit"], tolerance=fx["tol"], trace=True)

@@ -3,7 +3,9 @@ spinning beside it (DESIGN.md §5 "Host side"): slot fetches without a completio
 own poll one written by k_slot_publish instead of synchronising the stream - each stream
 synchronisation registered an asynchronous handler with the runtime, and the runtime thread that
 serves them spun at ~1 core within a second of solving (profiles/r05/config4_cpu/). n = 1e7 has
-7813 segments in 8 groups, so every fetch of the iteration takes that path."""
+7813 segments in 8 groups, so every fetch of the iteration takes that path. n = 1e5 under Wolfe
+runs the cooperative iteration and the device-resident line search (k_coop_search), whose host
+wait polls the completion word its block 0 writes."""
 import os
 import sys
 import time
@@ -29,13 +31,14 @@ def thread_ticks():
     return out
 
 
-@pytest.mark.parametrize("vector_free", [False, True])
-def test_no_runtime_thread_spins_during_a_solve(vector_free):
-    n, m = 10 ** 7, 10
+@pytest.mark.parametrize("n,ls,vector_free", [(10 ** 7, "backtracking", False), (10 ** 7, "backtracking", True),
+                                               (10 ** 5, "wolfe", False)])
+def test_no_runtime_thread_spins_during_a_solve(n, ls, vector_free):
+    m = 10
     x0 = L.x0_uniform(n, 42, -2.0, 2.0)
     hz = os.sysconf("SC_CLK_TCK")
     with L.Context(n, m) as c:
-        c.init("rosenbrock", x0, "backtracking", tolerance=1e-5, vector_free=vector_free)
+        c.init("rosenbrock", x0, ls, tolerance=1e-5, vector_free=vector_free)
         c.step(m)
         t_end = time.perf_counter() + 1.5  # past the ~1 s after which the spinning used to start
         while time.perf_counter() < t_end:

@@ -26,7 +26,7 @@ pytestmark = pytest.mark.gpu
 # the sharded ones (LBFGS_XGMI_FOLD, LBFGS_CU_PARTITION, the time-outs of the exchanges) are
 # covered by tests/test_gpu_xgmi.py and tests/test_gpu_rccl.py, the transfer paths (LBFGS_XFER)
 # by tests/test_gpu_xfer.py. A/B forms measured slower are compiled into variant builds only
-# (tools/build_variant.sh: LBK_PERSIST_ITER, LBK_SMALL_SEGS, LBK_XGMI_MIRROR, LBK_PERSIST_STRIDE,
+# (tools/build_variant.sh: LBK_PERSIST_ITER, LBK_PERSIST_STRIDE,
 # LBK_PERSIST_ALT, LBK_PERSIST_LDS; the q/r ping-pong was removed).
 KNOBS = ["LBFGS_TICKET", "LBFGS_DEFER", "LBFGS_REV", "LBFGS_NT", "LBFGS_DIRECT", "LBFGS_COOP",
          "LBFGS_PERSIST", "LBFGS_SPEC", "LBFGS_BATCH", "LBFGS_PERSIST_WG", "LBFGS_COLLECT",

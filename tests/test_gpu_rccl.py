@@ -67,6 +67,27 @@ def test_rccl_one_rank_bit_identical(monkeypatch, n, m, obj, ls, iters, vf, tick
     assert us > 0.0
 
 
+def test_rccl_stalled_collective_mid_solve_fails_bounded(monkeypatch):
+    """A collective that does not complete mid-solve (a peer that stops answering) ends the solve
+    with LBFGS_ERR_RCCL within the RCCL bound instead of hanging the rank: every host
+    wait on a stream that carries RCCL work is bounded (lbfgs_kernels_impl.h stream_wait). The
+    stalled peer is stood in for by a device-side sleep queued ahead of each collective
+    (LBFGS_DEBUG_RCCL_STALL_MS, longer than LBFGS_RCCL_TIMEOUT), which ends on its own."""
+    import time
+    monkeypatch.setenv("LBFGS_RCCL_TIMEOUT", "0.5")
+    monkeypatch.setenv("LBFGS_DEBUG_RCCL_STALL_MS", "4000")
+    n = 1_000_003
+    x0 = L.x0_uniform(n, 5, -2.0, 2.0)
+    with L.Context(n, 5, world=1, uid=L.unique_id()) as c:
+        assert c.backend == "rccl"
+        t0 = time.monotonic()
+        with pytest.raises(L.LbfgsError) as ei:
+            c.minimize("rosenbrock", x0, "backtracking", 10)
+        took = time.monotonic() - t0
+    assert "(-3)" in str(ei.value) and "did not complete" in str(ei.value), str(ei.value)
+    assert took < 3.5, took  # one 0.5 s bound, not the 4 s stall (nor a hang)
+
+
 N4 = 8192 * 8192 + 1  # smallest n whose canonical segments are >= 8192 long (L = 8320)
 
 

@@ -1,0 +1,83 @@
+# tools/gpu_r06.sh — round 6's GPU-box steps (run through gpurun from the repo root). Every GPU step
+# has its own time limit; steps are chained so the first failure ends the call. A heartbeat line a
+# minute keeps the watchdog informed while a step writes nothing.
+#
+#   bash tools/gpu_r06.sh first      host facts, smoke, the new / changed GPU tests, the gap probe
+#                                    plain and under rocprofv3 (kernel trace), the default bench line
+#   bash tools/gpu_r06.sh gappmc     SQ / TA counter passes over the gap probe (one pass per run)
+#   bash tools/gpu_r06.sh tests ARGS pytest -m gpu over ARGS (default: tests)
+#   bash tools/gpu_r06.sh bench ARGS one bench.py line -> gpurun_out/r06/bench.json
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 1
+export TMPDIR=/tmp
+O=gpurun_out/r06
+mkdir -p $O
+( while sleep 60; do echo "running $(date +%T)"; done ) & hb=$!
+trap 'kill $hb 2> /dev/null' EXIT
+
+host_facts() {
+    { date; free -g; nproc; cat /sys/fs/cgroup/cpu.max 2> /dev/null; cat /sys/fs/cgroup/memory.max 2> /dev/null;
+      df -h /tmp . | tail -2; } > $O/host_facts.txt 2>&1
+    cat $O/host_facts.txt
+}
+
+smoke() {
+    timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
+    local rc=$?; echo "smoke rc=$rc"; tail -2 $O/smoke.log; return $rc
+}
+
+tests() {
+    local args=("$@"); [ ${#args[@]} -eq 0 ] && args=(tests)
+    timeout -k 10 1000 python -u -m pytest "${args[@]}" -m gpu -v --timeout 300 --timeout-method thread \
+        > $O/pytest.log 2>&1 &
+    local pid=$! n=0
+    while kill -0 $pid 2> /dev/null; do
+        sleep 5; n=$((n + 1))
+        [ $((n % 12)) -eq 0 ] && echo "tests running: $(grep -c -E 'PASSED|FAILED|ERROR' $O/pytest.log) results"
+    done
+    wait $pid
+    local rc=$?; echo "tests rc=$rc"; grep -E "FAILED|ERROR|passed|failed" $O/pytest.log | tail -15; return $rc
+}
+
+gap() {
+    timeout -k 10 400 python tools/gap_probe.py $O/gap_probe.json 1e8 4 > $O/gap_probe.log 2>&1
+    local rc=$?; echo "gap rc=$rc"; tail -6 $O/gap_probe.log; return $rc
+}
+
+gap_trace() {
+    timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/gap_trace -o run --output-format csv -- \
+        python3 tools/gap_probe.py $O/gap_probe_traced.json 1e8 2 > $O/gap_trace.log 2>&1
+    local rc=$?; echo "gap trace rc=$rc"; tail -3 $O/gap_trace.log; return $rc
+}
+
+gap_pmc() {  # one counter pass: $1 = tag, rest = counters
+    local tag=$1; shift
+    timeout -s KILL 240 rocprofv3 --pmc "$@" -d $O/gap_pmc_$tag -o run --output-format csv -- \
+        python3 tools/gap_probe.py $O/gap_probe_pmc_$tag.json 1e8 1 > $O/gap_pmc_$tag.log 2>&1
+    local rc=$?; echo "pmc $tag rc=$rc"; [ $rc -eq 0 ] || tail -5 $O/gap_pmc_$tag.log; return $rc
+}
+
+bench() {
+    timeout -k 10 900 python bench.py "$@" > $O/bench.json 2> $O/bench.err
+    local rc=$?; echo "bench rc=$rc"; cut -c1-1500 $O/bench.json; [ $rc -eq 0 ] || tail -20 $O/bench.err
+    return $rc
+}
+
+case "$1" in
+    first)
+        host_facts && smoke &&
+        tests tests/test_gpu_rccl.py tests/test_gpu_host_threads.py tests/test_gpu_device_search.py \
+              tests/test_gpu_coop_safety.py tests/test_gpu_persist.py "tests/test_gpu_fullsize.py::test_fullsize_parity" &&
+        gap && gap_trace && bench ;;
+    gappmc)
+        timeout -k 10 60 rocprofv3 -L > $O/counters.txt 2>&1; echo "list rc=$?"
+        gap_pmc a SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
+                  SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR &&
+        gap_pmc b SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_ACTIVE_INST_VMEM SQ_INST_CYCLES_VMEM_RD \
+                  SQ_INST_CYCLES_VMEM_WR SQ_WAVES_RESTORED &&
+        gap_pmc c FETCH_SIZE &&
+        gap_pmc d WRITE_SIZE ;;
+    tests) shift; tests "$@" ;;
+    bench) shift; bench "$@" ;;
+    *) echo "unknown part $1"; exit 2 ;;
+esac
