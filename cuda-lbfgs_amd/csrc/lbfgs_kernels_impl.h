@@ -1578,8 +1578,16 @@ struct OpCommit {
     }
 };
 
+#ifndef LBK_COMMIT_WAVES
+#define LBK_COMMIT_WAVES 0  // A/B: > 0 asks the register allocation for that many waves per SIMD
+#endif
+#if LBK_COMMIT_WAVES > 0
+#define LBK_COMMIT_ATTR __attribute__((amdgpu_waves_per_eu(LBK_COMMIT_WAVES)))
+#else
+#define LBK_COMMIT_ATTR
+#endif
 template <int OBJ, int DMODE, bool NT, bool CAND = false>
-__global__ __launch_bounds__(LB_BLOCK) void k_commit(const double* __restrict__ x, DirArgs da, double alpha,
+__global__ __launch_bounds__(LB_BLOCK) LBK_COMMIT_ATTR void k_commit(const double* __restrict__ x, DirArgs da, double alpha,
                                                      double* __restrict__ xn, double* __restrict__ gn,
                                                      double* __restrict__ so, double* __restrict__ yo,
                                                      Geo geo, Red red, double cand = 0.0) {
@@ -3301,7 +3309,8 @@ int rccl_stream_wait(lbk_ctx* c, const char* what) {
 // is then bounded (rccl_stream_wait, LBFGS_RCCL_TIMEOUT) and ends in LBFGS_ERR_RCCL. Without one
 // every wait on the stream is on this process's own kernels, whose in-kernel waits are bounded.
 int stream_wait(lbk_ctx* c, const char* what) {
-    if (c->comm) return rccl_stream_wait(c, what);
+    // (after an abort, rccl_hung: the aborted collective may still sit on the stream)
+    if (c->comm || c->rccl_hung) return rccl_stream_wait(c, what);
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return 0;
 }

@@ -4,6 +4,7 @@
 #
 #   bash tools/gpu_r06.sh first      host facts, smoke, the new / changed GPU tests, the gap probe
 #                                    plain and under rocprofv3 (kernel trace), the default bench line
+#   bash tools/gpu_r06.sh gapbench   smoke, the stalled-collective test, the gap probe (plain, traced), bench
 #   bash tools/gpu_r06.sh gappmc     SQ / TA counter passes over the gap probe (one pass per run)
 #   bash tools/gpu_r06.sh tests ARGS pytest -m gpu over ARGS (default: tests)
 #   bash tools/gpu_r06.sh bench ARGS one bench.py line -> gpurun_out/r06/bench.json
@@ -69,6 +70,8 @@ case "$1" in
         tests tests/test_gpu_rccl.py tests/test_gpu_host_threads.py tests/test_gpu_device_search.py \
               tests/test_gpu_coop_safety.py tests/test_gpu_persist.py "tests/test_gpu_fullsize.py::test_fullsize_parity" &&
         gap && gap_trace && bench ;;
+    gapbench)
+        smoke && tests tests/test_gpu_rccl.py -k stalled && gap && gap_trace && bench ;;
     gappmc)
         timeout -k 10 60 rocprofv3 -L > $O/counters.txt 2>&1; echo "list rc=$?"
         gap_pmc a SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
