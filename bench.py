@@ -426,10 +426,14 @@ def _measure(a, D, ctx, x0, rank, world, uid, unfused, vector_free, box_probe, d
     vote("history fill / warm-up")
     D.barrier()
     run(ctx.sync)
+    w0 = run(ctx.wait_stats)
+    c0 = time.process_time()
     t0 = time.perf_counter()
     res = run(ctx.step, a.steps)
     run(ctx.sync)
     t_local = time.perf_counter() - t0
+    cpu_local = time.process_time() - c0
+    w1 = run(ctx.wait_stats)
     D.barrier()
     T = D.allreduce(t_local, "max")
     bytes_all = D.allreduce(res["bytes"] if res else 0.0, "sum")
@@ -490,6 +494,12 @@ def _measure(a, D, ctx, x0, rank, world, uid, unfused, vector_free, box_probe, d
         vote("exchange latency")
     if trace:
         res["trajectory"] = ctx.trace()
+    # this process's host CPU over the timed steps (all its threads) and the time its completion-word
+    # waits slept (LBFGS_WAIT)
+    res["host"] = ({"cpu_s": round(cpu_local, 4), "cpu_share": round(cpu_local / max(t_local, 1e-9), 4),
+                    "slept_share": round((w1["slept_s"] - w0["slept_s"]) / max(t_local, 1e-9), 4),
+                    "waits": w1["waits"] - w0["waits"], "wait_mode": "adaptive" if w1["adaptive"] else "spin"}
+                   if w0 and w1 else None)
     res["history_fill"] = fill["iterations"]
     res["warm_counters"] = {k: warm[k] for k in ("trials_f", "trials_fg", "commits", "passes")} if warm else None
     res["box_probe"] = probe
@@ -1023,6 +1033,7 @@ def main():
             "exchange_share": prof.get("_exchange_share"),
             "exchange_fallback": fallback,
             "kernel_busy": prof.get("_busy"),
+            "host": res.get("host"),
             "cpu_baseline": cpu,
             "reference_parity": parity,
             "solver": {"status": res["status"], "f": res["f"], "gnorm": res["gnorm"],

@@ -476,6 +476,14 @@ int lbfgs_exchange_latency(lbfgs_ctx* c, int backend, int components, int iters,
 
 int lbfgs_cu_partition(const lbfgs_ctx* c) { return c ? lbk_cu_partition(c->dev) : LBFGS_ERR_BAD_ARG; }
 
+int lbfgs_wait_stats(const lbfgs_ctx* c, double* slept_s, uint64_t* waits, int* adaptive) {
+    if (!c) return LBFGS_ERR_BAD_ARG;
+    unsigned long long w = 0;
+    const int rc = lbk_wait_stats(c->dev, slept_s, &w, adaptive);
+    if (waits) *waits = (uint64_t)w;
+    return rc;
+}
+
 int lbfgs_coop_info(const lbfgs_ctx* c, int* coop_max, int* search_max, int* fallbacks) {
     return c ? lbk_coop_info(c->dev, coop_max, search_max, fallbacks) : LBFGS_ERR_BAD_ARG;
 }

@@ -150,6 +150,8 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
     // after which the host loop redoes the search)
     c->search_timeout_s = 2.0;
     if (const char* e = getenv("LBFGS_SEARCH_TIMEOUT")) c->search_timeout_s = std::max(0.0, atof(e));
+    c->wait_adaptive = 1;
+    if (const char* e = getenv("LBFGS_WAIT")) c->wait_adaptive = strcmp(e, "spin") != 0;
     c->rccl_timeout_s = 60.0;
     if (const char* e = getenv("LBFGS_RCCL_TIMEOUT")) c->rccl_timeout_s = std::max(0.5, atof(e));
     if (const char* e = getenv("LBFGS_DEBUG_RCCL_STALL_MS")) c->rccl_stall_ms = std::max(0.0, atof(e));
@@ -1221,11 +1223,41 @@ int lbk_search_dev(lbk_ctx* c, int obj, int ls, const double* x, const double* d
 // core; profiles/r05/config4_cpu/: eight such ranks on one box exhausted its 16-CPU quota and
 // configs[4] ran at half speed). The stream is asked only once a wait has lasted 0.25 s - a
 // launch that faulted or never wrote its record - never on the way to a normal completion.
+// Spin-then-sleep (LBFGS_WAIT=adaptive, the default; =spin: spin from the start, rounds 2-5): a wait
+// whose word's last four waits all lasted more than 0.5 ms first sleeps, in steps of at most 200 us,
+// through 80 % of the shortest of them less 100 us, and spins only for the rest. At n = 1e8 an
+// iteration's host wait is ~11 ms, of which the polling core then sleeps ~90 %; a wait that ends
+// early costs at most one sleep step; short waits (small n: tens of us) spin as before.
+static void wait_sleep_phase(lbk_ctx* c, const volatile unsigned long long* done, unsigned long long epoch, int word,
+                             double t0) {
+    double est = 1e30;
+    for (int k = 0; k < 4; ++k) est = std::min(est, c->wait_hist[word][k]);
+    if (!(est > 0.5e-3) || est > 1e29) return;
+    const double until = t0 + 0.8 * est - 100e-6;
+    for (;;) {
+        if (__atomic_load_n(const_cast<unsigned long long*>(done), __ATOMIC_ACQUIRE) >= epoch) return;
+        const double left = until - mono_s();
+        if (left <= 0.0) return;
+        timespec ts;
+        ts.tv_sec = 0;
+        ts.tv_nsec = (long)(std::min(left, 200e-6) * 1e9);
+        nanosleep(&ts, nullptr);
+        c->wait_slept_s += std::min(left, 200e-6);
+    }
+}
+
 static int small_wait(lbk_ctx* c, unsigned long long epoch, int word) {
     const volatile unsigned long long* done = c->sp_h + word;
+    if (__atomic_load_n(const_cast<unsigned long long*>(done), __ATOMIC_ACQUIRE) >= epoch) return 0;
+    const double t0 = mono_s();
+    if (c->wait_adaptive) wait_sleep_phase(c, done, epoch, word, t0);
     double t_query = 0.0;
     for (unsigned long it = 1;; ++it) {
-        if (__atomic_load_n(const_cast<unsigned long long*>(done), __ATOMIC_ACQUIRE) >= epoch) return 0;
+        if (__atomic_load_n(const_cast<unsigned long long*>(done), __ATOMIC_ACQUIRE) >= epoch) {
+            c->wait_hist[word][c->wait_pos[word]++ & 3] = mono_s() - t0;
+            c->waits++;
+            return 0;
+        }
         if ((it & 0xffff) == 0) {
             if (*(volatile unsigned*)c->coop_err_h) break;
             const double now = mono_s();
@@ -1519,6 +1551,13 @@ int lbk_peer_enable(lbk_ctx* c, int on) {
 }
 
 int lbk_cu_partition(const lbk_ctx* c) { return c->cu_part ? c->cu_count : 0; }
+
+int lbk_wait_stats(const lbk_ctx* c, double* slept_s, unsigned long long* waits, int* adaptive) {
+    if (slept_s) *slept_s = c->wait_slept_s;
+    if (waits) *waits = c->waits;
+    if (adaptive) *adaptive = c->wait_adaptive;
+    return 0;
+}
 
 int lbk_coop_info(const lbk_ctx* c, int* coop_max, int* search_max, int* fallbacks) {
     if (coop_max) *coop_max = c->coop_max;

@@ -3073,6 +3073,13 @@ struct lbk_ctx {
     unsigned long long pub_epoch;
     // the device line search's completion word (sp_h[3], written by k_coop_search's block 0)
     unsigned long long search_epoch;
+    // host waits on the completion words (small_wait): spin-then-sleep, the last four waits' durations
+    // per word, and the time slept / waits completed (lbfgs_wait_stats)
+    int wait_adaptive;
+    double wait_hist[4][4];
+    unsigned wait_pos[4];
+    double wait_slept_s;
+    unsigned long long waits;
     double *dq_A, *dq_b, *dq_t;  // dense quadratic objective (lbk_dense_set): A (n x n), b, terms
     // folded exchanges (sharded over the mailboxes; LBFGS_XGMI_FOLD=0: off): the two-loop's
     // single-component reductions travel from the producing pass straight into the consuming pass

@@ -123,6 +123,7 @@ def lib():
     L.lbfgs_search_stats.argtypes = [vp, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
     L.lbfgs_cu_partition.argtypes = [vp]
     L.lbfgs_coop_info.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]
+    L.lbfgs_wait_stats.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_uint64), C.POINTER(C.c_int)]
     L.lbfgs_stream_probe.argtypes = [vp, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double)]
     L.lbfgs_stream_probe_variant.argtypes = [vp, C.c_int, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double)]
     L.lbfgs_prof_enable.argtypes = [vp, C.c_int]
@@ -146,7 +147,7 @@ EXPORTED_SYMBOLS = [
     "lbfgs_dev_twoloop", "lbfgs_dev_elementwise", "lbfgs_line_search", "lbfgs_prof_enable",
     "lbfgs_prof_reset", "lbfgs_prof_get", "lbfgs_peer_handle", "lbfgs_peer_connect", "lbfgs_peer_enable", "lbfgs_rccl_attach",
     "lbfgs_exchange_backend", "lbfgs_exchange_fold", "lbfgs_exchange_latency", "lbfgs_device_count", "lbfgs_set_dense_quadratic", "lbfgs_build_info",
-    "lbfgs_spec_stats", "lbfgs_cu_partition", "lbfgs_stream_probe", "lbfgs_stream_probe_variant", "lbfgs_coop_info", "lbfgs_search_stats",
+    "lbfgs_spec_stats", "lbfgs_cu_partition", "lbfgs_stream_probe", "lbfgs_stream_probe_variant", "lbfgs_coop_info", "lbfgs_wait_stats", "lbfgs_search_stats",
 ]
 PEER_HANDLE_BYTES = 64
 BACKENDS = {0: "single", 1: "rccl", 2: "xgmi", 3: "host-group"}
@@ -370,6 +371,12 @@ class Context:
         a, b, f = C.c_int(), C.c_int(), C.c_int()
         lib().lbfgs_coop_info(self.h, C.byref(a), C.byref(b), C.byref(f))
         return dict(coop_max=a.value, search_max=b.value, fallbacks=f.value)
+
+    def wait_stats(self):
+        """host waits on completion words: dict(slept_s, waits, adaptive) (lbfgs_wait_stats)"""
+        s, w, a = C.c_double(), C.c_uint64(), C.c_int()
+        lib().lbfgs_wait_stats(self.h, C.byref(s), C.byref(w), C.byref(a))
+        return dict(slept_s=s.value, waits=w.value, adaptive=bool(a.value))
 
     @property
     def cu_partition(self):

@@ -246,6 +246,11 @@ int lbfgs_cu_partition(const lbfgs_ctx* ctx);
  * for the device-resident line searches (k_coop_search; 0 when off); *fallbacks = device searches
  * whose grid barrier timed out (LBFGS_SEARCH_TIMEOUT, 2 s) and that the host loop redid. */
 int lbfgs_coop_info(const lbfgs_ctx* ctx, int* coop_max, int* search_max, int* fallbacks);
+/* The host's waits for device results poll a completion word in pinned memory. LBFGS_WAIT=adaptive
+ * (default): a wait expected to last over 0.5 ms (its word's last four waits) sleeps through most of
+ * it and spins for the rest; LBFGS_WAIT=spin: spin throughout. *slept_s = seconds slept so far,
+ * *waits = waits completed, *adaptive = the mode. */
+int lbfgs_wait_stats(const lbfgs_ctx* ctx, double* slept_s, uint64_t* waits, int* adaptive);
 /* Diagnostic (no reference counterpart): `launches` back-to-back streams of 3 reads + 1 write
  * over a scratch work vector and the context's history vectors (y, s of the pair pool, another
  * pair every launch as the two-loop passes read them) in the passes' geometry and cache policy;

@@ -154,6 +154,13 @@ int lbk_coop_info(const lbk_ctx* c, int* a, int* b, int* f) {
     if (f) *f = 0;
     return 0;
 }
+int lbk_wait_stats(const lbk_ctx* c, double* s, unsigned long long* w, int* a) {
+    (void)c;
+    if (s) *s = 0.0;
+    if (w) *w = 0;
+    if (a) *a = 0;
+    return 0;
+}
 int lbk_stream_probe(lbk_ctx* c, double* q, const double* const* ys, const double* const* ss, int npairs,
                      int launches, double* us, int variant) {
     (void)c, (void)q, (void)ys, (void)ss, (void)npairs, (void)launches, (void)variant;

@@ -57,6 +57,9 @@ class StubContext:
     def stream_probe(self, launches):
         return dict(avg_launch_us=500.0, bytes_per_launch=3.2e9, gbps=6400.0)
 
+    def wait_stats(self):
+        return dict(slept_s=0.0, waits=0, adaptive=True)
+
     def prof_reset(self):
         pass
 

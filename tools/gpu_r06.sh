@@ -5,6 +5,7 @@
 #   bash tools/gpu_r06.sh first      host facts, smoke, the new / changed GPU tests, the gap probe
 #                                    plain and under rocprofv3 (kernel trace), the default bench line
 #   bash tools/gpu_r06.sh gapbench   smoke, the stalled-collective test, the gap probe (plain, traced), bench
+#   bash tools/gpu_r06.sh waitab     LBFGS_WAIT=spin against adaptive, alternating, n = 1e8 and 1e4
 #   bash tools/gpu_r06.sh gappmc     SQ / TA counter passes over the gap probe (one pass per run)
 #   bash tools/gpu_r06.sh tests ARGS pytest -m gpu over ARGS (default: tests)
 #   bash tools/gpu_r06.sh bench ARGS one bench.py line -> gpurun_out/r06/bench.json
@@ -71,7 +72,22 @@ case "$1" in
               tests/test_gpu_coop_safety.py tests/test_gpu_persist.py "tests/test_gpu_fullsize.py::test_fullsize_parity" &&
         gap && gap_trace && bench ;;
     gapbench)
-        smoke && tests tests/test_gpu_rccl.py -k stalled && gap && gap_trace && bench ;;
+        smoke && tests tests/test_gpu_rccl.py -k stalled && gap && gap_trace && bench && bash $0 waitab ;;
+    waitab)  # the spin-then-sleep host wait against the spinning one, alternating, n = 1e8 and 1e4
+        for r in 1 2; do
+            for w in spin adaptive; do
+                LBFGS_WAIT=$w timeout -k 10 300 python bench.py --steps 100 --warmup 20 --no-cpu-baseline \
+                    --no-vector-free --no-persistent > $O/wait_${w}_n1e8_$r.json 2> $O/wait_${w}_n1e8_$r.err || exit 1
+                LBFGS_WAIT=$w timeout -k 10 300 python bench.py --size 1e4 --history 5 --steps 20000 --warmup 2000 \
+                    --no-cpu-baseline --no-vector-free --no-persistent --no-box-probe > $O/wait_${w}_n1e4_$r.json \
+                    2> $O/wait_${w}_n1e4_$r.err || exit 1
+                python -c "
+import json
+for n in ('1e8', '1e4'):
+    d = json.load(open('$O/wait_${w}_n' + n + '_$r.json'))
+    print('$w', n, '$r', d['value'], d['host'])" | tee -a $O/wait_ab.txt
+            done
+        done ;;
     gappmc)
         timeout -k 10 60 rocprofv3 -L > $O/counters.txt 2>&1; echo "list rc=$?"
         gap_pmc a SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
