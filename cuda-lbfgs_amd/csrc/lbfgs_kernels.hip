@@ -154,7 +154,15 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
     if (const char* e = getenv("LBFGS_WAIT")) c->wait_adaptive = strcmp(e, "spin") != 0;
     c->rccl_timeout_s = 60.0;
     if (const char* e = getenv("LBFGS_RCCL_TIMEOUT")) c->rccl_timeout_s = std::max(0.5, atof(e));
-    if (const char* e = getenv("LBFGS_DEBUG_RCCL_STALL_MS")) c->rccl_stall_ms = std::max(0.0, atof(e));
+    // test hook "stall_ms,wait_s": a device-side stall ahead of every collective and the bound of the
+    // host's waits on collectives (the communicator's init keeps LBFGS_RCCL_TIMEOUT)
+    if (const char* e = getenv("LBFGS_DEBUG_RCCL_STALL")) {
+        double st = 0.0, ws = 0.0;
+        if (sscanf(e, "%lf,%lf", &st, &ws) == 2 && st > 0.0 && ws > 0.0) {
+            c->rccl_stall_ms = st;
+            c->rccl_wait_s = ws;
+        }
+    }
     c->pend_slot = -1;
     c->xf_slot = -1;
     // folded exchanges over the mailboxes: 1 (default) when every peer has a GPU of

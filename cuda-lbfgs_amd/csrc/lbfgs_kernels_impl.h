@@ -2992,7 +2992,8 @@ struct lbk_ctx {
     // communicator abandoned or aborted, never in a hang; rccl_hung: an aborted collective may
     // still sit on the stream, which destroy then does not wait for
     double rccl_timeout_s;
-    double rccl_stall_ms;  // test hook: LBFGS_DEBUG_RCCL_STALL_MS (rccl_debug_stall)
+    double rccl_stall_ms;  // test hook: LBFGS_DEBUG_RCCL_STALL (rccl_debug_stall)
+    double rccl_wait_s;    // ... and its bound on the host's waits on collectives (0: rccl_timeout_s)
     int rccl_hung;
     char err[256];
     // profiling
@@ -3292,7 +3293,8 @@ int rccl_settle(lbk_ctx* c, ncclResult_t r, const char* what) {
 
 // A host wait on the solver stream while RCCL work is queued on it: bounded like rccl_settle
 int rccl_stream_wait(lbk_ctx* c, const char* what) {
-    const double t_end = mono_s() + c->rccl_timeout_s;
+    const double bound = c->rccl_wait_s > 0.0 ? c->rccl_wait_s : c->rccl_timeout_s;
+    const double t_end = mono_s() + bound;
     for (;;) {
         const hipError_t e = hipStreamQuery(c->stream);
         if (e == hipSuccess) return 0;
@@ -3303,8 +3305,8 @@ int rccl_stream_wait(lbk_ctx* c, const char* what) {
         if (mono_s() > t_end) break;
         usleep(50);
     }
-    snprintf(c->err, sizeof c->err, "%s: the RCCL collective did not complete in %.0f s (communicator aborted)", what,
-             c->rccl_timeout_s);
+    snprintf(c->err, sizeof c->err, "%s: the RCCL collective did not complete in %.1f s (communicator aborted)", what,
+             bound);
     if (c->comm) (void)ncclCommAbort(c->comm);
     c->comm = nullptr;
     c->rccl_hung = 1;
@@ -3322,9 +3324,10 @@ int stream_wait(lbk_ctx* c, const char* what) {
     return 0;
 }
 
-// Test hook (LBFGS_DEBUG_RCCL_STALL_MS): a one-thread kernel queued ahead of every RCCL collective
-// that sleeps that long on the device, standing in for a peer that stops answering; it ends on its
-// own, so the GPU is never held. tests/test_gpu_rccl.py sets it above LBFGS_RCCL_TIMEOUT.
+// Test hook (LBFGS_DEBUG_RCCL_STALL="stall_ms,wait_s"): a one-thread kernel queued ahead of every
+// RCCL collective that sleeps stall_ms on the device, standing in for a peer that stops answering,
+// and wait_s as the bound of the host's waits on collectives; the kernel ends on its own, so the GPU
+// is never held. tests/test_gpu_rccl.py sets a stall longer than the bound.
 __global__ void k_stall(unsigned long long ticks) {
     const unsigned long long t0 = wall_clock64();
     while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(127);

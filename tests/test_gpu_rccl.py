@@ -67,25 +67,50 @@ def test_rccl_one_rank_bit_identical(monkeypatch, n, m, obj, ls, iters, vf, tick
     assert us > 0.0
 
 
-def test_rccl_stalled_collective_mid_solve_fails_bounded(monkeypatch):
+_STALL_CHILD = r"""
+import json, os, sys, time
+sys.path.insert(0, os.path.join(sys.argv[1], "cuda-lbfgs_amd"))
+import lbfgs_amd as L
+n = 1_000_003
+x0 = L.x0_uniform(n, 5, -2.0, 2.0)
+out = {}
+try:
+    with L.Context(n, 5, world=1, uid=L.unique_id()) as c:
+        out["backend"] = c.backend
+        t0 = time.monotonic()
+        try:
+            c.minimize("rosenbrock", x0, "backtracking", 10)
+            out["error"] = None
+        except L.LbfgsError as e:
+            out["error"] = str(e)
+        out["took"] = time.monotonic() - t0
+except Exception as e:
+    out["setup_error"] = repr(e)
+print(json.dumps(out), flush=True)
+os._exit(0)  # an abandoned RCCL thread must not hold the interpreter's teardown
+"""
+
+
+def test_rccl_stalled_collective_mid_solve_fails_bounded():
     """A collective that does not complete mid-solve (a peer that stops answering) ends the solve
     with LBFGS_ERR_RCCL within the RCCL bound instead of hanging the rank: every host
     wait on a stream that carries RCCL work is bounded (lbfgs_kernels_impl.h stream_wait). The
-    stalled peer is stood in for by a device-side sleep queued ahead of each collective
-    (LBFGS_DEBUG_RCCL_STALL_MS, longer than LBFGS_RCCL_TIMEOUT), which ends on its own."""
-    import time
-    monkeypatch.setenv("LBFGS_RCCL_TIMEOUT", "0.5")
-    monkeypatch.setenv("LBFGS_DEBUG_RCCL_STALL_MS", "4000")
-    n = 1_000_003
-    x0 = L.x0_uniform(n, 5, -2.0, 2.0)
-    with L.Context(n, 5, world=1, uid=L.unique_id()) as c:
-        assert c.backend == "rccl"
-        t0 = time.monotonic()
-        with pytest.raises(L.LbfgsError) as ei:
-            c.minimize("rosenbrock", x0, "backtracking", 10)
-        took = time.monotonic() - t0
-    assert "(-3)" in str(ei.value) and "did not complete" in str(ei.value), str(ei.value)
-    assert took < 3.5, took  # one 0.5 s bound, not the 4 s stall (nor a hang)
+    stalled peer is stood in for by a device-side sleep queued ahead of each collective, longer than
+    the bound of the waits on collectives (LBFGS_DEBUG_RCCL_STALL="stall_ms,wait_s"); the sleep ends
+    on its own. The communicator's init keeps its own bound (LBFGS_RCCL_TIMEOUT, 60 s). Runs in a
+    child process under a time limit, so nothing RCCL leaves behind can hold this one."""
+    import json
+    import subprocess
+    env = dict(os.environ, LBFGS_DEBUG_RCCL_STALL="4000,0.5")
+    p = subprocess.run([sys.executable, "-c", _STALL_CHILD, ROOT], env=env, capture_output=True, text=True,
+                       timeout=150)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert lines, (p.returncode, p.stdout[-2000:], p.stderr[-2000:])
+    out = json.loads(lines[-1])
+    assert "setup_error" not in out and out["backend"] == "rccl", out
+    err = out["error"] or ""
+    assert "(-3)" in err and "did not complete" in err, out
+    assert out["took"] < 3.5, out  # the 0.5 s bound (twice at most), not the 4 s stall, nor a hang
 
 
 N4 = 8192 * 8192 + 1  # smallest n whose canonical segments are >= 8192 long (L = 8320)
