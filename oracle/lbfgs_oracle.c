@@ -15,6 +15,14 @@
 #include <stdlib.h>
 #include <string.h>
 
+/* Vector loops run over OpenMP threads where n is large: every parallel loop below writes
+ * disjoint elements (or canonical segment partials, or exact integer sums), so the results are
+ * the sequential program's bit for bit; only the time changes (configs[4]'s n = 1e9 restated on
+ * a 16-core host, tests/golden/make_fullsize.py). Without -fopenmp the pragmas are ignored. */
+#define ORC_PAR_MIN 65536
+#define ORC_STR(x) #x
+#define ORC_PAR(n) _Pragma(ORC_STR(omp parallel for schedule(static) if ((n) > ORC_PAR_MIN)))
+
 /* ------------------------------------------------------------------------------------------
  * x0: std::mt19937 + std::uniform_real_distribution<double> (libstdc++ 11)
  * ---------------------------------------------------------------------------------------- */
@@ -64,7 +72,8 @@ void orc_x0_uniform(double* x, int64_t n, uint32_t seed, double lo, double hi) {
 }
 
 void orc_checksum(const double* x, int64_t n, uint64_t* c1, uint64_t* c2) {
-    uint64_t a = 0, b = 0;
+    uint64_t a = 0, b = 0; /* modular integer sums: exact in any order */
+#pragma omp parallel for schedule(static) reduction(+ : a, b) if (n > ORC_PAR_MIN)
     for (int64_t i = 0; i < n; ++i) {
         uint64_t u;
         memcpy(&u, &x[i], 8);
@@ -147,8 +156,9 @@ static void canon_groups_mode(const double* a, const double* b, int64_t n, int64
         spg /= F;
     }
     double* segp = (double*)calloc(CANON_SEGS, sizeof(double));
-    double acc[256];
+#pragma omp parallel for schedule(dynamic, 4) if (n > ORC_PAR_MIN)
     for (int64_t s = 0; s < nseg; ++s) {
+        double acc[256];
         int64_t sbeg = s * L;
         int64_t send = sbeg + L < n ? sbeg + L : n;
         const int64_t nrow = (send - sbeg + 127) / 128, R = (nrow + 3) / 4;
@@ -326,18 +336,21 @@ double orc_f(int obj, const double* x, int64_t n, int mode) {
     double* t = terms_buf(n);
     int64_t limit = n;
     if (obj == ORC_OBJ_ROSENBROCK) {
-        for (int64_t i = 0; i + 1 < n; i++) {
+        ORC_PAR(n)
+        for (int64_t i = 0; i < n - 1; i++) {
             double term1 = x[i + 1] - x[i] * x[i];
             double term2 = 1 - x[i];
             t[i] = 100.0 * term1 * term1 + term2 * term2;
         }
         limit = n - 1;
     } else if (obj == ORC_OBJ_QUAD_TRIDIAG) {
+        ORC_PAR(n)
         for (int64_t i = 0; i < n; i++) {
             double dterm = 1000.0 * x[i] * x[i];
             t[i] = (i + 1 < n) ? dterm + 100.0 * x[i] * x[i + 1] : dterm;
         }
     } else {
+        ORC_PAR(n)
         for (int64_t i = 0; i < n; i++) t[i] = (x[i] - 1) * (x[i] - 1);
     }
     return orc_sum(t, n, limit, mode);
@@ -348,21 +361,35 @@ void orc_grad(int obj, const double* x, int64_t n, double* g) {
         for (int64_t i = 0; i < n; ++i) g[i] = 2.0 * dense_row(g_dense_A + i * n, x, n) + g_dense_b[i];
         return;
     }
+    /* benchmark.cpp's loops add into grad[i] and grad[i + 1] from iteration i; per element that is
+     * grad[i] = (0.0 + 200 term2_{i-1}) + (term1_i - 400 x_i term2_i) (Rosenbrock, :70-81) and
+     * grad[i] = (2000 x_i + 100 x_{i-1}) + 100 x_{i+1} (tridiagonal, :37-56): the same additions in
+     * the same order, written element by element so that the elements can run in parallel */
     if (obj == ORC_OBJ_ROSENBROCK) { /* benchmark.cpp:70-81 */
-        for (int64_t i = 0; i < n; ++i) g[i] = 0.0;
-        for (int64_t i = 0; i + 1 < n; i++) {
-            double term1 = 2.0 * (x[i] - 1);
-            double term2 = x[i + 1] - x[i] * x[i];
-            g[i] += term1 - 400.0 * x[i] * term2;
-            g[i + 1] += 200.0 * term2;
+        ORC_PAR(n)
+        for (int64_t i = 0; i < n; ++i) {
+            double v = 0.0;
+            if (i > 0) {
+                double term2 = x[i] - x[i - 1] * x[i - 1];
+                v += 200.0 * term2; /* grad[i + 1] += 200 term2 of iteration i - 1 */
+            }
+            if (i + 1 < n) {
+                double term1 = 2.0 * (x[i] - 1);
+                double term2 = x[i + 1] - x[i] * x[i];
+                v += term1 - 400.0 * x[i] * term2; /* grad[i] += ... of iteration i */
+            }
+            g[i] = v;
         }
     } else if (obj == ORC_OBJ_QUAD_TRIDIAG) { /* benchmark.cpp:37-56 */
-        for (int64_t i = 0; i < n; i++) g[i] = 2.0 * 1000.0 * x[i];
-        for (int64_t i = 0; i < n - 1; i++) {
-            g[i] += (1000.0 / 10.0) * x[i + 1];
-            g[i + 1] += (1000.0 / 10.0) * x[i];
+        ORC_PAR(n)
+        for (int64_t i = 0; i < n; i++) {
+            double v = 2.0 * 1000.0 * x[i];
+            if (i > 0) v += (1000.0 / 10.0) * x[i - 1];     /* grad[i + 1] += ... of iteration i - 1 */
+            if (i + 1 < n) v += (1000.0 / 10.0) * x[i + 1]; /* grad[i] += ... of iteration i */
+            g[i] = v;
         }
     } else { /* main.cpp:15-21 */
+        ORC_PAR(n)
         for (int64_t i = 0; i < n; i++) g[i] = 2.0 * (x[i] - 1);
     }
 }
@@ -423,6 +450,7 @@ static void G(ctx_t* c, const double* x, double* g) {
 }
 
 static void trial_point(const double* x, const double* d, double alpha, int64_t n, double* out) {
+    ORC_PAR(n)
     for (int64_t i = 0; i < n; ++i) out[i] = x[i] + alpha * d[i]; /* add(x, scalarProduct(alpha, d)) */
 }
 
@@ -1488,6 +1516,7 @@ int orc_lbfgs(const orc_opts* o, const double* x0, double* x_out,
             goto done;
         }
         if (k == 0 || h == 0) { /* :87-91 */
+            ORC_PAR(n)
             for (int64_t i = 0; i < n; ++i) d[i] = -g[i];
         } else { /* two-loop :94-143 */
             memcpy(q, g, vb);
@@ -1495,32 +1524,39 @@ int orc_lbfgs(const orc_opts* o, const double* x0, double* x_out,
                 double rho = 1.0 / orc_dot(hy[i], hs[i], n, mode);
                 if (!isfinite(rho)) {
                     say(&C, "Warning: Invalid rho at iteration %d\n", k);
+                    ORC_PAR(n)
                     for (int64_t j = 0; j < n; ++j) d[j] = -g[j];
                     goto perform_line_search;
                 }
                 alpha_i[i] = rho * orc_dot(hs[i], q, n, mode);
+                ORC_PAR(n)
                 for (int64_t j = 0; j < n; ++j) q[j] -= alpha_i[i] * hy[i][j];
             }
             {
                 double gamma = orc_dot(hs[h - 1], hy[h - 1], n, mode) / orc_dot(hy[h - 1], hy[h - 1], n, mode);
                 if (gamma <= 0 || !isfinite(gamma)) {
                     say(&C, "Warning: Invalid gamma at iteration %d\n", k);
+                    ORC_PAR(n)
                     for (int64_t j = 0; j < n; ++j) d[j] = -g[j];
                     goto perform_line_search;
                 }
+                ORC_PAR(n)
                 for (int64_t i = 0; i < n; ++i) r[i] = q[i] * gamma;
             }
             for (int i = 0; i < h; ++i) {
                 double rho = 1.0 / orc_dot(hy[i], hs[i], n, mode);
                 double beta = rho * orc_dot(hy[i], r, n, mode);
+                ORC_PAR(n)
                 for (int64_t j = 0; j < n; ++j) r[j] += hs[i][j] * (alpha_i[i] - beta);
             }
+            ORC_PAR(n)
             for (int64_t j = 0; j < n; ++j) d[j] = -r[j];
         }
     perform_line_search:; /* :146-156 */
         double gd = orc_dot(g, d, n, mode);
         if (gd >= 0) {
             say(&C, "Warning: Not a descent direction, using gradient\n");
+            ORC_PAR(n)
             for (int64_t j = 0; j < n; ++j) d[j] = -g[j];
             gd = orc_dot(g, d, n, mode);
         }
@@ -1546,6 +1582,7 @@ int orc_lbfgs(const orc_opts* o, const double* x0, double* x_out,
             /* :174-195 — the new pair is written to the spare pool slot hs[h] (h <= m) */
             double* sk = hs[h];
             double* yk = hy[h];
+            ORC_PAR(n)
             for (int64_t i = 0; i < n; ++i) {
                 sk[i] = xn[i] - x[i];
                 yk[i] = gn[i] - g[i];

@@ -36,6 +36,8 @@ iteration at n = 1e8 and the m = 20 runs ~40 GB of host memory, so the cases run
                 the reference itself (maxit = 0: it evaluates f and grad at x0 and stops).
 
 usage: python tests/golden/make_fullsize.py [config1_n1e7] [config2_n1e8] [config3_n1e8] [config4_n1e9]
+       python tests/golden/make_fullsize.py config4_deep OUT.json [iterations]   (a host with ~270 GB)
+       python tests/golden/make_fullsize.py merge_config4_deep OUT.json
 """
 import json
 import os
@@ -227,7 +229,55 @@ def make_config4():
         json.dump(meta, fp, indent=1)
 
 
+def make_config4_deep(out_path, iters=13):
+    """configs[4]'s whole canonical run (ORC_CANON, the oracle's orc_lbfgs at n = 1e9, m = 10,
+    backtracking, `iters` iterations: every trace entry, the history filled to h = m = 10 and three
+    steps with the ring full). ~265 GB of host memory (30 resident vectors of 8 GB, the terms buffer,
+    x0 and x): more than this container has, so it runs on a GPU box's host (tools/gpu_r06.sh
+    config4deep, OpenMP over the oracle's vector loops) and writes `out_path`; `merge_config4_deep`
+    adds it to tests/golden/fullsize/config4_n1e9.json as "canon_deep". Needs no reference build."""
+    n, m = 10 ** 9, 10
+    t0 = time.time()
+    x0 = O.x0_uniform(n, 42, -2.0, 2.0)
+    print(f"config4 deep: x0 in {time.time() - t0:.0f} s", flush=True)
+    t1 = time.time()
+    r = O.lbfgs("rosenbrock", x0, "backtracking", m, iters, 1e-5, mode=O.CANON)
+    del x0
+    xc = [str(v) for v in O.checksum(r["x"])]
+    deep = dict(f=hexbits(r["f"]), gnorm=hexbits(r["gnorm"]), alpha=hexbits(r["alpha"]), c1=dec(r["c1"]),
+                c2=dec(r["c2"]), entries=len(r["f"]), iterations=r["iters"], status=r["status"],
+                messages=r["messages"], x_checksum=xc, maxit=iters,
+                seconds=round(time.time() - t1, 1), threads=os.environ.get("OMP_NUM_THREADS"),
+                generator=("tests/golden/make_fullsize.py make_config4_deep: oracle/lbfgs_oracle.c orc_lbfgs "
+                           "(ORC_CANON) at n = 1e9, m = 10, run on a GPU box's host"))
+    with open(out_path, "w") as fp:
+        json.dump(deep, fp, indent=1)
+    print(f"config4 deep: {deep['entries']} trace entries in {deep['seconds']} s, {r['status']}", flush=True)
+
+
+def merge_config4_deep(deep_path):
+    """the deep run (make_config4_deep) into the fixture; its first two entries must be the
+    fixture's first_steps entries bit for bit"""
+    fx_path = os.path.join(OUT, "config4_n1e9.json")
+    fx = json.load(open(fx_path))
+    deep = json.load(open(deep_path))
+    can = fx["canon"]
+    for key in ("f", "gnorm", "c1", "c2"):
+        assert deep[key][:2] == can[key], key
+    assert deep["alpha"][:1] == can["alpha"]
+    fx["canon_deep"] = deep
+    with open(fx_path, "w") as fp:
+        json.dump(fx, fp, indent=1)
+    print(f"merged: {deep['entries']} entries", flush=True)
+
+
 def main(argv):
+    if argv[:1] == ["config4_deep"]:
+        make_config4_deep(argv[1], int(argv[2]) if len(argv) > 2 else 13)
+        return
+    if argv[:1] == ["merge_config4_deep"]:
+        merge_config4_deep(argv[1])
+        return
     if not os.path.exists(REF_BIN):
         sys.exit("build the reference first: make -C oracle ref")
     for nm in argv or list(CASES) + ["config4_n1e9"]:

@@ -6,6 +6,7 @@
 #                                    plain and under rocprofv3 (kernel trace), the default bench line
 #   bash tools/gpu_r06.sh gapbench   smoke, the stalled-collective test, the gap probe (plain, traced), bench
 #   bash tools/gpu_r06.sh waitab     LBFGS_WAIT=spin against adaptive, alternating, n = 1e8 and 1e4
+#   bash tools/gpu_r06.sh config4deep  configs[4]'s canonical oracle run at n = 1e9 on the box's host
 #   bash tools/gpu_r06.sh gappmc     SQ / TA counter passes over the gap probe (one pass per run)
 #   bash tools/gpu_r06.sh tests ARGS pytest -m gpu over ARGS (default: tests)
 #   bash tools/gpu_r06.sh bench ARGS one bench.py line -> gpurun_out/r06/bench.json
@@ -88,6 +89,10 @@ for n in ('1e8', '1e4'):
     print('$w', n, '$r', d['value'], d['host'])" | tee -a $O/wait_ab.txt
             done
         done ;;
+    config4deep)  # configs[4]'s whole canonical run on this box's host (~265 GB, OpenMP oracle)
+        timeout -k 10 1100 python -u tests/golden/make_fullsize.py config4_deep $O/config4_canon_deep.json 13 \
+            > $O/config4_deep.log 2>&1
+        rc=$?; echo "config4 deep rc=$rc"; tail -5 $O/config4_deep.log; exit $rc ;;
     gappmc)
         timeout -k 10 60 rocprofv3 -L > $O/counters.txt 2>&1; echo "list rc=$?"
         gap_pmc a SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
