@@ -14,9 +14,9 @@
 * configs[4] at its own size (n = 1e9, m = 10, backtracking): 8 processes over the mailboxes
   with the CUs partitioned between them (LBFGS_CU_PARTITION=1: the folded exchanges ungated, as
   on 8 distinct GPUs), history filled to h = 10, then 3 steps; bit-identical to the one-GPU run
-  at n = 1e9 (240 GB resident), whose first two trace entries are bit-exact with the canonical
-  fixture and whose f(x0), |g(x0)| are within 1e-10 of the reference's own
-  (tests/golden/fullsize/config4_n1e9.json).
+  at n = 1e9 (240 GB resident), whose every trace entry is bit-exact with the canonical oracle's
+  whole run at n = 1e9 (made on a GPU box's host, ~265 GB) and whose f(x0), |g(x0)| are within
+  1e-10 of the reference's own (tests/golden/fullsize/config4_n1e9.json).
 * configs[4]'s exchange exactly as bench.py's config4() runs it: 8 processes, no RCCL
   communicator (the xGMI peer mailboxes alone), the ticket stage 2 of segments >= 8192 elements
   (n = 8192^2 + 1, the smallest such n, L = 8320), m = 10, backtracking and Wolfe, plus the
@@ -171,12 +171,18 @@ def test_config4_n1e9_8_processes_cu_partitioned(tmp_path):
         for key in ("tr_f", "tr_gnorm", "tr_alpha"):
             assert np.array_equal(bits(o[key]), bits(tr[key])), (k, key)
         assert np.array_equal(o["tr_c1"], tr["tr_c1"]) and np.array_equal(o["tr_c2"], tr["tr_c2"]), k
-    # the canonical order's first two entries (x0 and the first step), bit for bit
-    can = fx["canon"]
-    assert np.array_equal(bits(tr["tr_f"][:2]), bits(f64(can["f"])))
-    assert np.array_equal(bits(tr["tr_gnorm"][:2]), bits(f64(can["gnorm"])))
-    assert np.array_equal(bits(tr["tr_alpha"][:1]), bits(f64(can["alpha"])))
-    assert np.array_equal(tr["tr_c1"][:2], u64(can["c1"])) and np.array_equal(tr["tr_c2"][:2], u64(can["c2"]))
+    # the canonical order, bit for bit: every state of the oracle's whole run at n = 1e9
+    # (canon_deep, made on a GPU box's host: tests/golden/make_fullsize.py config4_deep) where the
+    # fixture has it, else the first two entries (x0 and the first step)
+    can = fx.get("canon_deep") or fx["canon"]
+    k = min(len(tr["tr_f"]), len(can["f"]))
+    assert k >= (13 if "canon_deep" in fx else 2), (k, len(tr["tr_f"]), len(can["f"]))
+    assert np.array_equal(bits(tr["tr_f"][:k]), bits(f64(can["f"])[:k]))
+    assert np.array_equal(bits(tr["tr_gnorm"][:k]), bits(f64(can["gnorm"])[:k]))
+    ka = min(k, len(can["alpha"]))
+    ta, ca = tr["tr_alpha"][:ka], f64(can["alpha"])[:ka]
+    assert np.array_equal(np.isnan(ta), np.isnan(ca)) and np.array_equal(bits(ta[~np.isnan(ta)]), bits(ca[~np.isnan(ca)]))
+    assert np.array_equal(tr["tr_c1"][:k], u64(can["c1"])[:k]) and np.array_equal(tr["tr_c2"][:k], u64(can["c2"])[:k])
     # the reference itself at x0: f and |g| within 1e-10 relative; x0 has the reference's bits
     ref = fx["reference"]
     f_ref, g_ref = f64(ref["f_calls"])[0], f64(ref["grad_norm"])[0]
