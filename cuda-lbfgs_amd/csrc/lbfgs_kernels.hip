@@ -158,7 +158,11 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
     // host's waits on collectives (the communicator's init keeps LBFGS_RCCL_TIMEOUT)
     if (const char* e = getenv("LBFGS_DEBUG_RCCL_STALL")) {
         double st = 0.0, ws = 0.0;
-        if (sscanf(e, "%lf,%lf", &st, &ws) == 2 && st > 0.0 && ws > 0.0) {
+        if (sscanf(e, "%lf,%lf", &st, &ws) == 2 && st > 0.0 && ws > 0.0 &&
+            hipHostMalloc((void**)&c->stall_release_h, sizeof(unsigned), hipHostMallocMapped | hipHostMallocCoherent) ==
+                hipSuccess &&
+            hipHostGetDevicePointer((void**)&c->stall_release_d, c->stall_release_h, 0) == hipSuccess) {
+            *c->stall_release_h = 0;
             c->rccl_stall_ms = st;
             c->rccl_wait_s = ws;
         }
@@ -549,6 +553,7 @@ void lbk_destroy(lbk_ctx* c) {
     (void)hipFree(c->fold_wait);
     (void)hipFree(c->persist_gflag);
     if (c->coop_err_h) (void)hipHostFree(c->coop_err_h);
+    if (c->stall_release_h && !c->rccl_hung) (void)hipHostFree(c->stall_release_h);  // else a stall may still read it
     if (c->sp_h) (void)hipHostFree(c->sp_h);
     if (c->sp_vd) (void)hipFree(c->sp_vd);
     if (c->mark_ev) (void)hipEventDestroy(c->mark_ev);

@@ -2994,6 +2994,7 @@ struct lbk_ctx {
     double rccl_timeout_s;
     double rccl_stall_ms;  // test hook: LBFGS_DEBUG_RCCL_STALL (rccl_debug_stall)
     double rccl_wait_s;    // ... and its bound on the host's waits on collectives (0: rccl_timeout_s)
+    unsigned *stall_release_h, *stall_release_d;  // ... and its release word (pinned), set at the abort
     int rccl_hung;
     char err[256];
     // profiling
@@ -3307,6 +3308,7 @@ int rccl_stream_wait(lbk_ctx* c, const char* what) {
     }
     snprintf(c->err, sizeof c->err, "%s: the RCCL collective did not complete in %.1f s (communicator aborted)", what,
              bound);
+    if (c->stall_release_h) __atomic_store_n(c->stall_release_h, 1u, __ATOMIC_RELEASE);  // test hook's stand-in
     if (c->comm) (void)ncclCommAbort(c->comm);
     c->comm = nullptr;
     c->rccl_hung = 1;
@@ -3328,14 +3330,18 @@ int stream_wait(lbk_ctx* c, const char* what) {
 // RCCL collective that sleeps stall_ms on the device, standing in for a peer that stops answering,
 // and wait_s as the bound of the host's waits on collectives; the kernel ends on its own, so the GPU
 // is never held. tests/test_gpu_rccl.py sets a stall longer than the bound.
-__global__ void k_stall(unsigned long long ticks) {
+// The stand-in ends early when the host aborts the communicator (*release, pinned), as an aborted
+// RCCL collective stops: the abort then finds the stream moving again, as it would on a real hang.
+__global__ void k_stall(unsigned long long ticks, const unsigned* release) {
     const unsigned long long t0 = wall_clock64();
-    while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
+    while (wall_clock64() - t0 < ticks &&
+           __hip_atomic_load(release, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0u)
+        __builtin_amdgcn_s_sleep(127);
 }
 void rccl_debug_stall(lbk_ctx* c) {
-    if (c->rccl_stall_ms <= 0.0) return;
-    hipLaunchKernelGGL(k_stall, dim3(1), dim3(1), 0, c->stream,
-                       (unsigned long long)(c->rccl_stall_ms * c->wall_khz));
+    if (c->rccl_stall_ms <= 0.0 || !c->stall_release_d) return;
+    hipLaunchKernelGGL(k_stall, dim3(1), dim3(1), 0, c->stream, (unsigned long long)(c->rccl_stall_ms * c->wall_khz),
+                       (const unsigned*)c->stall_release_d);
 }
 
 // Sharded runs: each rank owns groups [g_lo, g_hi) of every result slot; gather them so
