@@ -145,7 +145,7 @@ int lbk_wait_stats(const lbk_ctx* c, double* slept_s, unsigned long long* waits,
  * y[(i + 1) % npairs] and s[i % npairs] (another pair every launch, as the passes: only q's tail
  * is left in the Infinity Cache by the launch before); mean microseconds per launch */
 int lbk_stream_probe(lbk_ctx* c, double* q, const double* const* ys, const double* const* ss, int npairs,
-                     int launches, double* us, int variant);
+                     int launches, double* us, int variant, double* const* outs);
 
 /* memory */
 double* lbk_vec_alloc(lbk_ctx* c);

@@ -493,17 +493,23 @@ int lbfgs_stream_probe(lbfgs_ctx* c, int launches, double* us, double* bytes) {
 }
 
 int lbfgs_stream_probe_variant(lbfgs_ctx* c, int variant, int launches, double* us, double* bytes) {
-    if (!c || !us || launches < 1 || variant < 0 || variant > 5) return LBFGS_ERR_BAD_ARG;
+    if (!c || !us || launches < 1 || variant < 0 || variant > 6) return LBFGS_ERR_BAD_ARG;
     if (!c->inited) return LBFGS_ERR_STATE;
     /* the written operand is a scratch vector, not the solver's q: nothing of the solve is touched
      * (q - 0 * y is q only while y is finite) */
     double* scratch = lbk_vec_alloc(c->dev);
     if (!scratch) return dev_err(c, -2);
-    const int rc = lbk_stream_probe(c->dev, scratch, (const double* const*)c->Y, (const double* const*)c->S, c->m + 1,
-                                    launches, us, variant);
+    double* outs[4] = {NULL, NULL, NULL, NULL}; /* variant 6: the commit's four written vectors */
+    int rc = 0;
+    for (int k = 0; variant == 6 && k < 4 && rc == 0; ++k)
+        if (!(outs[k] = lbk_vec_alloc(c->dev))) rc = -2;
+    if (rc == 0)
+        rc = lbk_stream_probe(c->dev, scratch, (const double* const*)c->Y, (const double* const*)c->S, c->m + 1,
+                              launches, us, variant, outs);
+    for (int k = 0; k < 4; ++k) lbk_vec_free(c->dev, outs[k]);
     lbk_vec_free(c->dev, scratch);
     if (rc != 0) return dev_err(c, rc);
-    if (bytes) *bytes = 32.0 * (double)c->geo->n_loc;
+    if (bytes) *bytes = (variant == 6 ? 64.0 : 32.0) * (double)c->geo->n_loc;
     return 0;
 }
 

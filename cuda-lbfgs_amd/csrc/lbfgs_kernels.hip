@@ -1580,7 +1580,7 @@ int lbk_coop_info(const lbk_ctx* c, int* coop_max, int* search_max, int* fallbac
 }
 
 int lbk_stream_probe(lbk_ctx* c, double* q, const double* const* ys, const double* const* ss, int npairs,
-                     int launches, double* us, int variant) {
+                     int launches, double* us, int variant, double* const* outs) {
     if (launches < 1 || !us || !q || !ys || !ss || npairs < 1) return -1;
     for (int k = 0; k < npairs; ++k)
         if (!ys[k] || !ss[k]) return -1;
@@ -1626,7 +1626,17 @@ int lbk_stream_probe(lbk_ctx* c, double* q, const double* const* ys, const doubl
         }
         const Geo g = kgeo(c);  // alternating walk, as the passes
         const double alpha = variant == 1 ? 1e-3 : 0.0;
-        if (variant <= 1) {
+        if (variant == 6) {  // the commit's 4 R + 4 W: x = q, g = y, r and s from the pool; 4 scratch outputs
+            if (!outs || !outs[0] || !outs[1] || !outs[2] || !outs[3]) {
+                c->rev_par = par;
+                return -1;
+            }
+            const double* rr = ys[(i + 2) % npairs];
+            NT_DISPATCH(c, hipLaunchKernelGGL(k_probe_commit<NT_>, dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream,
+                                              OpProbeCommit<NT_>{q, y, rr, s, outs[0], outs[1], outs[2], outs[3], 1e-3,
+                                                                 0.5},
+                                              g, c->partials));
+        } else if (variant <= 1) {
             NT_DISPATCH(c, hipLaunchKernelGGL(k_probe_stream<NT_>, dim3(nblocks(c)), dim3(LB_BLOCK), 0, c->stream, q, y,
                                               s, alpha, g, c->partials));
         } else {

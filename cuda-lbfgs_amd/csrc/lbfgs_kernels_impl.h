@@ -2942,6 +2942,56 @@ __global__ __launch_bounds__(LB_BLOCK) void k_probe_stream(double* q, const doub
     stream(OpAxpyDot<NT>{q, q, y, sv, alpha}, s, geo, acc);
     if (acc[0] == 1.0) sink[blockIdx.x] = acc[0];
 }
+// The commit's 4 R + 4 W mix (lbfgs_stream_probe_variant 6): x, g, r, s read and x_new, g_new, s, y
+// written with k_commit's loads, stores and cache policies (the TWOLOOP direction d = -(r + s c)),
+// in the two-loop passes' row geometry, elementwise arithmetic only and no stencil, f or stage 2:
+// what this box gives the commit's access pattern.
+template <bool NT>
+struct OpProbeCommit {
+    const double* __restrict__ x;
+    const double* __restrict__ g;
+    const double* __restrict__ r;
+    const double* __restrict__ s;
+    double* __restrict__ xn;
+    double* __restrict__ gn;
+    double* __restrict__ so;
+    double* __restrict__ yo;
+    double alpha, coef;
+    struct Row {
+        double2 x, g, r, s;
+    };
+    __device__ void load(Row& w, int64_t i) const {
+        w.x = ldx<NT>(x + i);
+        w.g = ldx<NT>(g + i);
+        w.r = ldd<NT>(r + i);
+        w.s = ldv<NT>(s + i);
+    }
+    template <bool MASK>
+    __device__ void apply(Row& w, int64_t i, int64_t, bool v0, bool v1, double (&acc)[1]) const {
+        double2 d, z, sv, yv;
+        d.x = -(w.r.x + w.s.x * coef);
+        d.y = -(w.r.y + w.s.y * coef);
+        z.x = w.x.x + alpha * d.x;
+        z.y = w.x.y + alpha * d.y;
+        sv.x = z.x - w.x.x;
+        sv.y = z.y - w.x.y;
+        yv.x = z.x - w.g.x;
+        yv.y = z.y - w.g.y;
+        st2x<MASK, NT>(xn + i, z, v0, v1);
+        st2x<MASK, NT>(gn + i, d, v0, v1);
+        st2h<MASK, NT>(so + i, sv, v0, v1);
+        st2h<MASK, NT>(yo + i, yv, v0, v1);
+        acc[0] = fma2<MASK>(w.g, d, acc[0], v0, v1);
+    }
+};
+template <bool NT>
+__global__ __launch_bounds__(LB_BLOCK) void k_probe_commit(OpProbeCommit<NT> op, Geo geo, double* sink) {
+    const Seg s = seg_setup(geo);
+    double acc[1] = {0.0};
+    stream(op, s, geo, acc);
+    if (acc[0] == 1.0) sink[blockIdx.x] = acc[0];
+}
+
 // Gap analysis (lbfgs_stream_probe_variant): the probe's stream with the pass's own segment
 // reduction after it - reduce_publish with the given Red (a plain partial store, or the collect
 // stage 2) - but no source slot read: k_axpy_dot without src_total.

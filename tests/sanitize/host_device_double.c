@@ -162,8 +162,8 @@ int lbk_wait_stats(const lbk_ctx* c, double* s, unsigned long long* w, int* a) {
     return 0;
 }
 int lbk_stream_probe(lbk_ctx* c, double* q, const double* const* ys, const double* const* ss, int npairs,
-                     int launches, double* us, int variant) {
-    (void)c, (void)q, (void)ys, (void)ss, (void)npairs, (void)launches, (void)variant;
+                     int launches, double* us, int variant, double* const* outs) {
+    (void)c, (void)q, (void)ys, (void)ss, (void)npairs, (void)launches, (void)variant, (void)outs;
     *us = 0.0;  /* no device: nothing to time */
     return 0;
 }

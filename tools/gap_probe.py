@@ -4,7 +4,8 @@ One process, one context at configs[2]'s geometry (n = 1e8, m = 10, Rosenbrock, 
 history filled), then rounds of lbfgs_stream_probe_variant alternating its six variants - the
 probe, the probe with alpha != 0, + the segment reduction stored plainly, + the collect stage 2,
 the product's own k_axpy_dot launch with alpha = 0 and != 0 - each 20 launches timed by one event
-pair, and between rounds 10 solver steps with per-launch events (the in-iteration k_axpy_dot).
+pair, and between rounds 10 solver steps with per-launch events (the in-iteration k_axpy_dot,
+k_axpy2_dot and k_commit); variant 6 is the commit's 4 R + 4 W mix (k_probe_commit) beside k_commit.
 Writes one JSON document (argv[1]). Under rocprofv3 the kernel trace separates the variants by
 kernel name (k_probe_stream / k_probe_stream2 / k_axpy_dot).
 
@@ -19,7 +20,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "cuda-lbfgs_amd"))
 import lbfgs_amd as L  # noqa: E402
 
-NAMES = ["probe", "probe_alpha", "probe+partial_store", "probe+collect", "k_axpy_dot_alpha0", "k_axpy_dot"]
+NAMES = ["probe", "probe_alpha", "probe+partial_store", "probe+collect", "k_axpy_dot_alpha0", "k_axpy_dot",
+         "commit_mix_4r4w"]
 
 
 def main():
@@ -29,14 +31,15 @@ def main():
     m = 10
     L.lib()
     x0 = L.x0_uniform(n, 42, -2.0, 2.0)
-    res = {"n": n, "m": m, "launches_per_sample": 20, "samples": {k: [] for k in NAMES}, "solver_axpy_dot_us": []}
+    res = {"n": n, "m": m, "launches_per_sample": 20, "samples": {k: [] for k in NAMES}, "solver_axpy_dot_us": [],
+           "solver_commit_us": [], "solver_axpy2_dot_us": []}
     with L.Context(n, m) as c:
         c.init("rosenbrock", x0, "backtracking", tolerance=1e-5)
         del x0
         c.step(m + 4)
         c.sync()
         for r in range(rounds):
-            order = list(range(6)) if r % 2 == 0 else list(range(5, -1, -1))
+            order = list(range(7)) if r % 2 == 0 else list(range(6, -1, -1))
             for v in order:
                 p = c.stream_probe(20, variant=v)
                 res["samples"][NAMES[v]].append(round(p["avg_launch_us"], 2))
@@ -45,14 +48,19 @@ def main():
             c.step(10)
             c.sync()
             c.prof_enable(False)
-            a = c.prof_get("axpy_dot")
-            res["solver_axpy_dot_us"].append(round(a["ms"] / a["launches"] * 1e3, 2))
+            for kind in ("axpy_dot", "axpy2_dot", "commit"):
+                a = c.prof_get(kind)
+                res[f"solver_{kind}_us"].append(round(a["ms"] / a["launches"] * 1e3, 2))
             print(f"round {r}: " + ", ".join(f"{k} {v[-1]}" for k, v in res["samples"].items())
                   + f", in-solve k_axpy_dot {res['solver_axpy_dot_us'][-1]}", flush=True)
     res["median_us"] = {k: sorted(v)[len(v) // 2] for k, v in res["samples"].items()}
-    res["median_us"]["solver_k_axpy_dot"] = sorted(res["solver_axpy_dot_us"])[len(res["solver_axpy_dot_us"]) // 2]
-    res["bytes_per_launch"] = 32.0 * n
-    res["tbps_median"] = {k: round(32.0 * n / (v * 1e-6) / 1e12, 3) for k, v in res["median_us"].items()}
+    for kind in ("axpy_dot", "axpy2_dot", "commit"):
+        v = sorted(res[f"solver_{kind}_us"])
+        res["median_us"][f"solver_k_{kind}"] = v[len(v) // 2]
+    res["bytes_per_launch"] = {k: (64.0 if k in ("commit_mix_4r4w", "solver_k_commit") else 32.0) * n
+                               for k in res["median_us"]}
+    res["tbps_median"] = {k: round(res["bytes_per_launch"][k] / (v * 1e-6) / 1e12, 3)
+                          for k, v in res["median_us"].items()}
     res["build"] = L.build_info()[0]
     res["time"] = time.strftime("%Y-%m-%d %H:%M:%S")
     json.dump(res, open(out, "w"), indent=1)
