@@ -7,6 +7,7 @@
 #   bash tools/gpu_r06.sh gapbench   smoke, the stalled-collective test, the gap probe (plain, traced), bench
 #   bash tools/gpu_r06.sh waitab     LBFGS_WAIT=spin against adaptive, alternating, n = 1e8 and 1e4
 #   bash tools/gpu_r06.sh config4deep  configs[4]'s canonical oracle run at n = 1e9 on the box's host
+#   bash tools/gpu_r06.sh cleantrace   kernel trace of the bench steps without any HIP events
 #   bash tools/gpu_r06.sh gappmc     SQ / TA counter passes over the gap probe (one pass per run)
 #   bash tools/gpu_r06.sh tests ARGS pytest -m gpu over ARGS (default: tests)
 #   bash tools/gpu_r06.sh bench ARGS one bench.py line -> gpurun_out/r06/bench.json
@@ -93,6 +94,11 @@ for n in ('1e8', '1e4'):
         timeout -k 10 1100 python -u tests/golden/make_fullsize.py config4_deep $O/config4_canon_deep.json 13 \
             > $O/config4_deep.log 2>&1
         rc=$?; echo "config4 deep rc=$rc"; tail -5 $O/config4_deep.log; exit $rc ;;
+    cleantrace)  # the bench's timed steps under a kernel trace with no HIP events anywhere (--no-prof)
+        timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/clean_trace -o run --output-format csv -- \
+            python3 bench.py --steps 40 --warmup 10 --no-cpu-baseline --no-prof --no-box-probe --no-vector-free \
+            --no-persistent > $O/clean_trace.log 2>&1
+        rc=$?; echo "clean trace rc=$rc"; tail -2 $O/clean_trace.log | cut -c1-300; exit $rc ;;
     gappmc)
         timeout -k 10 60 rocprofv3 -L > $O/counters.txt 2>&1; echo "list rc=$?"
         gap_pmc a SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
