@@ -21,7 +21,8 @@ sys.path.insert(0, os.path.join(ROOT, "cuda-lbfgs_amd"))
 import lbfgs_amd as L  # noqa: E402
 
 NAMES = ["probe", "probe_alpha", "probe+partial_store", "probe+collect", "k_axpy_dot_alpha0", "k_axpy_dot",
-         "commit_mix_4r4w"]
+         "commit_mix_4r4w", "probe_on_solver_q", "probe_alpha_on_solver_q", "k_axpy_dot_on_solver_q"]
+VARIANTS = [0, 1, 2, 3, 4, 5, 6, 8, 9, 13]  # + 8: on the solver's own q
 
 
 def main():
@@ -39,9 +40,9 @@ def main():
         c.step(m + 4)
         c.sync()
         for r in range(rounds):
-            order = list(range(7)) if r % 2 == 0 else list(range(6, -1, -1))
+            order = list(range(len(VARIANTS))) if r % 2 == 0 else list(range(len(VARIANTS) - 1, -1, -1))
             for v in order:
-                p = c.stream_probe(20, variant=v)
+                p = c.stream_probe(20, variant=VARIANTS[v])
                 res["samples"][NAMES[v]].append(round(p["avg_launch_us"], 2))
             c.prof_reset()
             c.prof_enable(True)
