@@ -493,12 +493,13 @@ int lbfgs_stream_probe(lbfgs_ctx* c, int launches, double* us, double* bytes) {
 }
 
 int lbfgs_stream_probe_variant(lbfgs_ctx* c, int variant, int launches, double* us, double* bytes) {
-    if (!c || !us || launches < 1 || variant < 0 || (variant & 7) > 6 || variant > 15) return LBFGS_ERR_BAD_ARG;
+    if (!c || !us || launches < 1 || variant < 0 || (variant & 7) > 6 || variant > 31) return LBFGS_ERR_BAD_ARG;
     if (!c->inited) return LBFGS_ERR_STATE;
     /* + 8: the work vector is the solver's own q (variants 0-5), which the next iteration's first
      * two-loop pass rewrites from g before anything reads it (gap analysis: the same buffer as the
      * in-solve passes) */
     const int own_q = (variant & 8) != 0 && (variant & 7) <= 5;
+    const int fill = (variant & 16) != 0; /* + 16: the scratch vector starts as a copy of y_0, not zeros */
     variant &= 7;
     /* the written operand is a scratch vector, not the solver's q: nothing of the solve is touched
      * (q - 0 * y is q only while y is finite) */
@@ -508,6 +509,7 @@ int lbfgs_stream_probe_variant(lbfgs_ctx* c, int variant, int launches, double* 
     int rc = 0;
     for (int k = 0; variant == 6 && k < 4 && rc == 0; ++k)
         if (!(outs[k] = lbk_vec_alloc(c->dev))) rc = -2;
+    if (rc == 0 && fill && !own_q) rc = lbk_copy(c->dev, scratch, c->Y[0]);
     if (rc == 0)
         rc = lbk_stream_probe(c->dev, own_q ? c->q : scratch, (const double* const*)c->Y, (const double* const*)c->S,
                               c->m + 1, launches, us, variant, outs);

@@ -266,7 +266,8 @@ int lbfgs_stream_probe(lbfgs_ctx* ctx, int launches, double* us, double* bytes);
  * slot read, collect stage 2) with alpha = 0 / != 0, chained through two scratch slots; 6 = the
  * commit's 4 reads + 4 writes (k_commit's loads, stores and cache policies, no stencil, f or
  * reductions) into scratch vectors: *bytes = 64 n_loc. Variants 8-13: 0-5 on the solver's own
- * work vector q instead of a scratch one (the next iteration rewrites q before reading it). */
+ * work vector q instead of a scratch one (the next iteration rewrites q before reading it);
+ * variants 16-22: 0-6 with the scratch vector filled with a copy of y_0 first (not zeros). */
 int lbfgs_stream_probe_variant(lbfgs_ctx* ctx, int variant, int launches, double* us, double* bytes);
 /* Emulated ranks: 'world' contexts driven by threads of ONE process (e.g. on one GPU, one
  * stream each) exchange their reductions through host memory instead of RCCL. Same data path

@@ -21,8 +21,10 @@ sys.path.insert(0, os.path.join(ROOT, "cuda-lbfgs_amd"))
 import lbfgs_amd as L  # noqa: E402
 
 NAMES = ["probe", "probe_alpha", "probe+partial_store", "probe+collect", "k_axpy_dot_alpha0", "k_axpy_dot",
-         "commit_mix_4r4w", "probe_on_solver_q", "probe_alpha_on_solver_q", "k_axpy_dot_on_solver_q"]
-VARIANTS = [0, 1, 2, 3, 4, 5, 6, 8, 9, 13]  # + 8: on the solver's own q
+         "commit_mix_4r4w", "probe_on_solver_q", "probe_alpha_on_solver_q", "k_axpy_dot_on_solver_q",
+         "probe_scratch_random", "k_axpy_dot_scratch_random", "commit_mix_4r4w_x_random"]
+# + 8: on the solver's own q; + 16: the scratch vector filled with a copy of y_0 (random data, not zeros)
+VARIANTS = [0, 1, 2, 3, 4, 5, 6, 8, 9, 13, 16, 21, 22]
 
 
 def main():
@@ -58,7 +60,7 @@ def main():
     for kind in ("axpy_dot", "axpy2_dot", "commit"):
         v = sorted(res[f"solver_{kind}_us"])
         res["median_us"][f"solver_k_{kind}"] = v[len(v) // 2]
-    res["bytes_per_launch"] = {k: (64.0 if k in ("commit_mix_4r4w", "solver_k_commit") else 32.0) * n
+    res["bytes_per_launch"] = {k: (64.0 if k in ("commit_mix_4r4w", "commit_mix_4r4w_x_random", "solver_k_commit") else 32.0) * n
                                for k in res["median_us"]}
     res["tbps_median"] = {k: round(res["bytes_per_launch"][k] / (v * 1e-6) / 1e12, 3)
                           for k, v in res["median_us"].items()}
