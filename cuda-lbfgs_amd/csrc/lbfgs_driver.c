@@ -520,6 +520,39 @@ int lbfgs_stream_probe_variant(lbfgs_ctx* c, int variant, int launches, double* 
     return 0;
 }
 
+/* the context's vectors in allocation order (lbfgs_ctx_create): x, g, xn, gn, d, q, r, gt, then
+ * S_0, Y_0, S_1, Y_1, ...; index 8 + 2 (m + 1) = a scratch vector allocated for the call */
+static double* vec_by_index(lbfgs_ctx* c, int k, double* scratch) {
+    double* w[] = {c->x, c->g, c->xn, c->gn, c->d, c->q, c->r, c->gt};
+    if (k >= 0 && k < 8) return w[k];
+    k -= 8;
+    if (k >= 0 && k < 2 * (c->m + 1)) return (k & 1) ? c->Y[k >> 1] : c->S[k >> 1];
+    return k == 2 * (c->m + 1) ? scratch : NULL;
+}
+
+int lbfgs_vector_address(lbfgs_ctx* c, int k, uint64_t* addr) {
+    if (!c || !addr) return LBFGS_ERR_BAD_ARG;
+    double* v = vec_by_index(c, k, NULL);
+    if (!v) return LBFGS_ERR_BAD_ARG;
+    *addr = (uint64_t)(uintptr_t)v;
+    return 0;
+}
+
+int lbfgs_stream_probe_vectors(lbfgs_ctx* c, int qk, int yk, int sk, int launches, double* us) {
+    if (!c || !us || launches < 1) return LBFGS_ERR_BAD_ARG;
+    if (!c->inited) return LBFGS_ERR_STATE;
+    double* scratch = lbk_vec_alloc(c->dev);
+    if (!scratch) return dev_err(c, -2);
+    double* q = vec_by_index(c, qk, scratch);
+    const double* y = vec_by_index(c, yk, scratch);
+    const double* s = vec_by_index(c, sk, scratch);
+    int rc = (q && y && s) ? 0 : -1;
+    /* alpha = 0: q is written back unchanged (the vectors are finite at any step of a solve) */
+    if (rc == 0) rc = lbk_stream_probe(c->dev, q, &y, &s, 1, launches, us, 0, NULL);
+    lbk_vec_free(c->dev, scratch);
+    return rc == 0 ? 0 : rc == -1 ? LBFGS_ERR_BAD_ARG : dev_err(c, rc);
+}
+
 /* ------------------------------------------------------------------------------------------
  * Host-callback objective (LBFGS_OBJ_HOST; single rank). The device forms every point the
  * objective is called at (z = x + alpha d, as the commit will form x_new) and the host calls

@@ -126,6 +126,8 @@ def lib():
     L.lbfgs_wait_stats.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_uint64), C.POINTER(C.c_int)]
     L.lbfgs_stream_probe.argtypes = [vp, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double)]
     L.lbfgs_stream_probe_variant.argtypes = [vp, C.c_int, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double)]
+    L.lbfgs_stream_probe_vectors.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_double)]
+    L.lbfgs_vector_address.argtypes = [vp, C.c_int, C.POINTER(C.c_uint64)]
     L.lbfgs_prof_enable.argtypes = [vp, C.c_int]
     L.lbfgs_prof_enable.restype = None
     L.lbfgs_prof_reset.argtypes = [vp]
@@ -147,7 +149,7 @@ EXPORTED_SYMBOLS = [
     "lbfgs_dev_twoloop", "lbfgs_dev_elementwise", "lbfgs_line_search", "lbfgs_prof_enable",
     "lbfgs_prof_reset", "lbfgs_prof_get", "lbfgs_peer_handle", "lbfgs_peer_connect", "lbfgs_peer_enable", "lbfgs_rccl_attach",
     "lbfgs_exchange_backend", "lbfgs_exchange_fold", "lbfgs_exchange_latency", "lbfgs_device_count", "lbfgs_set_dense_quadratic", "lbfgs_build_info",
-    "lbfgs_spec_stats", "lbfgs_cu_partition", "lbfgs_stream_probe", "lbfgs_stream_probe_variant", "lbfgs_coop_info", "lbfgs_wait_stats", "lbfgs_search_stats",
+    "lbfgs_spec_stats", "lbfgs_cu_partition", "lbfgs_stream_probe", "lbfgs_stream_probe_variant", "lbfgs_stream_probe_vectors", "lbfgs_vector_address", "lbfgs_coop_info", "lbfgs_wait_stats", "lbfgs_search_stats",
 ]
 PEER_HANDLE_BYTES = 64
 BACKENDS = {0: "single", 1: "rccl", 2: "xgmi", 3: "host-group"}
@@ -371,6 +373,21 @@ class Context:
         a, b, f = C.c_int(), C.c_int(), C.c_int()
         lib().lbfgs_coop_info(self.h, C.byref(a), C.byref(b), C.byref(f))
         return dict(coop_max=a.value, search_max=b.value, fallbacks=f.value)
+
+    def stream_probe_vectors(self, q, y, s, launches=20):
+        """the probe's stream over three of the context's vectors by allocation index
+        (lbfgs_stream_probe_vectors): mean microseconds per launch"""
+        us = C.c_double()
+        rc = lib().lbfgs_stream_probe_vectors(self.h, int(q), int(y), int(s), int(launches), C.byref(us))
+        if rc != 0:
+            self._err("lbfgs_stream_probe_vectors", rc)
+        return us.value
+
+    def vector_address(self, k):
+        a = C.c_uint64()
+        if lib().lbfgs_vector_address(self.h, int(k), C.byref(a)) != 0:
+            return None
+        return a.value
 
     def wait_stats(self):
         """host waits on completion words: dict(slept_s, waits, adaptive) (lbfgs_wait_stats)"""

@@ -269,6 +269,12 @@ int lbfgs_stream_probe(lbfgs_ctx* ctx, int launches, double* us, double* bytes);
  * work vector q instead of a scratch one (the next iteration rewrites q before reading it);
  * variants 16-22: 0-6 with the scratch vector filled with a copy of y_0 first (not zeros). */
 int lbfgs_stream_probe_variant(lbfgs_ctx* ctx, int variant, int launches, double* us, double* bytes);
+/* Diagnostic: the probe's stream (variant 0, alpha = 0) over three of the context's own vectors,
+ * by index in allocation order: 0-7 x, g, xn, gn, d, q, r, gt; 8 + 2p S_p, 9 + 2p Y_p; 8 + 2(m + 1)
+ * a scratch vector allocated for the call. The first is written back unchanged. */
+int lbfgs_stream_probe_vectors(lbfgs_ctx* ctx, int q, int y, int s, int launches, double* us);
+/* Diagnostic: the device address of vector k (the indexing above; not the scratch one) */
+int lbfgs_vector_address(lbfgs_ctx* ctx, int k, uint64_t* addr);
 /* Emulated ranks: 'world' contexts driven by threads of ONE process (e.g. on one GPU, one
  * stream each) exchange their reductions through host memory instead of RCCL. Same data path
  * and results as the RCCL shards; used to test sharding on a single GPU. */
