@@ -573,7 +573,14 @@ const char* lbk_last_error(const lbk_ctx* c) { return c ? c->err : "no context";
 
 double* lbk_vec_alloc(lbk_ctx* c) {
     double* p = nullptr;
-    if (hipMalloc(&p, sizeof(double) * c->vec_doubles) != hipSuccess) {
+    const char* ae = getenv("LBFGS_ALLOC");  // A/B (temporary): 4 = physically contiguous vectors
+    const int contig = ae && atoi(ae) == 4;
+    if (contig && hipExtMallocWithFlags((void**)&p, sizeof(double) * c->vec_doubles, hipDeviceMallocContiguous) != hipSuccess) {
+        (void)hipGetLastError();
+        p = nullptr;
+        fprintf(stderr, "lbfgs: contiguous allocation refused, plain hipMalloc\n");
+    }
+    if (!p && hipMalloc(&p, sizeof(double) * c->vec_doubles) != hipSuccess) {
         snprintf(c->err, sizeof c->err, "hipMalloc of %lld doubles failed", (long long)c->vec_doubles);
         return nullptr;
     }
