@@ -500,6 +500,7 @@ def _measure(a, D, ctx, x0, rank, world, uid, unfused, vector_free, box_probe, d
                     "slept_share": round((w1["slept_s"] - w0["slept_s"]) / max(t_local, 1e-9), 4),
                     "waits": w1["waits"] - w0["waits"], "wait_mode": "adaptive" if w1["adaptive"] else "spin"}
                    if w0 and w1 else None)
+    res["vector_fallbacks"] = run(lambda: ctx.vector_fallbacks)
     res["history_fill"] = fill["iterations"]
     res["warm_counters"] = {k: warm[k] for k in ("trials_f", "trials_fg", "commits", "passes")} if warm else None
     res["box_probe"] = probe
@@ -1034,6 +1035,8 @@ def main():
             "exchange_fallback": fallback,
             "kernel_busy": prof.get("_busy"),
             "host": res.get("host"),
+            "vectors": {"contiguous_fallbacks": res.get("vector_fallbacks"),
+                        "allocation": "one physically contiguous allocation per vector (hipDeviceMallocContiguous)"},
             "cpu_baseline": cpu,
             "reference_parity": parity,
             "solver": {"status": res["status"], "f": res["f"], "gnorm": res["gnorm"],

@@ -140,6 +140,8 @@ int lbk_coop_info(const lbk_ctx* c, int* coop_max, int* search_max, int* fallbac
 /* host waits on completion words: seconds slept in the spin-then-sleep phase, waits completed,
  * whether the wait is adaptive (LBFGS_WAIT) */
 int lbk_wait_stats(const lbk_ctx* c, double* slept_s, unsigned long long* waits, int* adaptive);
+/* vectors allocated with a plain hipMalloc because a physically contiguous one was refused */
+int lbk_vec_fallbacks(const lbk_ctx* c);
 /* box probe: `launches` back-to-back 3 R + 1 W streams over (q, y, s) in the two-loop passes'
  * geometry and cache policy, q written back unchanged; launch i reads the pair pool's
  * y[(i + 1) % npairs] and s[i % npairs] (another pair every launch, as the passes: only q's tail

@@ -348,41 +348,11 @@ static int ctx_create(lbfgs_ctx** out, int64_t n, int m, int device, int rank, i
     c->geo = lbk_geometry(c->dev);
     double** v[] = {&c->x, &c->g, &c->xn, &c->gn, &c->d, &c->q, &c->r, &c->gt};
     int ok = 1;
-    /* A/B of the vectors' placement (LBFGS_ALLOC, temporary): 0 work vectors then the pool; 1 the
-     * pool first; 2 as 0, then every work vector allocated again after the pool (the first copies
-     * freed); 3 as 0 with a 64 MiB spacer allocation between consecutive vectors */
-    int amode = 0;
-    {
-        const char* e = getenv("LBFGS_ALLOC");
-        if (e) amode = atoi(e);
+    for (size_t i = 0; i < sizeof v / sizeof v[0]; ++i) ok &= (*v[i] = lbk_vec_alloc(c->dev)) != NULL;
+    for (int i = 0; i <= m; ++i) {
+        ok &= (c->S[i] = lbk_vec_alloc(c->dev)) != NULL;
+        ok &= (c->Y[i] = lbk_vec_alloc(c->dev)) != NULL;
     }
-    double* spacers[MMAX + 10];
-    int nsp = 0;
-    if (amode == 1) {
-        for (int i = 0; i <= m; ++i) {
-            ok &= (c->S[i] = lbk_vec_alloc(c->dev)) != NULL;
-            ok &= (c->Y[i] = lbk_vec_alloc(c->dev)) != NULL;
-        }
-        for (size_t i = 0; i < sizeof v / sizeof v[0]; ++i) ok &= (*v[i] = lbk_vec_alloc(c->dev)) != NULL;
-    } else {
-        for (size_t i = 0; i < sizeof v / sizeof v[0]; ++i) {
-            ok &= (*v[i] = lbk_vec_alloc(c->dev)) != NULL;
-            if (amode == 3 && (spacers[nsp] = lbk_vec_alloc(c->dev)) != NULL) ++nsp;
-        }
-        for (int i = 0; i <= m; ++i) {
-            ok &= (c->S[i] = lbk_vec_alloc(c->dev)) != NULL;
-            ok &= (c->Y[i] = lbk_vec_alloc(c->dev)) != NULL;
-        }
-        if (amode == 2 && ok) {
-            double* old[8];
-            for (size_t i = 0; i < sizeof v / sizeof v[0]; ++i) {
-                old[i] = *v[i];
-                ok &= (*v[i] = lbk_vec_alloc(c->dev)) != NULL;
-            }
-            for (size_t i = 0; i < sizeof v / sizeof v[0]; ++i) lbk_vec_free(c->dev, old[i]);
-        }
-    }
-    for (int i = 0; i < nsp; ++i) lbk_vec_free(c->dev, spacers[i]);
     if (!ok) {
         fprintf(stderr, "lbfgs_ctx_create: %s\n", lbk_last_error(c->dev));
         free_vectors(c);
@@ -505,6 +475,8 @@ int lbfgs_exchange_latency(lbfgs_ctx* c, int backend, int components, int iters,
 }
 
 int lbfgs_cu_partition(const lbfgs_ctx* c) { return c ? lbk_cu_partition(c->dev) : LBFGS_ERR_BAD_ARG; }
+
+int lbfgs_vector_fallbacks(const lbfgs_ctx* c) { return c ? lbk_vec_fallbacks(c->dev) : LBFGS_ERR_BAD_ARG; }
 
 int lbfgs_wait_stats(const lbfgs_ctx* c, double* slept_s, uint64_t* waits, int* adaptive) {
     if (!c) return LBFGS_ERR_BAD_ARG;

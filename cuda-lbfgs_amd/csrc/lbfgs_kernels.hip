@@ -571,14 +571,22 @@ void lbk_destroy(lbk_ctx* c) {
 const lbk_geo* lbk_geometry(const lbk_ctx* c) { return &c->geo; }
 const char* lbk_last_error(const lbk_ctx* c) { return c ? c->err : "no context"; }
 
+// Every vector is one physically contiguous allocation (hipDeviceMallocContiguous) where the driver
+// can give one, else a plain hipMalloc. Measured at n = 1e8 (profiles/r06/alloc_ab/, alternating
+// contexts in one process): 88.5-89.0 it/s against 85.4-87.1, k_axpy_dot 534-540 us against 546-551,
+// the commit 1060-1082 against 1150-1184 (plain allocations streamed at a rate that changed from
+// context to context: the probe's stream over the solver's own q ran 4 % below the same stream over
+// a vector allocated later, whatever the pair; profiles/r06/gap/). A/B: -DLBK_VEC_PLAIN=1.
+#ifndef LBK_VEC_PLAIN
+#define LBK_VEC_PLAIN 0
+#endif
 double* lbk_vec_alloc(lbk_ctx* c) {
     double* p = nullptr;
-    const char* ae = getenv("LBFGS_ALLOC");  // A/B (temporary): 4 = physically contiguous vectors
-    const int contig = ae && atoi(ae) == 4;
-    if (contig && hipExtMallocWithFlags((void**)&p, sizeof(double) * c->vec_doubles, hipDeviceMallocContiguous) != hipSuccess) {
+    if (!LBK_VEC_PLAIN &&
+        hipExtMallocWithFlags((void**)&p, sizeof(double) * c->vec_doubles, hipDeviceMallocContiguous) != hipSuccess) {
         (void)hipGetLastError();
         p = nullptr;
-        fprintf(stderr, "lbfgs: contiguous allocation refused, plain hipMalloc\n");
+        c->vec_plain_fallbacks++;
     }
     if (!p && hipMalloc(&p, sizeof(double) * c->vec_doubles) != hipSuccess) {
         snprintf(c->err, sizeof c->err, "hipMalloc of %lld doubles failed", (long long)c->vec_doubles);
@@ -1571,6 +1579,8 @@ int lbk_peer_enable(lbk_ctx* c, int on) {
 }
 
 int lbk_cu_partition(const lbk_ctx* c) { return c->cu_part ? c->cu_count : 0; }
+
+int lbk_vec_fallbacks(const lbk_ctx* c) { return c->vec_plain_fallbacks; }
 
 int lbk_wait_stats(const lbk_ctx* c, double* slept_s, unsigned long long* waits, int* adaptive) {
     if (slept_s) *slept_s = c->wait_slept_s;

@@ -3127,6 +3127,7 @@ struct lbk_ctx {
     unsigned long long search_epoch;
     // host waits on the completion words (small_wait): spin-then-sleep, the last four waits' durations
     // per word, and the time slept / waits completed (lbfgs_wait_stats)
+    int vec_plain_fallbacks;  // vectors the driver could not give contiguous (lbk_vec_alloc)
     int wait_adaptive;
     double wait_hist[4][4];
     unsigned wait_pos[4];

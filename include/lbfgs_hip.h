@@ -251,6 +251,10 @@ int lbfgs_coop_info(const lbfgs_ctx* ctx, int* coop_max, int* search_max, int* f
  * it and spins for the rest; LBFGS_WAIT=spin: spin throughout. *slept_s = seconds slept so far,
  * *waits = waits completed, *adaptive = the mode. */
 int lbfgs_wait_stats(const lbfgs_ctx* ctx, double* slept_s, uint64_t* waits, int* adaptive);
+/* Every n-vector is one physically contiguous device allocation where the driver grants one
+ * (+3 % at n = 1e8); this returns how many of the context's allocations fell back to
+ * a plain hipMalloc. */
+int lbfgs_vector_fallbacks(const lbfgs_ctx* ctx);
 /* Diagnostic (no reference counterpart): `launches` back-to-back streams of 3 reads + 1 write
  * over a scratch work vector and the context's history vectors (y, s of the pair pool, another
  * pair every launch as the two-loop passes read them) in the passes' geometry and cache policy;

@@ -154,6 +154,10 @@ int lbk_coop_info(const lbk_ctx* c, int* a, int* b, int* f) {
     if (f) *f = 0;
     return 0;
 }
+int lbk_vec_fallbacks(const lbk_ctx* c) {
+    (void)c;
+    return 0;
+}
 int lbk_wait_stats(const lbk_ctx* c, double* s, unsigned long long* w, int* a) {
     (void)c;
     if (s) *s = 0.0;

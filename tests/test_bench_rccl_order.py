@@ -60,6 +60,8 @@ class StubContext:
     def wait_stats(self):
         return dict(slept_s=0.0, waits=0, adaptive=True)
 
+    vector_fallbacks = 0
+
     def prof_reset(self):
         pass
 
