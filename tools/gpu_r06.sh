@@ -32,7 +32,7 @@ smoke() {
 
 tests() {
     local args=("$@"); [ ${#args[@]} -eq 0 ] && args=(tests)
-    timeout -k 10 1000 python -u -m pytest "${args[@]}" -m gpu -v --timeout 300 --timeout-method thread \
+    timeout -k 10 1000 python -u -m pytest "${args[@]}" -m gpu -v --durations=40 --timeout 300 --timeout-method thread \
         > $O/pytest.log 2>&1 &
     local pid=$! n=0
     while kill -0 $pid 2> /dev/null; do
