@@ -3407,11 +3407,15 @@ int exchange_buf(lbk_ctx* c, double* base, int ks, double* host_mirror = nullptr
     }
     if (c->grp) {
         lbk_group* G = c->grp;
+        HIPCHK(c, hipMemcpyAsync(G->table + c->geo.g_lo * ks, base + c->geo.g_lo * ks, sizeof(double) * per,
+                                 hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
-        HIPCHK(c, hipMemcpy(G->table + c->geo.g_lo * ks, base + c->geo.g_lo * ks,
-                            sizeof(double) * per, hipMemcpyDeviceToHost));
         pthread_barrier_wait(&G->bar);
-        HIPCHK(c, hipMemcpy(base, G->table, sizeof(double) * LBK_GROUPS * ks, hipMemcpyHostToDevice));
+        // on the solver stream, and waited for: a synchronous hipMemcpy from pageable memory may
+        // return once the bytes are staged, before they land, and it does not order this rank's
+        // next kernels (a non-blocking stream) behind it - they could read the slot's old groups
+        HIPCHK(c, hipMemcpyAsync(base, G->table, sizeof(double) * LBK_GROUPS * ks, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
         pthread_barrier_wait(&G->bar);
         return 0;
     }
