@@ -1,9 +1,11 @@
-// tools/contig_probe.hip — are host uploads into physically contiguous allocations
-// (hipExtMallocWithFlags(..., hipDeviceMallocContiguous)) seen by the next kernel on the stream?
-// T host threads, one stream and one device buffer each (contiguous or plain hipMalloc), repeat:
-// hipMemsetAsync(0) -> sync -> hipMemcpyAsync H2D from pageable random data -> sync -> a kernel
-// sums the buffer's bit patterns (integer, exact) -> compare with the host's sum. Reports the
-// mismatches per mode. usage: contig_probe [threads] [iterations] [doubles]
+// tools/contig_probe.hip — are host transfers into / out of physically contiguous allocations
+// (hipExtMallocWithFlags(..., hipDeviceMallocContiguous)) coherent with the kernels around them?
+// T host threads, one non-blocking stream and one device buffer each, repeating either
+//   up:   hipMemsetAsync(0) -> sync -> hipMemcpyAsync H2D of random data -> sync -> a kernel sums the
+//         buffer (integer, exact) -> compare with the host's sum;
+//   down: a kernel fills the buffer with a pattern -> sync -> hipMemcpyAsync D2H -> sync -> compare,
+// for plain / contiguous allocations and pageable / pinned host buffers. Reports mismatches per case.
+// usage: contig_probe [threads] [iterations] [doubles]
 #include <hip/hip_runtime.h>
 
 #include <atomic>
@@ -21,7 +23,12 @@ __global__ void k_sum(const unsigned long long* __restrict__ x, long long n, uns
     if ((threadIdx.x & 63) == 0) atomicAdd(out, a);
 }
 
-static int run(int contig, int T, int iters, long long n) {
+__global__ void k_fill(unsigned long long* __restrict__ x, long long n, unsigned long long key) {
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+        x[i] = (unsigned long long)i * 0x9e3779b97f4a7c15ull ^ key;
+}
+
+static int run(int contig, int pinned, int down, int T, int iters, long long n) {
     std::atomic<int> bad{0}, errs{0};
     auto work = [&](int t) {
         hipStream_t s;
@@ -32,24 +39,45 @@ static int run(int contig, int T, int iters, long long n) {
         hipError_t e = contig ? hipExtMallocWithFlags((void**)&d, bytes, hipDeviceMallocContiguous)
                               : hipMalloc((void**)&d, bytes);
         if (e != hipSuccess || hipMalloc((void**)&dout, 8) != hipSuccess) { errs++; return; }
-        std::vector<unsigned long long> h((size_t)n);
-        unsigned long long seed = 0x9e3779b97f4a7c15ull * (t + 1) + (unsigned long long)contig;
-        for (int it = 0; it < iters; ++it) {
-            unsigned long long want = 0;
-            for (long long i = 0; i < n; ++i) {
-                seed ^= seed << 13; seed ^= seed >> 7; seed ^= seed << 17;
-                h[(size_t)i] = seed;
-                want += seed * (unsigned long long)(i + 1);
-            }
-            unsigned long long got = 0;
-            if (hipMemsetAsync(d, 0, bytes, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess ||
-                hipMemcpyAsync(d, h.data(), bytes, hipMemcpyHostToDevice, s) != hipSuccess ||
-                hipStreamSynchronize(s) != hipSuccess || hipMemsetAsync(dout, 0, 8, s) != hipSuccess) { errs++; break; }
-            hipLaunchKernelGGL(k_sum, dim3(512), dim3(256), 0, s, d, n, dout);
-            if (hipMemcpyAsync(&got, dout, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
-                hipStreamSynchronize(s) != hipSuccess) { errs++; break; }
-            if (got != want) bad++;
+        std::vector<unsigned long long> hv;
+        unsigned long long* h = nullptr;
+        if (pinned) {
+            if (hipHostMalloc((void**)&h, bytes, hipHostMallocDefault) != hipSuccess) { errs++; return; }
+        } else {
+            hv.resize((size_t)n);
+            h = hv.data();
         }
+        unsigned long long seed = 0x9e3779b97f4a7c15ull * (t + 1) + (unsigned long long)(contig + 2 * pinned);
+        for (int it = 0; it < iters; ++it) {
+            if (!down) {
+                unsigned long long want = 0;
+                for (long long i = 0; i < n; ++i) {
+                    seed ^= seed << 13; seed ^= seed >> 7; seed ^= seed << 17;
+                    h[i] = seed;
+                    want += seed * (unsigned long long)(i + 1);
+                }
+                unsigned long long got = 0;
+                if (hipMemsetAsync(d, 0, bytes, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess ||
+                    hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, s) != hipSuccess ||
+                    hipStreamSynchronize(s) != hipSuccess || hipMemsetAsync(dout, 0, 8, s) != hipSuccess) { errs++; break; }
+                hipLaunchKernelGGL(k_sum, dim3(512), dim3(256), 0, s, d, n, dout);
+                if (hipMemcpyAsync(&got, dout, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+                    hipStreamSynchronize(s) != hipSuccess) { errs++; break; }
+                if (got != want) bad++;
+            } else {
+                const unsigned long long key = seed + (unsigned long long)it * 7919ull;
+                memset(h, 0, bytes);
+                hipLaunchKernelGGL(k_fill, dim3(512), dim3(256), 0, s, d, n, key);
+                if (hipStreamSynchronize(s) != hipSuccess ||
+                    hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, s) != hipSuccess ||
+                    hipStreamSynchronize(s) != hipSuccess) { errs++; break; }
+                long long wrong = 0;
+                for (long long i = 0; i < n; ++i)
+                    if (h[i] != ((unsigned long long)i * 0x9e3779b97f4a7c15ull ^ key)) ++wrong;
+                if (wrong) bad++;
+            }
+        }
+        if (pinned) (void)hipHostFree(h);
         (void)hipFree(d);
         (void)hipFree(dout);
         (void)hipStreamDestroy(s);
@@ -57,8 +85,9 @@ static int run(int contig, int T, int iters, long long n) {
     std::vector<std::thread> th;
     for (int t = 0; t < T; ++t) th.emplace_back(work, t);
     for (auto& x : th) x.join();
-    printf("%s: threads %d iterations %d doubles %lld: mismatches %d, errors %d\n", contig ? "contiguous" : "plain", T,
-           iters, n, bad.load(), errs.load());
+    printf("%-10s %-8s %-4s: threads %d iterations %d doubles %lld: mismatched iterations %d, errors %d\n",
+           contig ? "contiguous" : "plain", pinned ? "pinned" : "pageable", down ? "down" : "up", T, iters, n,
+           bad.load(), errs.load());
     fflush(stdout);
     return bad.load() + errs.load();
 }
@@ -68,9 +97,9 @@ int main(int argc, char** argv) {
     const int iters = argc > 2 ? atoi(argv[2]) : 50;
     const long long n = argc > 3 ? atoll(argv[3]) : 1000000;
     int r = 0;
-    for (int round = 0; round < 2; ++round) {
-        r += run(0, T, iters, n);
-        r += run(1, T, iters, n);
-    }
+    for (int round = 0; round < 2; ++round)
+        for (int down = 0; down < 2; ++down)
+            for (int pinned = 0; pinned < 2; ++pinned)
+                for (int contig = 0; contig < 2; ++contig) r += run(contig, pinned, down, T, iters, n);
     return r ? 1 : 0;
 }
