@@ -61,20 +61,28 @@ static int run(int contig, int pinned, int down, int T, int iters, long long n) 
                     hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, s) != hipSuccess ||
                     hipStreamSynchronize(s) != hipSuccess || hipMemsetAsync(dout, 0, 8, s) != hipSuccess) { errs++; break; }
                 hipLaunchKernelGGL(k_sum, dim3(512), dim3(256), 0, s, d, n, dout);
+                if (hipGetLastError() != hipSuccess) { errs++; break; }
                 if (hipMemcpyAsync(&got, dout, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
                     hipStreamSynchronize(s) != hipSuccess) { errs++; break; }
-                if (got != want) bad++;
+                if (got != want) {
+                    if (bad.fetch_add(1) < 3) printf("  up mismatch t%d it%d: got %llx want %llx\n", t, it, got, want);
+                }
             } else {
                 const unsigned long long key = seed + (unsigned long long)it * 7919ull;
                 memset(h, 0, bytes);
                 hipLaunchKernelGGL(k_fill, dim3(512), dim3(256), 0, s, d, n, key);
+                if (hipGetLastError() != hipSuccess) { errs++; break; }
                 if (hipStreamSynchronize(s) != hipSuccess ||
                     hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, s) != hipSuccess ||
                     hipStreamSynchronize(s) != hipSuccess) { errs++; break; }
-                long long wrong = 0;
+                long long wrong = 0, first = -1;
                 for (long long i = 0; i < n; ++i)
-                    if (h[i] != ((unsigned long long)i * 0x9e3779b97f4a7c15ull ^ key)) ++wrong;
-                if (wrong) bad++;
+                    if (h[i] != ((unsigned long long)i * 0x9e3779b97f4a7c15ull ^ key)) {
+                        if (first < 0) first = i;
+                        ++wrong;
+                    }
+                if (wrong && bad.fetch_add(1) < 3)
+                    printf("  down mismatch t%d it%d: %lld wrong from %lld: got %llx\n", t, it, wrong, first, h[first]);
             }
         }
         if (pinned) (void)hipHostFree(h);
