@@ -283,6 +283,8 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
     CK(hipHostMalloc((void**)&c->coop_err_h, sizeof(unsigned), hipHostMallocMapped | hipHostMallocCoherent));
     *c->coop_err_h = 0;
     CK(hipHostGetDevicePointer((void**)&c->coop_err_d, c->coop_err_h, 0));
+    CK(hipHostMalloc((void**)&c->h_xchg, sizeof(double) * LBK_WSLOT, hipHostMallocMapped | hipHostMallocCoherent));
+    CK(hipHostGetDevicePointer((void**)&c->dh_xchg, c->h_xchg, 0));
     CK(hipHostMalloc((void**)&c->sp_h, sizeof(unsigned long long) * 20, hipHostMallocMapped | hipHostMallocCoherent));
     memset(c->sp_h, 0, sizeof(unsigned long long) * 20);
     CK(hipHostGetDevicePointer((void**)&c->sp_dh, c->sp_h, 0));
@@ -555,6 +557,7 @@ void lbk_destroy(lbk_ctx* c) {
     if (c->coop_err_h) (void)hipHostFree(c->coop_err_h);
     if (c->stall_release_h && !c->rccl_hung) (void)hipHostFree(c->stall_release_h);  // else a stall may still read it
     if (c->sp_h) (void)hipHostFree(c->sp_h);
+    if (c->h_xchg) (void)hipHostFree(c->h_xchg);
     if (c->sp_vd) (void)hipFree(c->sp_vd);
     if (c->mark_ev) (void)hipEventDestroy(c->mark_ev);
     (void)hipFree(c->cnt);
@@ -1434,8 +1437,9 @@ int lbk_checksum(lbk_ctx* c, const double* x, uint64_t* c1, uint64_t* c2) {
         HIPCHK(c, hipMemcpyAsync(c->d_ckslot + 2 * c->geo.g_lo, c->d_ck, 2 * sizeof(uint64_t), hipMemcpyDeviceToDevice,
                                  c->stream));
         if (lbk_xgmi_exchange_u64(c->xg, c->stream, c->d_ckslot, 2, c->geo.g_lo, c->geo.g_hi) != 0) return -3;
-        HIPCHK(c, hipMemcpyAsync(w, c->d_ckslot, sizeof w, hipMemcpyDeviceToHost, c->stream));
+        if (kcopy(c, c->dh_xchg, (const double*)c->d_ckslot, LBK_GROUPS * 2)) return -2;
         HIPCHK(c, hipStreamSynchronize(c->stream));
+        memcpy(w, (const void*)c->h_xchg, sizeof w);
         if (lbk_xgmi_failed(c->xg)) {
             snprintf(c->err, sizeof c->err, "xgmi exchange timed out waiting for a peer");
             return -3;
@@ -1459,11 +1463,12 @@ int lbk_checksum(lbk_ctx* c, const double* x, uint64_t* c1, uint64_t* c2) {
                                     "ncclAllReduce");
         if (rrc) return rrc;
     }
-    HIPCHK(c, hipMemcpyAsync(c->h_ck, c->d_ck, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+    if (kcopy(c, c->dh_xchg, (const double*)c->d_ck, 2)) return -2;  // a kernel's stores, not a DMA
     {
         const int wrc = stream_wait(c, "trajectory checksum (ncclAllReduce)");
         if (wrc) return wrc;
     }
+    memcpy(c->h_ck, (const void*)c->h_xchg, 2 * sizeof(unsigned long long));
     *c1 = c->h_ck[0];
     *c2 = c->h_ck[1];
     if (c->grp) {  // integer sums: exact in any order
@@ -1501,18 +1506,25 @@ int lbk_fetch_groups(lbk_ctx* c, int slot, double* groups64) {
         memcpy(groups64, h, bytes);
         return 0;
     }
+    // The slot reaches its host mirror through k_slot_publish's stores (a kernel on the solver
+    // stream, behind everything queued so far), never through a copy engine: a DMA into pinned
+    // memory returned stale groups here (an emulated 4-rank vector-free solve fetched a wrong
+    // f(x0) in 3 of 4 suite runs with that copy, none since; tools/contig_probe.hip).
+    double* hd = slot < LBK_NSLOTS ? c->dh_slots + (int64_t)slot * LBK_SLOT
+                                   : c->dh_wslots + (int64_t)(slot - LBK_WSLOT0) * LBK_WSLOT;
     if (!c->comm && !c->grp) {
-        // behind everything queued so far, as a stream synchronisation would wait for, but polled
-        // on a completion word (k_slot_publish)
-        double* hd = slot < LBK_NSLOTS ? c->dh_slots + (int64_t)slot * LBK_SLOT
-                                       : c->dh_wslots + (int64_t)(slot - LBK_WSLOT0) * LBK_WSLOT;
+        // polled on the completion word (no stream synchronisation: no runtime thread spins)
         hipLaunchKernelGGL(k_slot_publish, dim3(1), dim3(256), 0, c->stream, (const double*)slot_base(c, slot), hd,
                            (int)(LBK_GROUPS * slot_stride(slot)), c->sp_dh + 2, ++c->pub_epoch);
         HIPCHK(c, hipGetLastError());
         const int rc = small_wait(c, c->pub_epoch, 2);
         if (rc) return rc;
     } else {
-        if (!c->slot_mirror[si]) HIPCHK(c, hipMemcpyAsync(h, slot_base(c, slot), bytes, hipMemcpyDeviceToHost, c->stream));
+        if (!c->slot_mirror[si]) {
+            hipLaunchKernelGGL(k_slot_publish, dim3(1), dim3(256), 0, c->stream, (const double*)slot_base(c, slot), hd,
+                               (int)(LBK_GROUPS * slot_stride(slot)), c->sp_dh + 2, ++c->pub_epoch);
+            HIPCHK(c, hipGetLastError());
+        }
         const int wrc = stream_wait(c, "result slot (ncclAllGather)");
         if (wrc) return wrc;
     }

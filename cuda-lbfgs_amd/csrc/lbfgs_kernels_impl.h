@@ -3035,6 +3035,7 @@ struct lbk_ctx {
     unsigned char slot_mirror[LBK_NSLOTS + LBK_NWSLOTS];  // last write of the slot went to the mirror
     unsigned long long* d_ck;
     unsigned long long* h_ck;
+    double *h_xchg, *dh_xchg;  // mapped pinned scratch (LBK_WSLOT doubles) for kernel-side small copies
     int64_t vec_doubles;  // allocation per vector
     ncclComm_t comm;
     // RCCL waits are bounded: the communicator's init (on a helper thread), every enqueue and a
@@ -3366,6 +3367,20 @@ int rccl_stream_wait(lbk_ctx* c, const char* what) {
     return -3;
 }
 
+// Small copies between device memory and the context's mapped pinned scratch (h_xchg) done by a
+// kernel's loads and stores, not a copy engine (the result-slot fetches likewise: k_slot_publish);
+// the caller waits on the stream before the host reads the scratch.
+__global__ __launch_bounds__(256) void k_copy_words(const double* __restrict__ src, double* __restrict__ dst, int n) {
+    for (int i = (int)threadIdx.x; i < n; i += 256) dst[i] = src[i];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+}
+int kcopy(lbk_ctx* c, double* dst, const double* src, int n) {
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(k_copy_words, dim3(1), dim3(256), 0, c->stream, src, dst, n);
+    HIPCHK(c, hipGetLastError());
+    return 0;
+}
+
 // A host wait on the solver stream. With an RCCL communicator, collectives may sit on the stream,
 // and a peer that dies mid-solve would leave a plain hipStreamSynchronize waiting forever: the wait
 // is then bounded (rccl_stream_wait, LBFGS_RCCL_TIMEOUT) and ends in LBFGS_ERR_RCCL. Without one
@@ -3406,15 +3421,15 @@ int exchange_buf(lbk_ctx* c, double* base, int ks, double* host_mirror = nullptr
         if (rc) return rc;
     }
     if (c->grp) {
+        // through the rank's mapped pinned scratch, copied by kernels on the solver stream (kcopy):
+        // this rank's groups out, the whole table back in, each waited for before the barrier
         lbk_group* G = c->grp;
-        HIPCHK(c, hipMemcpyAsync(G->table + c->geo.g_lo * ks, base + c->geo.g_lo * ks, sizeof(double) * per,
-                                 hipMemcpyDeviceToHost, c->stream));
+        if (kcopy(c, c->dh_xchg, base + c->geo.g_lo * ks, per)) return -2;
         HIPCHK(c, hipStreamSynchronize(c->stream));
+        memcpy(G->table + c->geo.g_lo * ks, (const void*)c->h_xchg, sizeof(double) * per);
         pthread_barrier_wait(&G->bar);
-        // on the solver stream, and waited for: a synchronous hipMemcpy from pageable memory may
-        // return once the bytes are staged, before they land, and it does not order this rank's
-        // next kernels (a non-blocking stream) behind it - they could read the slot's old groups
-        HIPCHK(c, hipMemcpyAsync(base, G->table, sizeof(double) * LBK_GROUPS * ks, hipMemcpyHostToDevice, c->stream));
+        memcpy(c->h_xchg, G->table, sizeof(double) * LBK_GROUPS * ks);
+        if (kcopy(c, base, c->dh_xchg, LBK_GROUPS * ks)) return -2;
         HIPCHK(c, hipStreamSynchronize(c->stream));
         pthread_barrier_wait(&G->bar);
         return 0;
