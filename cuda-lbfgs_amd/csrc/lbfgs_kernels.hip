@@ -1633,7 +1633,7 @@ int lbk_stream_probe(lbk_ctx* c, double* q, const double* const* ys, const doubl
     // launch (lbk_axpy_dot: source slot read, collect stage 2), alpha = 0 / != 0, chained through
     // two scratch slots as the passes chain theirs
     constexpr int kProbeSlot = LBK_NSLOTS - 2;  // scratch slots no solver path uses
-    if (variant >= 4) {  // the chained source slot starts at 0.0
+    if (variant == 4 || variant == 5) {  // the chained source slot starts at 0.0
         HIPCHK(c, hipMemsetAsync(c->slots + (int64_t)kProbeSlot * LBK_SLOT, 0, 2 * LBK_SLOT * sizeof(double),
                                  c->stream));
     }
@@ -1644,7 +1644,7 @@ int lbk_stream_probe(lbk_ctx* c, double* q, const double* const* ys, const doubl
         const double* y = ys[(i + 1) % npairs];
         const double* s = ss[i % npairs];
         hipError_t e = hipSuccess;
-        if (variant >= 4) {
+        if (variant == 4 || variant == 5) {
             const int src = kProbeSlot + (i & 1), dst = kProbeSlot + ((i + 1) & 1);
             const int rc = lbk_axpy_dot(c, q, q, y, s, variant == 5 ? 1e-12 : 0.0, src * LBK_KMAX, dst);
             if (rc) {
