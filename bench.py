@@ -821,7 +821,8 @@ def box_fields(probe, value, achieved_gbps, world):
             "value_per_box_tbps": round(value / (gb / 1e3), 4),
             "hbm_frac_of_box": round(achieved_gbps / gb, 4),
             "box_probe": {"kernel": "k_probe_stream (3 R + 1 W, k_axpy_dot's loads and store, no stage 2; "
-                                    "another history pair every launch, as the passes)",
+                                    "another history pair every launch, as the passes; the written vector "
+                                    "holds random data, a copy of y_0: zeros stream ~3 % faster)",
                           "avg_launch_us": round(probe["avg_launch_us"], 2), "launches": 20,
                           "bytes_per_launch": probe["bytes_per_launch"],
                           "rank0_gbps": round(probe["gbps"], 1),

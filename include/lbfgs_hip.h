@@ -258,6 +258,7 @@ int lbfgs_vector_fallbacks(const lbfgs_ctx* ctx);
 /* Diagnostic (no reference counterpart): `launches` back-to-back streams of 3 reads + 1 write
  * over a scratch work vector and the context's history vectors (y, s of the pair pool, another
  * pair every launch as the two-loop passes read them) in the passes' geometry and cache policy;
+ * the scratch vector starts as a copy of y_0 (random data: zeros stream ~3 % faster);
  * the solve's own vectors and state are untouched. *us = mean microseconds per
  * launch, *bytes = this rank's bytes per launch (32 n_loc). bench.py reports this box's rate for
  * the passes' access pattern beside the solver's. Call between lbfgs_solver_step calls of an
