@@ -152,6 +152,8 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
     if (const char* e = getenv("LBFGS_SEARCH_TIMEOUT")) c->search_timeout_s = std::max(0.0, atof(e));
     c->wait_adaptive = 1;
     if (const char* e = getenv("LBFGS_WAIT")) c->wait_adaptive = strcmp(e, "spin") != 0;
+    c->vec_plain = 0;
+    if (const char* e = getenv("LBFGS_VEC_ALLOC")) c->vec_plain = strcmp(e, "plain") == 0;
     c->rccl_timeout_s = 60.0;
     if (const char* e = getenv("LBFGS_RCCL_TIMEOUT")) c->rccl_timeout_s = std::max(0.5, atof(e));
     // test hook "stall_ms,wait_s": a device-side stall ahead of every collective and the bound of the
@@ -579,13 +581,10 @@ const char* lbk_last_error(const lbk_ctx* c) { return c ? c->err : "no context";
 // contexts in one process): 88.5-89.0 it/s against 85.4-87.1, k_axpy_dot 534-540 us against 546-551,
 // the commit 1060-1082 against 1150-1184 (plain allocations streamed at a rate that changed from
 // context to context: the probe's stream over the solver's own q ran 4 % below the same stream over
-// a vector allocated later, whatever the pair; profiles/r06/gap/). A/B: -DLBK_VEC_PLAIN=1.
-#ifndef LBK_VEC_PLAIN
-#define LBK_VEC_PLAIN 0
-#endif
+// a vector allocated later, whatever the pair; profiles/r06/gap/). A/B: LBFGS_VEC_ALLOC=plain.
 double* lbk_vec_alloc(lbk_ctx* c) {
     double* p = nullptr;
-    if (!LBK_VEC_PLAIN &&
+    if (!c->vec_plain &&
         hipExtMallocWithFlags((void**)&p, sizeof(double) * c->vec_doubles, hipDeviceMallocContiguous) != hipSuccess) {
         (void)hipGetLastError();
         p = nullptr;
