@@ -1037,7 +1037,9 @@ def main():
             "kernel_busy": prof.get("_busy"),
             "host": res.get("host"),
             "vectors": {"contiguous_fallbacks": res.get("vector_fallbacks"),
-                        "allocation": "one physically contiguous allocation per vector (hipDeviceMallocContiguous)"},
+                        "allocation": ("one physically contiguous allocation per vector (hipDeviceMallocContiguous)"
+                                       if os.environ.get("LBFGS_VEC_ALLOC") == "contiguous"
+                                       else "plain hipMalloc per vector (default)")},
             "cpu_baseline": cpu,
             "reference_parity": parity,
             "solver": {"status": res["status"], "f": res["f"], "gnorm": res["gnorm"],

@@ -152,8 +152,8 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
     if (const char* e = getenv("LBFGS_SEARCH_TIMEOUT")) c->search_timeout_s = std::max(0.0, atof(e));
     c->wait_adaptive = 1;
     if (const char* e = getenv("LBFGS_WAIT")) c->wait_adaptive = strcmp(e, "spin") != 0;
-    c->vec_plain = 0;
-    if (const char* e = getenv("LBFGS_VEC_ALLOC")) c->vec_plain = strcmp(e, "plain") == 0;
+    c->vec_plain = 1;
+    if (const char* e = getenv("LBFGS_VEC_ALLOC")) c->vec_plain = strcmp(e, "contiguous") != 0;
     c->rccl_timeout_s = 60.0;
     if (const char* e = getenv("LBFGS_RCCL_TIMEOUT")) c->rccl_timeout_s = std::max(0.5, atof(e));
     // test hook "stall_ms,wait_s": a device-side stall ahead of every collective and the bound of the
@@ -576,12 +576,16 @@ void lbk_destroy(lbk_ctx* c) {
 const lbk_geo* lbk_geometry(const lbk_ctx* c) { return &c->geo; }
 const char* lbk_last_error(const lbk_ctx* c) { return c ? c->err : "no context"; }
 
-// Every vector is one physically contiguous allocation (hipDeviceMallocContiguous) where the driver
-// can give one, else a plain hipMalloc. Measured at n = 1e8 (profiles/r06/alloc_ab/, alternating
-// contexts in one process): 88.5-89.0 it/s against 85.4-87.1, k_axpy_dot 534-540 us against 546-551,
-// the commit 1060-1082 against 1150-1184 (plain allocations streamed at a rate that changed from
-// context to context: the probe's stream over the solver's own q ran 4 % below the same stream over
-// a vector allocated later, whatever the pair; profiles/r06/gap/). A/B: LBFGS_VEC_ALLOC=plain.
+// Every vector is a plain hipMalloc. A physically contiguous allocation per vector
+// (hipDeviceMallocContiguous, LBFGS_VEC_ALLOC=contiguous) streams faster at n = 1e8
+// (profiles/r06/alloc_ab/, alternating contexts in one process: 88.5-89.0 it/s against 85.4-87.1,
+// k_axpy_dot 534-540 us against 546-551, the commit 1060-1082 against 1150-1184), but on this
+// ROCm stack it is not safe once such vectors are freed and others allocated: tools/repeat_stress.py
+// gave a wrong f(x0) / |g(x0)| in 99 of 400 emulated 4-rank solves, every one right after a context
+// of n = 300,007 had been destroyed, against 0 of 400 with plain allocations in the same call
+// (profiles/r06/alloc_reuse/). The wrong values were low by a few hundred segment partials, as if
+// those partials had been overwritten with zeros by the new contexts' copy-engine work (their
+// vectors' zero fill or x0's upload) - the mode stays opt-in for runs that allocate once.
 double* lbk_vec_alloc(lbk_ctx* c) {
     double* p = nullptr;
     if (!c->vec_plain &&

@@ -3129,7 +3129,7 @@ struct lbk_ctx {
     // host waits on the completion words (small_wait): spin-then-sleep, the last four waits' durations
     // per word, and the time slept / waits completed (lbfgs_wait_stats)
     int vec_plain_fallbacks;  // vectors the driver could not give contiguous (lbk_vec_alloc)
-    int vec_plain;            // LBFGS_VEC_ALLOC=plain: plain hipMalloc for every vector
+    int vec_plain;            // plain hipMalloc for every vector (LBFGS_VEC_ALLOC=contiguous: 0)
     int wait_adaptive;
     double wait_hist[4][4];
     unsigned wait_pos[4];

@@ -392,7 +392,7 @@ class Context:
 
     @property
     def vector_fallbacks(self):
-        """vectors allocated without the physically contiguous flag (lbfgs_vector_fallbacks)"""
+        """vectors that asked for a physically contiguous allocation (LBFGS_VEC_ALLOC=contiguous) and got a plain one"""
         return int(lib().lbfgs_vector_fallbacks(self.h))
 
     def wait_stats(self):

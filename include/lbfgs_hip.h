@@ -251,9 +251,10 @@ int lbfgs_coop_info(const lbfgs_ctx* ctx, int* coop_max, int* search_max, int* f
  * it and spins for the rest; LBFGS_WAIT=spin: spin throughout. *slept_s = seconds slept so far,
  * *waits = waits completed, *adaptive = the mode. */
 int lbfgs_wait_stats(const lbfgs_ctx* ctx, double* slept_s, uint64_t* waits, int* adaptive);
-/* Every n-vector is one physically contiguous device allocation where the driver grants one
- * (+3 % at n = 1e8); this returns how many of the context's allocations fell back to
- * a plain hipMalloc. */
+/* Every n-vector is a plain hipMalloc; with LBFGS_VEC_ALLOC=contiguous at context creation each is
+ * one physically contiguous device allocation where the driver grants one (+3 % at n = 1e8, not safe
+ * on this ROCm stack once vectors are freed and re-allocated). Returns how many of the
+ * context's allocations asked for a contiguous one and fell back to a plain hipMalloc. */
 int lbfgs_vector_fallbacks(const lbfgs_ctx* ctx);
 /* Diagnostic (no reference counterpart): `launches` back-to-back streams of 3 reads + 1 write
  * over a scratch work vector and the context's history vectors (y, s of the pair pool, another

@@ -1,0 +1,58 @@
+"""Contexts created after others were destroyed give the same bits (round 6).
+
+With one physically contiguous allocation per vector (now opt-in, LBFGS_VEC_ALLOC=contiguous),
+tools/repeat_stress.py found the emulated 4-rank vector-free solve's f(x0) / |g(x0)| wrong right
+after a context of n = 300,007 had been solved and destroyed (99 of 400 repetitions), and never
+with plain allocations (profiles/r06/alloc_reuse/). This runs that sequence with the
+shipped allocation: a small context solved and destroyed, then four emulated ranks, each of their
+trajectories bit-identical to the one-rank run, four times over.
+"""
+import os
+import sys
+import threading
+
+import numpy as np
+import pytest
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "cuda-lbfgs_amd"))
+import lbfgs_amd as L  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+def bits(a):
+    return np.asarray(a, dtype=np.float64).view(np.uint64)
+
+
+def test_vectors_freed_then_reallocated_give_the_same_bits(monkeypatch):
+    monkeypatch.setenv("LBFGS_TICKET", "0")
+    n, m, iters = 4_000_003, 5, 12
+    x0 = L.x0_uniform(n, 42, -2.0, 2.0)
+    with L.Context(n, m) as c:
+        ref = c.minimize("rosenbrock", x0, "backtracking", iters, trace=True, vector_free=True)
+    for rep in range(4):
+        nc = 300_007
+        with L.Context(nc, 5) as c:
+            c.minimize("rosenbrock", L.x0_uniform(nc, rep, -2.0, 2.0), "wolfe", 5, trace=True)
+        grp = L.HostGroup(4)
+        ctxs = [L.Context(n, m, rank=r, group=grp) for r in range(4)]
+        out, err = [None] * 4, [None] * 4
+
+        def run(r):
+            try:
+                out[r] = ctxs[r].minimize("rosenbrock", x0, "backtracking", iters, trace=True, vector_free=True)
+            except Exception as e:  # pragma: no cover
+                err[r] = e
+
+        th = [threading.Thread(target=run, args=(r,)) for r in range(4)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=300)
+        for c in ctxs:
+            c.close()
+        grp.close()
+        assert not any(err), err
+        for r in range(4):
+            for key in ("tr_f", "tr_gnorm", "tr_alpha"):
+                assert np.array_equal(bits(out[r][key]), bits(ref[key])), (rep, r, key)

@@ -9,7 +9,7 @@
 #   bash tools/gpu_r06.sh config4deep  configs[4]'s canonical oracle run at n = 1e9 on the box's host
 #   bash tools/gpu_r06.sh cleantrace   kernel trace of the bench steps without any HIP events
 #   bash tools/gpu_r06.sh gappmc     SQ / TA counter passes over the gap probe (one pass per run)
-#   bash tools/gpu_r06.sh stress R  tools/repeat_stress.py R reps, contiguous vectors then plain ones
+#   bash tools/gpu_r06.sh stress R  tools/repeat_stress.py R reps, the default (plain) vectors then contiguous ones
 #   bash tools/gpu_r06.sh vflane     tools/vflaneprobe: the vector-free stream shape, one element per lane vs two
 #   bash tools/gpu_r06.sh tests ARGS pytest -m gpu over ARGS (default: tests)
 #   bash tools/gpu_r06.sh bench ARGS one bench.py line -> gpurun_out/r06/bench.json
@@ -111,13 +111,13 @@ for n in ('1e8', '1e4'):
         gap_pmc d WRITE_SIZE &&
         gap_pmc e TA_BUSY_avr TA_BUSY_max &&
         python tools/gap_pmc_summary.py $O/gap_pmc_summary.json $O/gap_pmc_? > $O/gap_pmc_summary.txt ;;
-    stress)
+    stress)  # the shipped (plain) allocation first, then LBFGS_VEC_ALLOC=contiguous
         R=${2:-20}
-        timeout -k 10 500 python -u tools/repeat_stress.py $O/stress_contig.json $R > $O/stress_contig.log 2>&1
-        rc=$?; echo "stress contiguous rc=$rc"; tail -2 $O/stress_contig.log; [ $rc -eq 0 ] || exit $rc
-        LBFGS_VEC_ALLOC=plain timeout -k 10 500 python -u tools/repeat_stress.py $O/stress_plain.json $R \
-            > $O/stress_plain.log 2>&1
-        rc=$?; echo "stress plain rc=$rc"; tail -2 $O/stress_plain.log; exit $rc ;;
+        timeout -k 10 500 python -u tools/repeat_stress.py $O/stress_default.json $R > $O/stress_default.log 2>&1
+        rc=$?; echo "stress default rc=$rc"; tail -2 $O/stress_default.log; [ $rc -eq 0 ] || exit $rc
+        LBFGS_VEC_ALLOC=contiguous timeout -k 10 500 python -u tools/repeat_stress.py $O/stress_contig.json $R \
+            > $O/stress_contig.log 2>&1
+        rc=$?; echo "stress contiguous rc=$rc"; tail -2 $O/stress_contig.log; exit $rc ;;
     vflane)
         timeout -k 10 300 tools/vflaneprobe 1e8 9 > $O/vflaneprobe.txt 2>&1
         rc=$?; echo "vflane rc=$rc"; cat $O/vflaneprobe.txt; exit $rc ;;
