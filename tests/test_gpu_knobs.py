@@ -30,7 +30,7 @@ pytestmark = pytest.mark.gpu
 # LBK_PERSIST_ALT, LBK_PERSIST_LDS; the q/r ping-pong was removed).
 KNOBS = ["LBFGS_TICKET", "LBFGS_DEFER", "LBFGS_REV", "LBFGS_NT", "LBFGS_DIRECT", "LBFGS_COOP",
          "LBFGS_PERSIST", "LBFGS_SPEC", "LBFGS_BATCH", "LBFGS_PERSIST_WG", "LBFGS_COLLECT",
-         "LBFGS_COLLECT_TIMEOUT", "LBFGS_DEV_SEARCH", "LBFGS_DEV_WOLFE", "LBFGS_SEARCH_TIMEOUT"]
+         "LBFGS_COLLECT_TIMEOUT", "LBFGS_DEV_SEARCH", "LBFGS_DEV_WOLFE", "LBFGS_SEARCH_TIMEOUT", "LBFGS_WAIT"]
 
 VARIANTS = {
     "ticket1": {"LBFGS_TICKET": "1"},
@@ -61,6 +61,7 @@ VARIANTS = {
     "devsearch0_spec0": {"LBFGS_DEV_SEARCH": "0", "LBFGS_SPEC": "0"},
     "devwolfe0_round4_name": {"LBFGS_DEV_WOLFE": "0"},
     "search_timeout0": {"LBFGS_SEARCH_TIMEOUT": "0"},  # the device search gives up, the host loop redoes it
+    "wait_spin": {"LBFGS_WAIT": "spin"},  # host waits spin throughout (no sleep phase)
 }
 
 CASES = [  # n, m, objective, line search, iterations
