@@ -71,6 +71,12 @@ def test_search_barrier_timeout_falls_back_bit_identical(monkeypatch, n, m, obj,
     assert dev["coop"]["fallbacks"] == 0
     same(forced, host)
     same(dev, host)
+    # the counters: the timed-out launch counts no trial pass and the host loop redoes the search
+    # from the same state, so the trial passes are the host loop's; the redo commits again even at
+    # the first trial's step (recommit_a0), at most once per solve since the device form then stays off
+    for k in ("trials_f", "trials_fg"):
+        assert forced[k] == host[k], (k, forced[k], host[k])
+    assert host["commits"] <= forced["commits"] <= host["commits"] + 1, (forced["commits"], host["commits"])
     o = O.lbfgs(obj, x0, ls, m, iters, 1e-5, mode=O.CANON)
     assert np.array_equal(bits(forced["tr_f"]), bits(o["f"])) and np.array_equal(bits(forced["x"]), bits(o["x"]))
 
