@@ -501,6 +501,7 @@ def _measure(a, D, ctx, x0, rank, world, uid, unfused, vector_free, box_probe, d
                     "waits": w1["waits"] - w0["waits"], "wait_mode": "adaptive" if w1["adaptive"] else "spin"}
                    if w0 and w1 else None)
     res["vector_fallbacks"] = run(lambda: ctx.vector_fallbacks)
+    res["vector_pool"] = run(lambda: ctx.vector_pool)
     res["history_fill"] = fill["iterations"]
     res["warm_counters"] = {k: warm[k] for k in ("trials_f", "trials_fg", "commits", "passes")} if warm else None
     res["box_probe"] = probe
@@ -853,6 +854,18 @@ def roofline(prof, n, world):
                 kernel_rates=rates)
 
 
+def vectors_info(res):
+    """how the timed context's vectors were allocated (LBFGS_VEC_ALLOC)"""
+    vp = res.get("vector_pool")
+    mode, pooled, held = vp if isinstance(vp, (tuple, list)) else (None, None, None)
+    what = {"pool": "physically contiguous vectors (hipDeviceMallocContiguous) from a process-wide pool that "
+                    "never returns them to the driver (64 MiB .. 8 GiB vectors; others plain hipMalloc)",
+            "plain": "plain hipMalloc per vector",
+            "contiguous": "physically contiguous per vector, freed with hipFree (A/B only)"}.get(mode)
+    return {"mode": mode, "allocation": what, "pooled_vectors": pooled, "pool_gib": round(held, 2) if held else held,
+            "contiguous_fallbacks": res.get("vector_fallbacks")}
+
+
 def main():
     a = parse()
     if a.gpus > 1 and "RANK" not in os.environ:
@@ -1036,10 +1049,7 @@ def main():
             "exchange_fallback": fallback,
             "kernel_busy": prof.get("_busy"),
             "host": res.get("host"),
-            "vectors": {"contiguous_fallbacks": res.get("vector_fallbacks"),
-                        "allocation": ("one physically contiguous allocation per vector (hipDeviceMallocContiguous)"
-                                       if os.environ.get("LBFGS_VEC_ALLOC") == "contiguous"
-                                       else "plain hipMalloc per vector (default)")},
+            "vectors": vectors_info(res),
             "cpu_baseline": cpu,
             "reference_parity": parity,
             "solver": {"status": res["status"], "f": res["f"], "gnorm": res["gnorm"],

@@ -142,6 +142,9 @@ int lbk_coop_info(const lbk_ctx* c, int* coop_max, int* search_max, int* fallbac
 int lbk_wait_stats(const lbk_ctx* c, double* slept_s, unsigned long long* waits, int* adaptive);
 /* vectors allocated with a plain hipMalloc because a physically contiguous one was refused */
 int lbk_vec_fallbacks(const lbk_ctx* c);
+/* the context's allocation mode (0 pool, 1 plain, 2 contiguous), its vectors taken from or added
+ * to the process-wide contiguous pool, and the GiB the pool owns */
+int lbk_vec_pool_stats(const lbk_ctx* c, int* pooled, double* held_gb);
 /* box probe: `launches` back-to-back 3 R + 1 W streams over (q, y, s) in the two-loop passes'
  * geometry and cache policy, q written back unchanged; launch i reads the pair pool's
  * y[(i + 1) % npairs] and s[i % npairs] (another pair every launch, as the passes: only q's tail

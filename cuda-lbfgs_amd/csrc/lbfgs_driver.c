@@ -478,6 +478,10 @@ int lbfgs_cu_partition(const lbfgs_ctx* c) { return c ? lbk_cu_partition(c->dev)
 
 int lbfgs_vector_fallbacks(const lbfgs_ctx* c) { return c ? lbk_vec_fallbacks(c->dev) : LBFGS_ERR_BAD_ARG; }
 
+int lbfgs_vector_pool(const lbfgs_ctx* c, int* pooled, double* held_gb) {
+    return c ? lbk_vec_pool_stats(c->dev, pooled, held_gb) : LBFGS_ERR_BAD_ARG;
+}
+
 int lbfgs_wait_stats(const lbfgs_ctx* c, double* slept_s, uint64_t* waits, int* adaptive) {
     if (!c) return LBFGS_ERR_BAD_ARG;
     unsigned long long w = 0;

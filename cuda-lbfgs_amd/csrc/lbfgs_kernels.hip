@@ -3,6 +3,8 @@
 #include "lbfgs_kernels_impl.h"
 
 #include <atomic>
+#include <mutex>
+#include <unordered_set>
 #include <thread>
 
 // A slot the host reads whose launch leaves no completion word (stage 2 in several groups, the
@@ -152,8 +154,13 @@ int lbk_create(lbk_ctx** out, int device, int64_t n, int rank, int world, const 
     if (const char* e = getenv("LBFGS_SEARCH_TIMEOUT")) c->search_timeout_s = std::max(0.0, atof(e));
     c->wait_adaptive = 1;
     if (const char* e = getenv("LBFGS_WAIT")) c->wait_adaptive = strcmp(e, "spin") != 0;
-    c->vec_plain = 1;
-    if (const char* e = getenv("LBFGS_VEC_ALLOC")) c->vec_plain = strcmp(e, "contiguous") != 0;
+    c->vec_mode = LBK_VEC_POOL;
+    if (const char* e = getenv("LBFGS_VEC_ALLOC"))
+        c->vec_mode = !strcmp(e, "plain") ? LBK_VEC_PLAIN : !strcmp(e, "contiguous") ? LBK_VEC_CONTIGUOUS : LBK_VEC_POOL;
+    c->vec_pool_cap = size_t(32) << 30;
+    if (const char* e = getenv("LBFGS_VEC_POOL_GB")) c->vec_pool_cap = (size_t)(std::max(0.0, atof(e)) * double(size_t(1) << 30));
+    c->vec_pool_min = kPoolMinBytes;
+    if (const char* e = getenv("LBFGS_VEC_POOL_MIN_MB")) c->vec_pool_min = (size_t)(std::max(0.0, atof(e)) * double(1 << 20));
     c->rccl_timeout_s = 60.0;
     if (const char* e = getenv("LBFGS_RCCL_TIMEOUT")) c->rccl_timeout_s = std::max(0.5, atof(e));
     // test hook "stall_ms,wait_s": a device-side stall ahead of every collective and the bound of the
@@ -576,38 +583,103 @@ void lbk_destroy(lbk_ctx* c) {
 const lbk_geo* lbk_geometry(const lbk_ctx* c) { return &c->geo; }
 const char* lbk_last_error(const lbk_ctx* c) { return c ? c->err : "no context"; }
 
-// Every vector is a plain hipMalloc. A physically contiguous allocation per vector
-// (hipDeviceMallocContiguous, LBFGS_VEC_ALLOC=contiguous) streams faster at n = 1e8
-// (profiles/r06/alloc_ab/, alternating contexts in one process: 88.5-89.0 it/s against 85.4-87.1,
-// k_axpy_dot 534-540 us against 546-551, the commit 1060-1082 against 1150-1184), but on this
-// ROCm stack it is not safe once such vectors are freed and others allocated: tools/repeat_stress.py
-// gave a wrong f(x0) / |g(x0)| in 99 of 400 emulated 4-rank solves, every one right after a context
-// of n = 300,007 had been destroyed, against 0 of 400 with plain allocations in the same call
-// (profiles/r06/alloc_reuse/). The wrong values were low by a few hundred segment partials, as if
-// those partials had been overwritten with zeros by the new contexts' copy-engine work (their
-// vectors' zero fill or x0's upload) - the mode stays opt-in for runs that allocate once.
+// Vector allocation (LBFGS_VEC_ALLOC, read at context creation):
+//   pool (default)  vectors of 64 MiB .. 8 GiB are physically contiguous allocations
+//                   (hipDeviceMallocContiguous) that are never returned to the driver: a freed one
+//                   goes to a process-wide pool and the next vector of the same size and device takes
+//                   it (at most LBFGS_VEC_POOL_GB = 32 GiB held per process, then plain); other
+//                   sizes are plain hipMalloc
+//   plain           every vector a plain hipMalloc
+//   contiguous      every vector contiguous, freed with hipFree (A/B only: not safe, below)
+// Contiguous vectors stream faster at n = 1e8 (profiles/r06/alloc_ab/, alternating contexts in one
+// process: 88.5-89.0 it/s against 85.4-87.1, k_axpy_dot 534-540 us against 546-551, the commit
+// 1060-1082 against 1150-1184): a plain allocation's rate depends on the physical pages it gets.
+// But on this ROCm stack freeing a contiguous allocation corrupts the process's next allocations:
+// tools/repeat_stress.py (profiles/r06/alloc_reuse/) found wrong results in the first solve of
+// contexts created after contiguous vectors had been freed - 131 of 200 when only the destroyed
+// contexts' vectors were contiguous, 50 of 200 the other way round (the freed ones contiguous, the
+// failing new ones plain), 0 of 400 with plain allocations throughout. The pool never frees one.
+namespace {
+struct VecPool {
+    std::mutex mu;
+    std::vector<std::pair<std::pair<int, size_t>, void*>> idle;  // ((device, bytes), base)
+    std::unordered_set<void*> mine;                                // every base the pool owns
+    size_t held = 0;                                              // bytes owned (idle + in use)
+};
+VecPool& vec_pool() {
+    static VecPool* p = new VecPool();  // never destroyed: its memory is never given back
+    return *p;
+}
+constexpr size_t kPoolMax = size_t(8) << 30;
+}  // namespace
+
 double* lbk_vec_alloc(lbk_ctx* c) {
+    const size_t bytes = sizeof(double) * (size_t)c->vec_doubles;
     double* p = nullptr;
-    if (!c->vec_plain &&
-        hipExtMallocWithFlags((void**)&p, sizeof(double) * c->vec_doubles, hipDeviceMallocContiguous) != hipSuccess) {
-        (void)hipGetLastError();
-        p = nullptr;
-        c->vec_plain_fallbacks++;
+    if (c->vec_mode == LBK_VEC_POOL && bytes >= c->vec_pool_min && bytes <= kPoolMax) {
+        VecPool& P = vec_pool();
+        std::lock_guard<std::mutex> lk(P.mu);
+        for (size_t i = 0; i < P.idle.size(); ++i)
+            if (P.idle[i].first == std::make_pair(c->device, bytes)) {
+                p = static_cast<double*>(P.idle[i].second);
+                P.idle[i] = P.idle.back();
+                P.idle.pop_back();
+                c->vec_pooled++;
+                break;
+            }
+        if (!p && P.held + bytes <= c->vec_pool_cap) {
+            if (hipExtMallocWithFlags((void**)&p, bytes, hipDeviceMallocContiguous) == hipSuccess) {
+                P.mine.insert(p);
+                P.held += bytes;
+                c->vec_pooled++;
+            } else {
+                (void)hipGetLastError();
+                p = nullptr;
+                c->vec_plain_fallbacks++;
+            }
+        }
+    } else if (c->vec_mode == LBK_VEC_CONTIGUOUS) {
+        if (hipExtMallocWithFlags((void**)&p, bytes, hipDeviceMallocContiguous) != hipSuccess) {
+            (void)hipGetLastError();
+            p = nullptr;
+            c->vec_plain_fallbacks++;
+        }
     }
-    if (!p && hipMalloc(&p, sizeof(double) * c->vec_doubles) != hipSuccess) {
+    if (!p && hipMalloc(&p, bytes) != hipSuccess) {
         snprintf(c->err, sizeof c->err, "hipMalloc of %lld doubles failed", (long long)c->vec_doubles);
         return nullptr;
     }
-    if (hipMemsetAsync(p, 0, sizeof(double) * c->vec_doubles, c->stream) != hipSuccess) {
-        (void)hipFree(p);
+    if (hipMemsetAsync(p, 0, bytes, c->stream) != hipSuccess) {
+        lbk_vec_free(c, p + LBK_FRONT);
         return nullptr;
     }
     return p + LBK_FRONT;
 }
 
 void lbk_vec_free(lbk_ctx* c, double* v) {
-    (void)c;
-    if (v) (void)hipFree(v - LBK_FRONT);
+    if (!v) return;
+    void* base = v - LBK_FRONT;
+    VecPool& P = vec_pool();
+    {
+        std::lock_guard<std::mutex> lk(P.mu);
+        if (!P.mine.count(base)) {
+            (void)hipFree(base);  // (synchronises the device: no kernel of this context still uses it)
+            return;
+        }
+    }
+    // a pooled vector: the context's queued work on it finishes before another context can take it
+    // (a stream that may hold a hung RCCL collective keeps it: it stays owned and idle forever)
+    if (c->rccl_hung || hipStreamSynchronize(c->stream) != hipSuccess) return;
+    std::lock_guard<std::mutex> lk(P.mu);
+    P.idle.push_back({{c->device, sizeof(double) * (size_t)c->vec_doubles}, base});
+}
+
+int lbk_vec_pool_stats(const lbk_ctx* c, int* pooled, double* held_gb) {
+    VecPool& P = vec_pool();
+    std::lock_guard<std::mutex> lk(P.mu);
+    if (pooled) *pooled = c ? c->vec_pooled : 0;
+    if (held_gb) *held_gb = (double)P.held / double(size_t(1) << 30);
+    return c ? c->vec_mode : -1;
 }
 
 void* lbk_host_alloc(size_t bytes) {

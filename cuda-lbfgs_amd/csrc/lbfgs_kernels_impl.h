@@ -3017,6 +3017,10 @@ struct lbk_group {
     unsigned long long ck[LBK_GROUPS][2];
 };
 
+// vector allocation modes (lbk_vec_alloc, LBFGS_VEC_ALLOC)
+enum { LBK_VEC_POOL = 0, LBK_VEC_PLAIN = 1, LBK_VEC_CONTIGUOUS = 2 };
+constexpr size_t kPoolMinBytes = size_t(64) << 20;
+
 struct lbk_ctx {
     lbk_geo geo;
     int device;
@@ -3129,7 +3133,10 @@ struct lbk_ctx {
     // host waits on the completion words (small_wait): spin-then-sleep, the last four waits' durations
     // per word, and the time slept / waits completed (lbfgs_wait_stats)
     int vec_plain_fallbacks;  // vectors the driver could not give contiguous (lbk_vec_alloc)
-    int vec_plain;            // plain hipMalloc for every vector (LBFGS_VEC_ALLOC=contiguous: 0)
+    int vec_mode;             // LBK_VEC_POOL (default) / _PLAIN / _CONTIGUOUS (LBFGS_VEC_ALLOC; lbk_vec_alloc)
+    int vec_pooled;           // this context's vectors taken from / added to the contiguous pool
+    size_t vec_pool_cap;      // bytes the process-wide pool may own (LBFGS_VEC_POOL_GB, 32 GiB)
+    size_t vec_pool_min;      // smallest pooled vector (LBFGS_VEC_POOL_MIN_MB, 64 MiB)
     int wait_adaptive;
     double wait_hist[4][4];
     unsigned wait_pos[4];

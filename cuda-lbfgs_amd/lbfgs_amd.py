@@ -125,6 +125,7 @@ def lib():
     L.lbfgs_coop_info.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]
     L.lbfgs_wait_stats.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_uint64), C.POINTER(C.c_int)]
     L.lbfgs_vector_fallbacks.argtypes = [vp]
+    L.lbfgs_vector_pool.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_double)]
     L.lbfgs_stream_probe.argtypes = [vp, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double)]
     L.lbfgs_stream_probe_variant.argtypes = [vp, C.c_int, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double)]
     L.lbfgs_stream_probe_vectors.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_double)]
@@ -150,7 +151,7 @@ EXPORTED_SYMBOLS = [
     "lbfgs_dev_twoloop", "lbfgs_dev_elementwise", "lbfgs_line_search", "lbfgs_prof_enable",
     "lbfgs_prof_reset", "lbfgs_prof_get", "lbfgs_peer_handle", "lbfgs_peer_connect", "lbfgs_peer_enable", "lbfgs_rccl_attach",
     "lbfgs_exchange_backend", "lbfgs_exchange_fold", "lbfgs_exchange_latency", "lbfgs_device_count", "lbfgs_set_dense_quadratic", "lbfgs_build_info",
-    "lbfgs_spec_stats", "lbfgs_cu_partition", "lbfgs_stream_probe", "lbfgs_stream_probe_variant", "lbfgs_stream_probe_vectors", "lbfgs_vector_address", "lbfgs_coop_info", "lbfgs_wait_stats", "lbfgs_vector_fallbacks", "lbfgs_search_stats",
+    "lbfgs_spec_stats", "lbfgs_cu_partition", "lbfgs_stream_probe", "lbfgs_stream_probe_variant", "lbfgs_stream_probe_vectors", "lbfgs_vector_address", "lbfgs_coop_info", "lbfgs_wait_stats", "lbfgs_vector_fallbacks", "lbfgs_vector_pool", "lbfgs_search_stats",
 ]
 PEER_HANDLE_BYTES = 64
 BACKENDS = {0: "single", 1: "rccl", 2: "xgmi", 3: "host-group"}
@@ -389,6 +390,14 @@ class Context:
         if lib().lbfgs_vector_address(self.h, int(k), C.byref(a)) != 0:
             return None
         return a.value
+
+    @property
+    def vector_pool(self):
+        """(mode, vectors of this context taken from / added to the contiguous pool, GiB the process's
+        pool owns); mode 'pool' (default), 'plain' or 'contiguous' (lbfgs_vector_pool)"""
+        n, gb = C.c_int(), C.c_double()
+        mode = int(lib().lbfgs_vector_pool(self.h, C.byref(n), C.byref(gb)))
+        return {0: "pool", 1: "plain", 2: "contiguous"}.get(mode, mode), n.value, gb.value
 
     @property
     def vector_fallbacks(self):

@@ -251,11 +251,17 @@ int lbfgs_coop_info(const lbfgs_ctx* ctx, int* coop_max, int* search_max, int* f
  * it and spins for the rest; LBFGS_WAIT=spin: spin throughout. *slept_s = seconds slept so far,
  * *waits = waits completed, *adaptive = the mode. */
 int lbfgs_wait_stats(const lbfgs_ctx* ctx, double* slept_s, uint64_t* waits, int* adaptive);
-/* Every n-vector is a plain hipMalloc; with LBFGS_VEC_ALLOC=contiguous at context creation each is
- * one physically contiguous device allocation where the driver grants one (+3 % at n = 1e8, not safe
- * on this ROCm stack once vectors are freed and re-allocated). Returns how many of the
- * context's allocations asked for a contiguous one and fell back to a plain hipMalloc. */
+/* Vector allocation (LBFGS_VEC_ALLOC at context creation): by default ("pool") every
+ * n-vector of 64 MiB .. 8 GiB is a physically contiguous device allocation (+3 % at n = 1e8) that is
+ * never returned to the driver - a freed one waits in a process-wide pool (at most LBFGS_VEC_POOL_GB,
+ * 32 GiB) for the next vector of its size - because freeing contiguous allocations corrupts later
+ * ones on this ROCm stack; other sizes, "plain", and the pool's overflow are plain hipMalloc;
+ * "contiguous" (A/B only) frees them. Returns how many of the context's vectors asked for a
+ * contiguous allocation and got a plain one. */
 int lbfgs_vector_fallbacks(const lbfgs_ctx* ctx);
+/* The context's allocation mode (0 pool, 1 plain, 2 contiguous) or LBFGS_ERR_BAD_ARG; *pooled = its
+ * vectors taken from or added to the pool, *held_gb = GiB the process's pool owns. */
+int lbfgs_vector_pool(const lbfgs_ctx* ctx, int* pooled, double* held_gb);
 /* Diagnostic (no reference counterpart): `launches` back-to-back streams of 3 reads + 1 write
  * over a scratch work vector and the context's history vectors (y, s of the pair pool, another
  * pair every launch as the two-loop passes read them) in the passes' geometry and cache policy;

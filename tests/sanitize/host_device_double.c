@@ -158,6 +158,12 @@ int lbk_vec_fallbacks(const lbk_ctx* c) {
     (void)c;
     return 0;
 }
+int lbk_vec_pool_stats(const lbk_ctx* c, int* pooled, double* held_gb) {
+    (void)c;
+    if (pooled) *pooled = 0;
+    if (held_gb) *held_gb = 0.0;
+    return 1; /* host memory: plain */
+}
 int lbk_wait_stats(const lbk_ctx* c, double* s, unsigned long long* w, int* a) {
     (void)c;
     if (s) *s = 0.0;

@@ -61,6 +61,7 @@ class StubContext:
         return dict(slept_s=0.0, waits=0, adaptive=True)
 
     vector_fallbacks = 0
+    vector_pool = ("pool", 0, 0.0)
 
     def prof_reset(self):
         pass

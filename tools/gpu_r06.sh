@@ -118,6 +118,27 @@ for n in ('1e8', '1e4'):
         LBFGS_VEC_ALLOC=contiguous timeout -k 10 500 python -u tools/repeat_stress.py $O/stress_contig.json $R \
             > $O/stress_contig.log 2>&1
         rc=$?; echo "stress contiguous rc=$rc"; tail -2 $O/stress_contig.log; exit $rc ;;
+    stressab)  # which side's contiguous allocations matter: the destroyed contexts' or the new ones'
+        R=${2:-100}
+        for modes in contiguous,contiguous contiguous,plain plain,contiguous; do
+            timeout -k 10 300 python -u tools/repeat_stress.py $O/stress_$modes.json $R churn,vf4 $modes \
+                > $O/stress_$modes.log 2>&1
+            rc=$?; echo "stress $modes rc=$rc"; tail -1 $O/stress_$modes.log; [ $rc -eq 0 ] || exit $rc
+        done ;;
+    pool)  # the contiguous pool: stress with every vector pooled, then pool against plain at n = 1e8
+        LBFGS_VEC_POOL_MIN_MB=0 timeout -k 10 400 python -u tools/repeat_stress.py $O/stress_pool_all.json 300 \
+            > $O/stress_pool_all.log 2>&1
+        rc=$?; echo "stress pool rc=$rc"; tail -1 $O/stress_pool_all.log; [ $rc -eq 0 ] || exit $rc
+        for r in 1 2; do
+            for v in pool plain; do
+                LBFGS_VEC_ALLOC=$v timeout -k 10 300 python bench.py --steps 100 --warmup 20 --no-cpu-baseline \
+                    --no-vector-free --no-persistent > $O/poolab_${v}_$r.json 2> $O/poolab_${v}_$r.err || exit 1
+                python -c "
+import json
+d = json.load(open('$O/poolab_${v}_$r.json'))
+print('$v', '$r', d['value'], d['roofline']['avg_launch_us'], d['box_copy_tbps'], d['vectors'])" | tee -a $O/poolab.txt
+            done
+        done ;;
     vflane)
         timeout -k 10 300 tools/vflaneprobe 1e8 9 > $O/vflaneprobe.txt 2>&1
         rc=$?; echo "vflane rc=$rc"; cat $O/vflaneprobe.txt; exit $rc ;;

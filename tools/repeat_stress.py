@@ -13,7 +13,9 @@ Kinds, interleaved every repetition:
           one-rank vector-free run
 The environment (LBFGS_VEC_ALLOC=plain, ...) selects the library's mode; no oracle is used.
 
-usage: python tools/repeat_stress.py out.json [reps] [kinds]
+usage: python tools/repeat_stress.py out.json [reps] [kinds] [churn_alloc,vf_alloc]
+  (the last argument sets LBFGS_VEC_ALLOC for the churn contexts and for the 4-rank contexts
+  separately, e.g. "contiguous,plain": which side's allocations matter)
 """
 import json
 import os
@@ -46,8 +48,18 @@ def same(a, b):
     return bad, first
 
 
-def vf4(x0, ref, n, m, iters):
+def alloc_env(mode):
+    if mode is None:
+        return
+    if mode == "default":
+        os.environ.pop("LBFGS_VEC_ALLOC", None)
+    else:
+        os.environ["LBFGS_VEC_ALLOC"] = mode
+
+
+def vf4(x0, ref, n, m, iters, mode=None):
     grp = L.HostGroup(4)
+    alloc_env(mode)
     ctxs = [L.Context(n, m, rank=r, group=grp) for r in range(4)]
     out, err = [None] * 4, [None] * 4
 
@@ -79,8 +91,9 @@ def main():
     out_path = sys.argv[1]
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
     kinds = sys.argv[3].split(",") if len(sys.argv) > 3 else ["small", "churn", "vf4"]
+    modes = sys.argv[4].split(",") if len(sys.argv) > 4 else [None, None]
     env = {k: v for k, v in os.environ.items() if k.startswith("LBFGS_")}
-    res = {"env": env, "reps": reps, "kinds": kinds, "fail": {k: 0 for k in kinds}, "runs": {k: 0 for k in kinds},
+    res = {"env": env, "reps": reps, "kinds": kinds, "alloc_modes": modes, "fail": {k: 0 for k in kinds}, "runs": {k: 0 for k in kinds},
            "failures": [], "build": L.build_info()[0]}
     t0 = time.time()
     n_s, m_s = 4097, 7
@@ -106,6 +119,7 @@ def main():
         if "churn" in kinds:
             n = sizes[rep % len(sizes)]
             x = L.x0_uniform(n, rep, -2.0, 2.0)
+            alloc_env(modes[0])
             with L.Context(n, 5) as c:
                 a = c.minimize("rosenbrock", x, "wolfe", 5, trace=True)
                 b2 = c.minimize("rosenbrock", x, "wolfe", 5, trace=True)
@@ -115,7 +129,7 @@ def main():
                 res["fail"]["churn"] += 1
                 res["failures"].append({"rep": rep, "kind": "churn", "n": n, "keys": b, "first": first})
         if "vf4" in kinds:
-            bad = vf4(x_v, ref_v, n_v, m_v, it_v)
+            bad = vf4(x_v, ref_v, n_v, m_v, it_v, modes[1])
             res["runs"]["vf4"] += 1
             if bad:
                 res["fail"]["vf4"] += 1
