@@ -859,7 +859,7 @@ def vectors_info(res):
     vp = res.get("vector_pool")
     mode, pooled, held = vp if isinstance(vp, (tuple, list)) else (None, None, None)
     what = {"pool": "physically contiguous vectors (hipDeviceMallocContiguous) from a process-wide pool that "
-                    "never returns them to the driver (64 MiB .. 8 GiB vectors; others plain hipMalloc)",
+                    "never returns them to the driver (64 MiB .. 2 GiB vectors; others plain hipMalloc)",
             "plain": "plain hipMalloc per vector",
             "contiguous": "physically contiguous per vector, freed with hipFree (A/B only)"}.get(mode)
     return {"mode": mode, "allocation": what, "pooled_vectors": pooled, "pool_gib": round(held, 2) if held else held,

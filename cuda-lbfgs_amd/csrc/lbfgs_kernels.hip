@@ -584,7 +584,7 @@ const lbk_geo* lbk_geometry(const lbk_ctx* c) { return &c->geo; }
 const char* lbk_last_error(const lbk_ctx* c) { return c ? c->err : "no context"; }
 
 // Vector allocation (LBFGS_VEC_ALLOC, read at context creation):
-//   pool (default)  vectors of 64 MiB .. 8 GiB are physically contiguous allocations
+//   pool (default)  vectors of 64 MiB .. 2 GiB are physically contiguous allocations
 //                   (hipDeviceMallocContiguous) that are never returned to the driver: a freed one
 //                   goes to a process-wide pool and the next vector of the same size and device takes
 //                   it (at most LBFGS_VEC_POOL_GB = 32 GiB held per process, then plain); other
@@ -598,7 +598,9 @@ const char* lbk_last_error(const lbk_ctx* c) { return c ? c->err : "no context";
 // tools/repeat_stress.py (profiles/r06/alloc_reuse/) found wrong results in the first solve of
 // contexts created after contiguous vectors had been freed - 131 of 200 when only the destroyed
 // contexts' vectors were contiguous, 50 of 200 the other way round (the freed ones contiguous, the
-// failing new ones plain), 0 of 400 with plain allocations throughout. The pool never frees one.
+// failing new ones plain), 0 of 400 with plain allocations throughout. The pool never frees one:
+// 0 of 900 with every vector pooled (LBFGS_VEC_POOL_MIN_MB=0), and 88.0 / 88.3 it/s against plain
+// 86.8 / 86.8 alternating at n = 1e8 (profiles/r06/pool/).
 namespace {
 struct VecPool {
     std::mutex mu;
@@ -610,7 +612,7 @@ VecPool& vec_pool() {
     static VecPool* p = new VecPool();  // never destroyed: its memory is never given back
     return *p;
 }
-constexpr size_t kPoolMax = size_t(8) << 30;
+constexpr size_t kPoolMax = size_t(2) << 30;
 }  // namespace
 
 double* lbk_vec_alloc(lbk_ctx* c) {

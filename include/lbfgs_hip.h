@@ -252,7 +252,7 @@ int lbfgs_coop_info(const lbfgs_ctx* ctx, int* coop_max, int* search_max, int* f
  * *waits = waits completed, *adaptive = the mode. */
 int lbfgs_wait_stats(const lbfgs_ctx* ctx, double* slept_s, uint64_t* waits, int* adaptive);
 /* Vector allocation (LBFGS_VEC_ALLOC at context creation): by default ("pool") every
- * n-vector of 64 MiB .. 8 GiB is a physically contiguous device allocation (+3 % at n = 1e8) that is
+ * n-vector of 64 MiB .. 2 GiB is a physically contiguous device allocation (+3 % at n = 1e8) that is
  * never returned to the driver - a freed one waits in a process-wide pool (at most LBFGS_VEC_POOL_GB,
  * 32 GiB) for the next vector of its size - because freeing contiguous allocations corrupts later
  * ones on this ROCm stack; other sizes, "plain", and the pool's overflow are plain hipMalloc;
