@@ -1,11 +1,13 @@
 """Contexts created after others were destroyed give the same bits (round 6).
 
-With one physically contiguous allocation per vector (now opt-in, LBFGS_VEC_ALLOC=contiguous),
+With physically contiguous vectors freed back to the driver (LBFGS_VEC_ALLOC=contiguous, A/B only),
 tools/repeat_stress.py found the emulated 4-rank vector-free solve's f(x0) / |g(x0)| wrong right
 after a context of n = 300,007 had been solved and destroyed (99 of 400 repetitions), and never
-with plain allocations (profiles/r06/alloc_reuse/). This runs that sequence with the
-shipped allocation: a small context solved and destroyed, then four emulated ranks, each of their
-trajectories bit-identical to the one-rank run, four times over.
+with plain allocations (profiles/r06/alloc_reuse/). The shipped allocation pools
+contiguous vectors and never frees them. This runs that sequence - a small context solved and
+destroyed, then four emulated ranks, each trajectory bit-identical to the one-rank run, four times
+over - with the default allocation (these sizes are below the pool's 64 MiB: plain) and with every
+vector pooled (LBFGS_VEC_POOL_MIN_MB=0), which makes each context reuse the previous ones' vectors.
 """
 import os
 import sys
@@ -24,8 +26,12 @@ def bits(a):
     return np.asarray(a, dtype=np.float64).view(np.uint64)
 
 
-def test_vectors_freed_then_reallocated_give_the_same_bits(monkeypatch):
+@pytest.mark.parametrize("pool_all", [False, True])
+def test_vectors_freed_then_reallocated_give_the_same_bits(monkeypatch, pool_all):
     monkeypatch.setenv("LBFGS_TICKET", "0")
+    monkeypatch.delenv("LBFGS_VEC_ALLOC", raising=False)
+    if pool_all:
+        monkeypatch.setenv("LBFGS_VEC_POOL_MIN_MB", "0")
     n, m, iters = 4_000_003, 5, 12
     x0 = L.x0_uniform(n, 42, -2.0, 2.0)
     with L.Context(n, m) as c:
@@ -49,10 +55,14 @@ def test_vectors_freed_then_reallocated_give_the_same_bits(monkeypatch):
             t.start()
         for t in th:
             t.join(timeout=300)
+        modes = [c.vector_pool for c in ctxs]
         for c in ctxs:
             c.close()
         grp.close()
         assert not any(err), err
+        assert all(md[0] == "pool" for md in modes), modes
+        if pool_all:  # every vector came from (or went into) the pool
+            assert all(md[1] > 0 for md in modes), modes
         for r in range(4):
             for key in ("tr_f", "tr_gnorm", "tr_alpha"):
                 assert np.array_equal(bits(out[r][key]), bits(ref[key])), (rep, r, key)
