@@ -139,6 +139,17 @@ d = json.load(open('$O/poolab_${v}_$r.json'))
 print('$v', '$r', d['value'], d['roofline']['avg_launch_us'], d['box_copy_tbps'], d['vectors'])" | tee -a $O/poolab.txt
             done
         done ;;
+    vfpool)  # the vector-free line with pooled against plain vectors, alternating
+        for r in 1 2; do
+            for v in pool plain; do
+                LBFGS_VEC_ALLOC=$v timeout -k 10 300 python bench.py --vector-free --steps 100 --warmup 20 \
+                    --no-cpu-baseline --no-persistent > $O/vfpool_${v}_$r.json 2> $O/vfpool_${v}_$r.err || exit 1
+                python -c "
+import json
+d = json.load(open('$O/vfpool_${v}_$r.json'))
+print('$v', '$r', d['value'], d['roofline']['avg_launch_us'], d['box_copy_tbps'])" | tee -a $O/vfpool.txt
+            done
+        done ;;
     vflane)
         timeout -k 10 300 tools/vflaneprobe 1e8 9 > $O/vflaneprobe.txt 2>&1
         rc=$?; echo "vflane rc=$rc"; cat $O/vflaneprobe.txt; exit $rc ;;
