@@ -150,6 +150,24 @@ d = json.load(open('$O/vfpool_${v}_$r.json'))
 print('$v', '$r', d['value'], d['roofline']['avg_launch_us'], d['box_copy_tbps'])" | tee -a $O/vfpool.txt
             done
         done ;;
+    midn)  # mid n on the final library: collect against the reduce kernel, alternating, and a trace
+        for r in 1 2; do
+            for n in 2.5e6 5e6; do
+                for col in 0 1; do
+                    LBFGS_COLLECT=$col timeout -k 10 200 python bench.py --size $n --steps 400 --warmup 40 \
+                        --no-cpu-baseline --no-vector-free --no-persistent --no-box-probe \
+                        > $O/midn_${n}_c${col}_$r.json 2> $O/midn_${n}_c${col}_$r.err || exit 1
+                    python -c "
+import json
+d = json.load(open('$O/midn_${n}_c${col}_$r.json'))
+print('$n', 'collect=$col', '$r', d['value'], d['ms_per_step'], d['roofline']['kernel_share'])" | tee -a $O/midn.txt
+                done
+            done
+        done
+        timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/midn_trace -o run --output-format csv -- \
+            python3 bench.py --size 2.5e6 --steps 200 --warmup 20 --no-cpu-baseline --no-vector-free --no-persistent \
+            --no-box-probe --no-prof > $O/midn_trace.log 2>&1
+        rc=$?; echo "midn trace rc=$rc"; exit $rc ;;
     vflane)
         timeout -k 10 300 tools/vflaneprobe 1e8 9 > $O/vflaneprobe.txt 2>&1
         rc=$?; echo "vflane rc=$rc"; cat $O/vflaneprobe.txt; exit $rc ;;
