@@ -168,6 +168,14 @@ print('$n', 'collect=$col', '$r', d['value'], d['ms_per_step'], d['roofline']['k
             python3 bench.py --size 2.5e6 --steps 200 --warmup 20 --no-cpu-baseline --no-vector-free --no-persistent \
             --no-box-probe --no-prof > $O/midn_trace.log 2>&1
         rc=$?; echo "midn trace rc=$rc"; exit $rc ;;
+    stressbig)  # the stress at 10x sizes (churn 0.65-10 M, 4 ranks of 1e7: pooled vectors), default
+        # allocation, then freed-contiguous as the positive control
+        for md in default contiguous; do
+            LBFGS_VEC_ALLOC=$([ $md = default ] && echo pool || echo contiguous) timeout -k 10 400 python -u \
+                tools/repeat_stress.py $O/stressbig_$md.json ${2:-120} small,churn,vf4 default,default 10 \
+                > $O/stressbig_$md.log 2>&1
+            rc=$?; echo "stressbig $md rc=$rc"; tail -1 $O/stressbig_$md.log; [ $rc -eq 0 ] || exit $rc
+        done ;;
     vflane)
         timeout -k 10 300 tools/vflaneprobe 1e8 9 > $O/vflaneprobe.txt 2>&1
         rc=$?; echo "vflane rc=$rc"; cat $O/vflaneprobe.txt; exit $rc ;;

@@ -13,9 +13,11 @@ Kinds, interleaved every repetition:
           one-rank vector-free run
 The environment (LBFGS_VEC_ALLOC=plain, ...) selects the library's mode; no oracle is used.
 
-usage: python tools/repeat_stress.py out.json [reps] [kinds] [churn_alloc,vf_alloc]
+usage: python tools/repeat_stress.py out.json [reps] [kinds] [churn_alloc,vf_alloc] [scale]
   (the last argument sets LBFGS_VEC_ALLOC for the churn contexts and for the 4-rank contexts
-  separately, e.g. "contiguous,plain": which side's allocations matter)
+  separately, e.g. "contiguous,plain": which side's allocations matter; "default,default" leaves
+  the environment alone; scale multiplies the churn and 4-rank sizes, e.g. 10 puts them in the
+  pool's 64 MiB+ range)
 """
 import json
 import os
@@ -92,22 +94,24 @@ def main():
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
     kinds = sys.argv[3].split(",") if len(sys.argv) > 3 else ["small", "churn", "vf4"]
     modes = sys.argv[4].split(",") if len(sys.argv) > 4 else [None, None]
+    modes = [None if md == "default" else md for md in modes]
+    scale = int(sys.argv[5]) if len(sys.argv) > 5 else 1
     env = {k: v for k, v in os.environ.items() if k.startswith("LBFGS_")}
-    res = {"env": env, "reps": reps, "kinds": kinds, "alloc_modes": modes, "fail": {k: 0 for k in kinds}, "runs": {k: 0 for k in kinds},
+    res = {"env": env, "reps": reps, "kinds": kinds, "alloc_modes": modes, "scale": scale, "fail": {k: 0 for k in kinds}, "runs": {k: 0 for k in kinds},
            "failures": [], "build": L.build_info()[0]}
     t0 = time.time()
     n_s, m_s = 4097, 7
     x_s = L.x0_uniform(n_s, 7, -2.0, 2.0)
     cs = L.Context(n_s, m_s)
     ref_s = cs.minimize("rosenbrock", x_s, "interpolation", 150, tolerance=1e-5, trace=True)
-    n_v, m_v, it_v = 4_000_003, 5, 12
+    n_v, m_v, it_v = 4_000_003 * scale, 5, 12
     x_v = L.x0_uniform(n_v, 42, -2.0, 2.0)
     ref_v = None
     if "vf4" in kinds:
         os.environ["LBFGS_TICKET"] = "0"
         with L.Context(n_v, m_v) as c:
             ref_v = c.minimize("rosenbrock", x_v, "backtracking", it_v, trace=True, vector_free=True)
-    sizes = [100_003, 1_000_003, 65_537, 300_007]
+    sizes = [k * scale for k in (100_003, 1_000_003, 65_537, 300_007)]
     for rep in range(reps):
         if "small" in kinds:
             r = cs.minimize("rosenbrock", x_s, "interpolation", 150, tolerance=1e-5, trace=True)
