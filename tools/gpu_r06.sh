@@ -176,6 +176,21 @@ print('$n', 'collect=$col', '$r', d['value'], d['ms_per_step'], d['roofline']['k
                 > $O/stressbig_$md.log 2>&1
             rc=$?; echo "stressbig $md rc=$rc"; tail -1 $O/stressbig_$md.log; [ $rc -eq 0 ] || exit $rc
         done ;;
+    persistab)  # the persistent two-loop (noinline passes): 4 waves (shipped) / 6 / 8 per SIMD
+        for r in 1 2; do
+            for v in base pw6 pw8; do
+                lib=cuda-lbfgs_amd/liblbfgs_hip.so; wg=4
+                [ $v = pw6 ] && lib=cuda-lbfgs_amd/liblbfgs_hip_pw6.so && wg=6
+                [ $v = pw8 ] && lib=cuda-lbfgs_amd/liblbfgs_hip_pw8.so && wg=8
+                LBFGS_LIB=$lib LBFGS_PERSIST_WG=$wg timeout -k 10 300 python bench.py --steps 100 --warmup 20 \
+                    --no-cpu-baseline --no-vector-free > $O/persistab_${v}_$r.json 2> $O/persistab_${v}_$r.err || exit 1
+                python -c "
+import json
+d = json.load(open('$O/persistab_${v}_$r.json'))
+p = d['persistent']
+print('$v', '$r', d['value'], p['value'], p['vs_default'], p['trajectory_bit_identical_to_default'], p['roofline']['avg_launch_us'])" | tee -a $O/persistab.txt
+            done
+        done ;;
     vflane)
         timeout -k 10 300 tools/vflaneprobe 1e8 9 > $O/vflaneprobe.txt 2>&1
         rc=$?; echo "vflane rc=$rc"; cat $O/vflaneprobe.txt; exit $rc ;;
