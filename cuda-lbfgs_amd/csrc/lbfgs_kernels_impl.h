@@ -2622,6 +2622,11 @@ __global__ __launch_bounds__(LB_BLOCK) void k_coop_search(SmallArgs a, Geo geo, 
 // counter round trip plus one flagged hop per pass.
 // ---------------------------------------------------------------------------------------
 __device__ __forceinline__ int64_t ceil_pos(int64_t x, int64_t y) { return x <= 0 ? 0 : (x + y - 1) / y; }
+// persist_pass: one workgroup barrier per pass instead of two per owned segment (A/B: -DLBK_PERSIST_SEGBAR=1)
+#ifndef LBK_PERSIST_SEGBAR
+#define LBK_PERSIST_SEGBAR 0
+#endif
+constexpr int kPersistSegMax = 64;
 
 template <int K, bool HALO, class Op>
 __device__ __forceinline__ void persist_pass(const Op& op, const Geo& geo, const SmallArgs& a, int pass, double* slot,
@@ -2636,6 +2641,11 @@ __device__ __forceinline__ void persist_pass(const Op& op, const Geo& geo, const
     const unsigned seq = a.seq_base + (unsigned)pass + 1u;
     const bool down = (seq & 1u) != 0 && a.alt;
     unsigned long long* P = a.ll + (size_t)(pass & 1) * LBK_LL_COMPS * LBK_LL_SEGS * 2;
+    // a single-component pass without halos or edges: each wave keeps its segment sums in LDS and
+    // the workgroup meets once after all its segments, instead of twice per segment (the waves read
+    // back only rows they wrote themselves); the same partials, the same bits
+    __shared__ double segp[kPersistSegMax][4];
+    const bool one_bar = !LBK_PERSIST_SEGBAR && K == 1 && !HALO && rvec == nullptr && cnt <= kPersistSegMax;
     for (int64_t k = 0; k < cnt; ++k) {
         const int64_t kk = down ? cnt - 1 - k : k;
         const int64_t sidx = a.spw > 0 ? c0 + kk : b + kk * G;
@@ -2647,6 +2657,11 @@ __device__ __forceinline__ void persist_pass(const Op& op, const Geo& geo, const
             stream_halo(op, s, geo, acc);
         else
             stream(op, s, geo, acc);
+        if (one_bar) {
+            const double v = wave_sum(acc[0]);
+            if (lane == 0) segp[kk][w] = v;
+            continue;
+        }
 #pragma unroll
         for (int k2 = 0; k2 < K; ++k2) {
             const double v = wave_sum(acc[k2]);
@@ -2669,6 +2684,15 @@ __device__ __forceinline__ void persist_pass(const Op& op, const Geo& geo, const
             }
         }
         __syncthreads();  // lds reuse
+    }
+    if (one_bar) {
+        __syncthreads();
+        if (t < cnt) {  // (cnt <= 64: wave 0)
+            const int64_t sidx = a.spw > 0 ? c0 + t : b + (int64_t)t * G;
+            __hip_atomic_store(reinterpret_cast<unsigned long long*>(a.partials + sidx),
+                               dbits((segp[t][0] + segp[t][1]) + (segp[t][2] + segp[t][3])), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
     // wave 0 stored the partials: drained before its counter adds
     if (t < 64) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -191,6 +191,21 @@ p = d['persistent']
 print('$v', '$r', d['value'], p['value'], p['vs_default'], p['trajectory_bit_identical_to_default'], p['roofline']['avg_launch_us'])" | tee -a $O/persistab.txt
             done
         done ;;
+    segbarab)  # the persistent two-loop with one barrier per pass (shipped candidate) against two per segment
+        bash $0 tests tests/test_gpu_persist.py "tests/test_gpu_fullsize.py::test_fullsize_parity" || exit 1
+        for r in 1 2; do
+            for v in onebar segbar; do
+                lib=cuda-lbfgs_amd/liblbfgs_hip.so
+                [ $v = segbar ] && lib=cuda-lbfgs_amd/liblbfgs_hip_segbar.so
+                LBFGS_LIB=$lib timeout -k 10 300 python bench.py --steps 100 --warmup 20 --no-cpu-baseline \
+                    --no-vector-free > $O/segbar_${v}_$r.json 2> $O/segbar_${v}_$r.err || exit 1
+                python -c "
+import json
+d = json.load(open('$O/segbar_${v}_$r.json'))
+p = d['persistent']
+print('$v', '$r', d['value'], p['value'], p['vs_default'], p['trajectory_bit_identical_to_default'], p['roofline']['avg_launch_us'])" | tee -a $O/segbar.txt
+            done
+        done ;;
     vflane)
         timeout -k 10 300 tools/vflaneprobe 1e8 9 > $O/vflaneprobe.txt 2>&1
         rc=$?; echo "vflane rc=$rc"; cat $O/vflaneprobe.txt; exit $rc ;;
