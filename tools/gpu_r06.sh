@@ -206,6 +206,11 @@ p = d['persistent']
 print('$v', '$r', d['value'], p['value'], p['vs_default'], p['trajectory_bit_identical_to_default'], p['roofline']['avg_launch_us'])" | tee -a $O/segbar.txt
             done
         done ;;
+    persisttrace)  # kernel trace of the persistent mode's timed steps (LBFGS_PERSIST=2 as the headline mode)
+        LBFGS_PERSIST=2 timeout -k 10 300 rocprofv3 --kernel-trace -d $O/persist_trace -o run --output-format csv -- \
+            python3 bench.py --steps 30 --warmup 10 --no-cpu-baseline --no-prof --no-box-probe --no-vector-free \
+            --no-persistent > $O/persist_trace.log 2>&1
+        rc=$?; echo "persist trace rc=$rc"; tail -1 $O/persist_trace.log | cut -c1-200; exit $rc ;;
     vflane)
         timeout -k 10 300 tools/vflaneprobe 1e8 9 > $O/vflaneprobe.txt 2>&1
         rc=$?; echo "vflane rc=$rc"; cat $O/vflaneprobe.txt; exit $rc ;;
