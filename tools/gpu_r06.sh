@@ -211,6 +211,20 @@ print('$v', '$r', d['value'], p['value'], p['vs_default'], p['trajectory_bit_ide
             python3 bench.py --steps 30 --warmup 10 --no-cpu-baseline --no-prof --no-box-probe --no-vector-free \
             --no-persistent > $O/persist_trace.log 2>&1
         rc=$?; echo "persist trace rc=$rc"; tail -1 $O/persist_trace.log | cut -c1-200; exit $rc ;;
+    strideab)  # persistent ownership: contiguous chunks (shipped) against strided segments (variant)
+        for r in 1 2; do
+            for v in chunk stride; do
+                lib=cuda-lbfgs_amd/liblbfgs_hip.so
+                [ $v = stride ] && lib=cuda-lbfgs_amd/liblbfgs_hip_stride.so
+                LBFGS_LIB=$lib timeout -k 10 300 python bench.py --steps 100 --warmup 20 --no-cpu-baseline \
+                    --no-vector-free > $O/stride_${v}_$r.json 2> $O/stride_${v}_$r.err || exit 1
+                python -c "
+import json
+d = json.load(open('$O/stride_${v}_$r.json'))
+p = d['persistent']
+print('$v', '$r', d['value'], p['value'], p['vs_default'], p['trajectory_bit_identical_to_default'], p['roofline']['avg_launch_us'])" | tee -a $O/stride.txt
+            done
+        done ;;
     vflane)
         timeout -k 10 300 tools/vflaneprobe 1e8 9 > $O/vflaneprobe.txt 2>&1
         rc=$?; echo "vflane rc=$rc"; cat $O/vflaneprobe.txt; exit $rc ;;
